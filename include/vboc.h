@@ -1,0 +1,118 @@
+/*
+ * vboc.h - C ABI of the MI355X-native batched VBOC boundary-OCP solver (libvboc_amd.so).
+ *
+ * Plain pointers and sizes only (no torch / HIP types in the signatures; streams are passed as
+ * void* = hipStream_t, NULL = default stream).  One handle <-> one device; not thread-safe.
+ *
+ * What each entry point replaces (the reference binds ACADOS's generated C solver through
+ * acados_template's ctypes wrapper; every call below is a batched version of that path):
+ *
+ *   vboc_create            <- AcadosOcpSolver(self.ocp, json_file=...)
+ *                             VBOC/triplependulum_class_vboc.py:153 (double :181, pendulum :105)
+ *   vboc_set_option        <- ocp.solver_options.* (nlp_solver_tol_stat, qp_solver_iter_max,
+ *                             levenberg_marquardt, alpha_min, alpha_reduction, nlp_solver_max_iter)
+ *                             VBOC/triplependulum_class_vboc.py:129-141
+ *   vboc_solve_batch       <- one OCPtriplependulumINIT.OCP_solve(...) per problem:
+ *                             reset/set/constraints_set/solve, VBOC/triplependulum_class_vboc.py:155-191
+ *                             (called from VBOC/triplependulum_vboc.py:110,262 and
+ *                             triplependulum_testdata.py:44-75); results = ocp_solver.get(i,'x'|'u'),
+ *                             get_cost(), solve() status (:115,126-129,189)
+ *   vboc_rk4_batch         <- SYMtriplependulumINIT().acados_integrator set('x','u','T')/solve()/get('x')
+ *                             VBOC/triplependulum_class_vboc.py:235-239, VBOC/triplependulum_vboc.py:346-353
+ *   vboc_destroy           <- solver object destruction (acados_template __del__ -> free)
+ *   vboc_last_error        <- Python exceptions raised by acados_template on bad fields
+ *
+ * Problem layout (problem-major, exactly the numpy arrays the reference passes, float64):
+ *   nq = number of links (1 pendulum, 2 double, 3 triple); nx = 2*nq+1 (theta, dtheta, dt);
+ *   nu = nq; np = nq+1 (w_1..w_nq, w_t).
+ *   N[b]                 horizon of problem b (<= nmax of the handle)
+ *   x_guess[b][nmax+1][nx]  stage guesses; row N[b] is the stage-N guess (OCP_solve sets it from
+ *                        x_sol_guess[-1], triplependulum_class_vboc.py:185)
+ *   u_guess[b][nmax][nu]
+ *   p[b][np]             cost parameters (stage-0 cost w.dtheta + wt.dt, :85-86)
+ *   lbx/ubx[b][nx]       path state bounds q_lb/q_ub       (:165-166)
+ *   lbu/ubu[b][nu]       control bounds u_lb/u_ub          (:167-168)
+ *   lbx_0/ubx_0[b][nx]   stage-0 bounds q_init_lb/ub       (:180-181)
+ *   lbx_e/ubx_e[b][nx]   terminal bounds q_fin_lb/ub       (:183-184)
+ *   The stage-0 general constraint C = [0 | I - d d^T | 0], d = p[:nq], lg = ug = 0 (:174-178) is
+ *   implied (as in OCP_solve).  Requirements (checked, VBOC_ERR_UNSUPPORTED otherwise): dt fixed
+ *   (lb == ub on the dt column everywhere), stage-0 positions fixed, terminal velocities fixed.
+ * Outputs:
+ *   status[b]            0 success, 1 NaN, 2 max iter, 4 QP failure (ACADOS codes)
+ *   x_out[b][nmax+1][nx], u_out[b][nmax][nu]  solution (rows beyond N[b] untouched)
+ *   cost[b]              NLP cost at the solution (= get_cost())
+ *   sqp_iter[b], qp_iter[b]  iteration counters (qp_iter summed over SQP iterations)
+ *
+ * Return value of every call: 0 on success, a negative VBOC_ERR_* code otherwise; the message is
+ * available from vboc_last_error().
+ */
+#ifndef VBOC_H
+#define VBOC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VBOC_OK 0
+#define VBOC_ERR_ARG (-1)
+#define VBOC_ERR_HIP (-2)
+#define VBOC_ERR_UNSUPPORTED (-3)
+#define VBOC_ERR_NOMEM (-4)
+
+typedef struct vboc_solver* vboc_handle;
+
+typedef struct {
+  int B;                 /* number of problems */
+  int nmax;              /* leading horizon dimension of x_guess/u_guess/x_out/u_out */
+  const int* N;
+  const double* x_guess;
+  const double* u_guess;
+  const double* p;
+  const double* lbx;
+  const double* ubx;
+  const double* lbu;
+  const double* ubu;
+  const double* lbx_0;
+  const double* ubx_0;
+  const double* lbx_e;
+  const double* ubx_e;
+  int* status;
+  double* x_out;
+  double* u_out;
+  double* cost;
+  int* sqp_iter;
+  int* qp_iter;
+} vboc_batch_t;
+
+/* Create a solver for nq links with horizons up to nmax on HIP device `device`.  `slots` is the
+ * number of concurrently resident problems (lanes) of the persistent kernel; 0 = default. */
+int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out);
+int vboc_destroy(vboc_handle h);
+
+/* Solver options (names of AcadosOcpOptions): "nlp_solver_tol_stat", "nlp_solver_tol_eq",
+ * "nlp_solver_tol_ineq", "nlp_solver_tol_comp", "nlp_solver_max_iter", "qp_solver_iter_max",
+ * "qp_solver_tol_stat", "qp_solver_tol_eq", "qp_solver_tol_comp", "levenberg_marquardt",
+ * "alpha_min", "alpha_reduction"; interior-point internals "ipm_mu0", "ipm_push", "ipm_tau". */
+int vboc_set_option(vboc_handle h, const char* field, double value);
+int vboc_get_option(vboc_handle h, const char* field, double* value);
+
+/* Batched solve, every pointer a DEVICE pointer (inputs resident in HBM); asynchronous on stream. */
+int vboc_solve_batch(vboc_handle h, const vboc_batch_t* batch, void* stream);
+/* Same with HOST pointers: staged through the handle's device buffers; synchronous. */
+int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* batch);
+
+/* Twin integrator: one ERK4 step of length T of the unscaled 2nq-state model for B states.
+ * x[B][2nq], u[B][nq] -> x_out[B][2nq].  Device pointers (async) / host pointers (sync). */
+int vboc_rk4_batch(int nq, int B, double T, const double* x, const double* u, double* x_out, void* stream);
+int vboc_rk4_batch_host(int nq, int B, double T, const double* x, const double* u, double* x_out);
+
+/* Device time of the last vboc_solve_batch* call's solver kernel in milliseconds (HIP events on
+ * the call's stream) and the number of kernel launches it used. */
+int vboc_last_kernel_ms(vboc_handle h, double* ms, int* launches);
+
+const char* vboc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VBOC_H */

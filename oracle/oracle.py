@@ -1,0 +1,102 @@
+"""ORACLE - TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of the plain-C FP64 restatement (oracle/vboc_oracle.c).  Importable by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg only; the product package vboc_amd never
+imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libvboc_oracle.so")
+
+
+class Opts(ctypes.Structure):
+    _fields_ = [("tol_stat", ctypes.c_double), ("tol_eq", ctypes.c_double),
+                ("tol_ineq", ctypes.c_double), ("tol_comp", ctypes.c_double),
+                ("max_iter", ctypes.c_int), ("qp_max_iter", ctypes.c_int),
+                ("alpha_min", ctypes.c_double), ("alpha_reduction", ctypes.c_double),
+                ("lm", ctypes.c_double), ("mu0", ctypes.c_double), ("ipm_push", ctypes.c_double),
+                ("ipm_tau", ctypes.c_double), ("qp_tol_stat", ctypes.c_double),
+                ("qp_tol_eq", ctypes.c_double), ("qp_tol_comp", ctypes.c_double)]
+
+
+RESULT_DTYPE = np.dtype([("status", "i4"), ("sqp_iter", "i4"), ("qp_iter", "i4"), ("pad", "i4"),
+                         ("cost", "f8"), ("res_stat", "f8"), ("res_eq", "f8"), ("res_ineq", "f8"),
+                         ("res_comp", "f8")])
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = ctypes.CDLL(LIB)
+        dp = ctypes.POINTER(ctypes.c_double)
+        _lib.vboc_oracle_solve_batch.restype = ctypes.c_int
+    return _lib
+
+
+def default_opts(**kw):
+    o = Opts()
+    lib().vboc_oracle_default_opts(ctypes.byref(o))
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def model(nq, th, om, u):
+    th, om, u = (np.ascontiguousarray(a, dtype=np.float64) for a in (th, om, u))
+    acc = np.zeros(nq)
+    Jth, Jom, Ju = np.zeros((nq, nq)), np.zeros((nq, nq)), np.zeros((nq, nq))
+    lib().vboc_oracle_model(nq, _p(th), _p(om), _p(u), _p(acc), _p(Jth), _p(Jom), _p(Ju))
+    return acc, Jth, Jom, Ju
+
+
+def rk4(nq, h, x, u):
+    x, u = (np.ascontiguousarray(a, dtype=np.float64) for a in (x, u))
+    x1 = np.zeros(2 * nq)
+    lib().vboc_oracle_rk4(nq, ctypes.c_double(h), _p(x), _p(u), _p(x1))
+    return x1
+
+
+def rk4_sens(nq, h, x, u):
+    x, u = (np.ascontiguousarray(a, dtype=np.float64) for a in (x, u))
+    x1, A, B = np.zeros(2 * nq), np.zeros((2 * nq, 2 * nq)), np.zeros((2 * nq, nq))
+    lib().vboc_oracle_rk4_sens(nq, ctypes.c_double(h), _p(x), _p(u), _p(x1), _p(A), _p(B))
+    return x1, A, B
+
+
+def solve_batch(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe, ubxe,
+                opts=None, nthreads=None):
+    """Problem-major batch in the reference layout (see vboc_oracle.c).  Returns
+    (x_out, u_out, results)."""
+    N = np.ascontiguousarray(N, dtype=np.int32)
+    B = N.shape[0]
+    arrs = [np.ascontiguousarray(a, dtype=np.float64)
+            for a in (x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe, ubxe)]
+    Nmax = arrs[0].shape[1] - 1
+    assert arrs[1].shape[1] == Nmax
+    x_out = np.zeros_like(arrs[0])
+    u_out = np.zeros_like(arrs[1])
+    res = np.zeros(B, dtype=RESULT_DTYPE)
+    o = opts if opts is not None else default_opts()
+    nthreads = nthreads or os.cpu_count()
+    rc = lib().vboc_oracle_solve_batch(nq, B, Nmax, _p(N), *[_p(a) for a in arrs], ctypes.byref(o),
+                                       int(nthreads), _p(x_out), _p(u_out), _p(res))
+    if rc != 0:
+        raise RuntimeError(f"oracle solve_batch failed rc={rc}")
+    return x_out, u_out, res

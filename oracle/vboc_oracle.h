@@ -1,0 +1,39 @@
+/* ORACLE - TEST INFRASTRUCTURE ONLY (see vboc_oracle.c header). */
+#ifndef VBOC_ORACLE_H
+#define VBOC_ORACLE_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  double tol_stat, tol_eq, tol_ineq, tol_comp;
+  int max_iter, qp_max_iter;
+  double alpha_min, alpha_reduction, lm;
+  double mu0, ipm_push, ipm_tau;
+  double qp_tol_stat, qp_tol_eq, qp_tol_comp;
+} vboc_opts_t;
+
+typedef struct {
+  int status, sqp_iter, qp_iter, pad;
+  double cost, res_stat, res_eq, res_ineq, res_comp;
+} vboc_result_t;
+
+void vboc_oracle_default_opts(vboc_opts_t* o);
+void vboc_oracle_model(int nq, const double* th, const double* om, const double* u, double* acc,
+                       double* Jth, double* Jom, double* Ju);
+void vboc_oracle_rk4(int nq, double h, const double* x, const double* u, double* x1);
+void vboc_oracle_rk4_sens(int nq, double h, const double* x, const double* u, double* x1, double* A,
+                          double* B);
+int vboc_oracle_solve(int nq, int N, const double* x_guess, const double* u_guess, const double* p,
+                      const double* lbx, const double* ubx, const double* lbu, const double* ubu,
+                      const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
+                      const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res);
+int vboc_oracle_solve_batch(int nq, int B, int Nmax, const int* N, const double* x_guess,
+                            const double* u_guess, const double* p, const double* lbx, const double* ubx,
+                            const double* lbu, const double* ubu, const double* lbx0, const double* ubx0,
+                            const double* lbxe, const double* ubxe, const vboc_opts_t* opts, int nthreads,
+                            double* x_out, double* u_out, vboc_result_t* res);
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,256 @@
+// model.h - N-link pendulum dynamics, analytic Jacobians and ERK4 (+ forward sensitivities) for
+// gfx950.  Device-only; one lane evaluates one problem's stage, everything in registers.
+//
+// Physics (same function as the reference's CasADi f_expl, pinned by tests/golden/dynamics_*.npz):
+//  * nq = 2, 3: point-mass chain, mass m_i = 0.4 at the tip of massless link l_i = 0.8, absolute
+//    angles from the downward vertical, generalised forces C_i on the angles
+//      M(th) acc = u - cor(th, om) - grav(th),  M_jk = a_jk cos(th_j - th_k),
+//      cor_j = sum_k a_jk sin(th_j - th_k) om_k^2,  grav_j = g mu_j l_j sin th_j,
+//      mu_j = sum_{i>=j} m_i,  a_jk = mu_max(j,k) l_j l_k
+//    (VBOC/doublependulum_class_vboc.py:14-91, VBOC/triplependulum_class_vboc.py:15-58).
+//  * nq = 1: damped pendulum acc = (m g d sin th + F - b om) / (d^2 m), m=0.5, d=0.3, b=0.01
+//    (VBOC/pendulum_class_vboc.py:14-39).
+// The dt state of the reference (f = dt * f_phys, RK4 with h = 1, tf = N) is folded into the
+// step length h = dt (exact: the dt state has zero derivative and is pinned by the bounds).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace vboc {
+
+template <int NQ>
+struct Dim {
+  static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1;
+};
+
+template <int NQ>
+struct Chain {
+  static constexpr double g = 9.81, m = 0.4, l = 0.8;
+  __device__ __forceinline__ static constexpr double mu(int j) { return m * (NQ - j); }
+  __device__ __forceinline__ static constexpr double a(int j, int k) { return mu(j > k ? j : k) * l * l; }
+};
+
+// Cholesky of a small SPD matrix held in registers (row-major, lower factor in place).
+// Returns false on a non-positive pivot.
+template <int n>
+__device__ __forceinline__ bool chol(double (&A)[n * n]) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < n; ++j) {
+    double s = A[j * n + j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) s -= A[j * n + k] * A[j * n + k];
+    ok = ok && (s > 0.0);
+    const double d = sqrt(s > 0.0 ? s : 1.0);
+    const double inv = 1.0 / d;
+    A[j * n + j] = d;
+#pragma unroll
+    for (int i = j + 1; i < n; ++i) {
+      double t = A[i * n + j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) t -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = t * inv;
+    }
+  }
+  return ok;
+}
+
+template <int n>
+__device__ __forceinline__ void chol_solve(const double (&L)[n * n], double (&b)[n]) {
+#pragma unroll
+  for (int i = 0; i < n; ++i) {
+    double t = b[i];
+#pragma unroll
+    for (int k = 0; k < i; ++k) t -= L[i * n + k] * b[k];
+    b[i] = t / L[i * n + i];
+  }
+#pragma unroll
+  for (int i = n - 1; i >= 0; --i) {
+    double t = b[i];
+#pragma unroll
+    for (int k = i + 1; k < n; ++k) t -= L[k * n + i] * b[k];
+    b[i] = t / L[i * n + i];
+  }
+}
+
+// acc = f(th, om, u); if JAC also Jth, Jom, Ju (row-major NQ x NQ).
+template <int NQ, bool JAC>
+__device__ __forceinline__ void model_eval(const double* th, const double* om, const double* u, double* acc,
+                                           double* Jth, double* Jom, double* Ju) {
+  if constexpr (NQ == 1) {
+    constexpr double pm = 0.5, pd = 0.3, pb = 0.01, g = 9.81;
+    constexpr double inv = 1.0 / (pd * pd * pm);
+    double sn, cs;
+    sincos(th[0], &sn, &cs);
+    acc[0] = (pm * g * pd * sn + u[0] - pb * om[0]) * inv;
+    if constexpr (JAC) {
+      Jth[0] = pm * g * pd * cs * inv;
+      Jom[0] = -pb * inv;
+      Ju[0] = inv;
+    }
+  } else {
+    using C = Chain<NQ>;
+    double S[NQ][NQ], Cc[NQ][NQ], M[NQ * NQ], r[NQ], sth[NQ], cth[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) sincos(th[j], &sth[j], &cth[j]);
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      S[j][j] = 0.0;
+      Cc[j][j] = 1.0;
+#pragma unroll
+      for (int k = 0; k < j; ++k) {
+        // sin/cos of differences from the per-angle values (angle-difference identities)
+        const double s = sth[j] * cth[k] - cth[j] * sth[k];
+        const double c = cth[j] * cth[k] + sth[j] * sth[k];
+        S[j][k] = s; S[k][j] = -s;
+        Cc[j][k] = c; Cc[k][j] = c;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j)
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) M[j * NQ + k] = C::a(j, k) * Cc[j][k];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      double cor = 0.0;
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) cor += C::a(j, k) * S[j][k] * om[k] * om[k];
+      r[j] = u[j] - cor - C::g * C::mu(j) * C::l * sth[j];
+    }
+    chol<NQ>(M);
+    double a_[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) a_[j] = r[j];
+    chol_solve<NQ>(M, a_);
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) acc[j] = a_[j];
+    if constexpr (JAC) {
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) {
+        double col[NQ], co[NQ], e[NQ];
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+          if (j == c) {
+            double diag = 0.0;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k)
+              if (k != j) diag += C::a(j, k) * (Cc[j][k] * om[k] * om[k] - S[j][k] * a_[k]);
+            col[j] = -diag - C::g * C::mu(j) * C::l * cth[j];
+          } else {
+            col[j] = C::a(j, c) * (Cc[j][c] * om[c] * om[c] - S[j][c] * a_[c]);
+          }
+          co[j] = -2.0 * C::a(j, c) * S[j][c] * om[c];
+          e[j] = (j == c) ? 1.0 : 0.0;
+        }
+        chol_solve<NQ>(M, col);
+        chol_solve<NQ>(M, co);
+        chol_solve<NQ>(M, e);
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) {
+          Jth[j * NQ + c] = col[j];
+          Jom[j * NQ + c] = co[j];
+          Ju[j * NQ + c] = e[j];
+        }
+      }
+    }
+  }
+}
+
+template <int NQ>
+__device__ __forceinline__ void rhs(const double* x, const double* u, double* k) {
+#pragma unroll
+  for (int j = 0; j < NQ; ++j) k[j] = x[NQ + j];
+  model_eval<NQ, false>(x, x + NQ, u, k + NQ, nullptr, nullptr, nullptr);
+}
+
+// One classical RK4 step of length h.
+template <int NQ>
+__device__ __forceinline__ void rk4(double h, const double* x, const double* u, double* x1) {
+  constexpr int NX = 2 * NQ;
+  double k[NX], X[NX], acc[NX];
+  rhs<NQ>(x, u, k);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { acc[i] = k[i]; X[i] = x[i] + 0.5 * h * k[i]; }
+  rhs<NQ>(X, u, k);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { acc[i] += 2.0 * k[i]; X[i] = x[i] + 0.5 * h * k[i]; }
+  rhs<NQ>(X, u, k);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) { acc[i] += 2.0 * k[i]; X[i] = x[i] + h * k[i]; }
+  rhs<NQ>(X, u, k);
+#pragma unroll
+  for (int i = 0; i < NX; ++i) x1[i] = x[i] + h / 6.0 * (acc[i] + k[i]);
+}
+
+// RK4 step with forward sensitivities = exact derivative of the discrete map (ACADOS ERK
+// forward VDE).  Sensitivity columns are propagated in groups of NQ directions (theta block,
+// omega block, u block) to bound register pressure; each group re-runs the nominal stages.
+// Outputs x1 (NX); sensitivity entry (i, c), c < NX for A = dx1/dx, c >= NX for B = dx1/du, is
+// handed to store(i, c, value) (the caller writes it straight to its HBM slot).
+template <int NQ, class Store>
+__device__ __forceinline__ void rk4_sens(double h, const double* x, const double* u, double* x1, Store store) {
+  constexpr int NX = 2 * NQ;
+#pragma unroll 1
+  for (int grp = 0; grp < 3; ++grp) {
+    // tangent T (NX x NQ): columns of d X / d (x_grp or u)
+    double T[NX][NQ], Ts[NX][NQ], X[NX], ks[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+      X[i] = x[i];
+      ks[i] = 0.0;
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) {
+        T[i][c] = (grp < 2 && i == grp * NQ + c) ? 1.0 : 0.0;
+        Ts[i][c] = 0.0;
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
+      const double cnext = (st < 2) ? 0.5 * h : h;
+      double k[NX], Jth[NQ * NQ], Jom[NQ * NQ], Ju[NQ * NQ];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j) k[j] = X[NQ + j];
+      model_eval<NQ, true>(X, X + NQ, u, k + NQ, Jth, Jom, Ju);
+      double dk[NX][NQ];
+#pragma unroll
+      for (int j = 0; j < NQ; ++j)
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+          dk[j][c] = T[NQ + j][c];
+          double t = (grp == 2 ? Ju[j * NQ + c] : 0.0);
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) t += Jth[j * NQ + q] * T[q][c] + Jom[j * NQ + q] * T[NQ + q][c];
+          dk[NQ + j][c] = t;
+        }
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        ks[i] += wgt * k[i];
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) Ts[i][c] += wgt * dk[i][c];
+      }
+      if (st < 3) {
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+          X[i] = x[i] + cnext * k[i];
+#pragma unroll
+          for (int c = 0; c < NQ; ++c)
+            T[i][c] = ((grp < 2 && i == grp * NQ + c) ? 1.0 : 0.0) + cnext * dk[i][c];
+        }
+      }
+    }
+    if (grp == 0) {
+#pragma unroll
+      for (int i = 0; i < NX; ++i) x1[i] = x[i] + h / 6.0 * ks[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+#pragma unroll
+      for (int c = 0; c < NQ; ++c) {
+        const double v = ((grp < 2 && i == grp * NQ + c) ? 1.0 : 0.0) + h / 6.0 * Ts[i][c];
+        store(i, grp * NQ + c, v);
+      }
+    }
+  }
+}
+
+}  // namespace vboc

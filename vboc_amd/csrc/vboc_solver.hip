@@ -1,0 +1,1362 @@
+// vboc_solver.hip - MI355X-native batched boundary-OCP solver (the ACADOS SQP/HPIPM path of
+// OCP<sys>INIT.OCP_solve, VBOC/triplependulum_class_vboc.py:155-191, run for a whole batch).
+//
+// Execution model (DESIGN.md "Kernels"):
+//  * one OCP per LANE.  A wave carries 64 independent problems; every per-stage quantity is stored
+//    slot-major SoA in HBM, [stage][field][slot], so the 64 lanes of a wave touch 512 contiguous
+//    bytes per (stage, field) access - fully coalesced, no LDS needed, no cross-lane traffic.
+//    Stage loops run over a wave-uniform stage index (bound = the wave's largest horizon, lanes
+//    with a shorter horizon are predicated off), so every access is SGPR base + one per-lane VGPR
+//    offset;
+//  * a persistent kernel: each lane pulls problems from a global work queue (wave-aggregated
+//    atomicAdd on one head word) and runs the SQP to termination, one synchronous SQP iteration at
+//    a time for the whole wave, then pulls the next problem.  The SQP iteration count has a long
+//    tail (median ~20, cap 1000), so the queue keeps lanes busy instead of idling behind the
+//    slowest problem of a statically assigned wave;
+//  * per SQP iteration: ERK4 + forward sensitivities (compute-heavy, registers only), then the
+//    Riccati interior-point QP whose stage sweeps stream A_k, B_k, factors and iterates through HBM
+//    (memory-bound), then merit line search (re-simulation) and the primal/dual update.
+// Arithmetic is FP64 throughout (near-LP QPs with a 1e-5 Hessian need it).
+//
+// The algorithm is the one restated in oracle/vboc_oracle.c (the checker); see that file for the
+// reference line of every option and reformulation.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/vboc.h"
+#include "model.h"
+
+#define UNR _Pragma("unroll")
+
+namespace vboc {
+
+struct Opts {
+  double tol_stat, tol_eq, tol_ineq, tol_comp;
+  double qp_tol_stat, qp_tol_eq, qp_tol_comp;
+  double alpha_min, alpha_red, lm, mu0, push, tau;
+  int max_iter, qp_max_iter;
+};
+
+// Slot-major workspace.  Field counts per stage are fixed by NQ.
+struct Work {
+  double *X, *U, *PI, *LL, *LU, *WPI;        // SQP iterate + NLP multipliers + merit weights
+  double *A, *Bm, *BD;                        // linearisation (A_k, B_k, defect b_k)
+  double *DZ, *QL, *QU, *E0;                  // IPM iterate (step, bound duals), initial residual
+  double *K, *KF, *LR, *M, *Y, *PE, *D, *DAFF, *QPI;  // Riccati factors, directions, costate
+  double *F0, *LR0, *M0, *Y0, *PE0, *PAR;     // stage-0 specials, problem parameters (per slot)
+  long long S;                                // number of slots (lanes)
+};
+
+struct Inputs {
+  int B, nmax;
+  const int* N;
+  const double *xg, *ug, *p, *lbx, *ubx, *lbu, *ubu, *lbx0, *ubx0, *lbxe, *ubxe;
+  int* status;
+  double *xo, *uo, *cost;
+  int *sqp_iter, *qp_iter;
+  unsigned int* head;   // work-queue head
+};
+
+// per-slot parameter fields
+template <int NQ>
+struct Par {
+  static constexpr int NX = 2 * NQ, NU = NQ;
+  enum : int {
+    H = 0, Q0 = 1, DIR = Q0 + NQ, SLB = DIR + NQ, SUB, CS, CCONST, XLB, XUB = XLB + NX, ULB = XUB + NX,
+    UUB = ULB + NU, QNLB = UUB + NU, QNUB = QNLB + NQ, VFIN = QNUB + NQ, S = VFIN + NQ, NU_ = S + 1,
+    WNU = NU_ + NQ, WBND = WNU + NQ, E0N = WBND + 1, QNU = E0N + NQ, COUNT = QNU + NQ
+  };
+};
+
+// Force a wave-uniform pointer into SGPRs.  Opaque to loop strength reduction, so each access
+// becomes `global_load ... vOFF, s[base]` with ONE shared per-lane offset register instead of a
+// 64-bit per-field VGPR induction pointer.  Only for pointers that ARE uniform.
+__device__ __forceinline__ double* uptr(double* p) {
+  const unsigned long long v = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (double*)(((unsigned long long)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+  UNR for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+template <int NQ>
+struct Lane {
+  static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1;
+  static constexpr int FX = NX, FU = NU, FPI = NX, FZ = NZ, FA = NX * NX, FB = NX * NU, FK = NU * NX,
+                       FLR = NU * NU, FM = NU * NQ;
+  using PF = Par<NQ>;
+
+  const Work& w;
+  const Opts& o;
+  const unsigned slot;
+  int N;    // this lane's horizon
+  int Nw;   // wave-uniform: largest horizon of the wave's active lanes (SGPR)
+  // QP scalars (registers only while the QP runs)
+  double rs, rd0, e00, mu, nbox;
+
+  __device__ Lane(const Work& w_, const Opts& o_, unsigned slot_) : w(w_), o(o_), slot(slot_), N(0), Nw(0) {}
+
+  // k wave-uniform -> SGPR address + one VGPR offset
+  __device__ __forceinline__ double& at(double* base, int F, int k, int f) const {
+    return uptr(base + ((long long)k * F + f) * w.S)[slot];
+  }
+  // k per lane (the terminal stage N)
+  __device__ __forceinline__ double& atv(double* base, int F, int k, int f) const {
+    return (base + ((long long)k * F + f) * w.S)[slot];
+  }
+  template <bool U>
+  __device__ __forceinline__ double& atk(double* base, int F, int k, int f) const {
+    return U ? at(base, F, k, f) : atv(base, F, k, f);
+  }
+  __device__ __forceinline__ double& at0(double* base, int f) const { return uptr(base + (long long)f * w.S)[slot]; }
+  __device__ __forceinline__ double& par(int f) const { return at0(w.PAR, f); }
+
+  // ---------------------------------------------------------------------------------------------
+  // stage component view: value, bounds, boxed flag of the NZ step components of stage k
+  // stage 0: (s, u_0); 0<k<N: (x_k, u_k); k == N: x_N with only the positions boxed.
+  // ---------------------------------------------------------------------------------------------
+  template <bool U = true>
+  __device__ __forceinline__ void stage_box(int k, double (&z)[NZ], double (&lb)[NZ], double (&ub)[NZ],
+                                            bool (&bx)[NZ]) const {
+    if (k == 0) {
+      z[0] = par(PF::S); lb[0] = par(PF::SLB); ub[0] = par(PF::SUB); bx[0] = true;
+      UNR for (int a = 0; a < NU; ++a) {
+        z[1 + a] = at(w.U, FU, 0, a); lb[1 + a] = par(PF::ULB + a); ub[1 + a] = par(PF::UUB + a); bx[1 + a] = true;
+      }
+      UNR for (int i = M0; i < NZ; ++i) { z[i] = 0; lb[i] = -1; ub[i] = 1; bx[i] = false; }
+    } else if (k == N) {
+      UNR for (int i = 0; i < NX; ++i) {
+        z[i] = atk<U>(w.X, FX, k, i);
+        const bool b = i < NQ;
+        bx[i] = b;
+        lb[i] = b ? par(PF::QNLB + (i < NQ ? i : 0)) : -1;
+        ub[i] = b ? par(PF::QNUB + (i < NQ ? i : 0)) : 1;
+      }
+      UNR for (int i = NX; i < NZ; ++i) { z[i] = 0; lb[i] = -1; ub[i] = 1; bx[i] = false; }
+    } else {
+      UNR for (int i = 0; i < NX; ++i) {
+        z[i] = atk<U>(w.X, FX, k, i); lb[i] = par(PF::XLB + i); ub[i] = par(PF::XUB + i); bx[i] = true;
+      }
+      UNR for (int a = 0; a < NU; ++a) {
+        z[NX + a] = atk<U>(w.U, FU, k, a); lb[NX + a] = par(PF::ULB + a); ub[NX + a] = par(PF::UUB + a); bx[NX + a] = true;
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  // problem setup / output (per lane, divergent - once per problem)
+  // ---------------------------------------------------------------------------------------------
+  __device__ void load(const Inputs& in, int pid) {
+    constexpr int NXR = NX + 1, NP = NQ + 1;
+    N = in.N[pid];
+    const double* p = in.p + (long long)pid * NP;
+    const double* lbx = in.lbx + (long long)pid * NXR;
+    const double* ubx = in.ubx + (long long)pid * NXR;
+    const double* lbx0 = in.lbx0 + (long long)pid * NXR;
+    const double* ubx0 = in.ubx0 + (long long)pid * NXR;
+    const double* lbxe = in.lbxe + (long long)pid * NXR;
+    const double* ubxe = in.ubxe + (long long)pid * NXR;
+    const double h = lbx[NX];
+    par(PF::H) = h;
+    double nrm = 0.0;
+    UNR for (int j = 0; j < NQ; ++j) nrm += p[j] * p[j];
+    nrm = sqrt(nrm);
+    double slb = -INFINITY, sub = INFINITY, cs = 0.0, dir[NQ];
+    UNR for (int j = 0; j < NQ; ++j) {
+      dir[j] = (NQ == 1) ? 1.0 : p[j] / nrm;
+      par(PF::DIR + j) = dir[j];
+      par(PF::Q0 + j) = lbx0[j];
+      cs += p[j] * dir[j];
+      const double dj = dir[j], lo = lbx0[NQ + j], hi = ubx0[NQ + j];
+      if (dj > 0) { slb = fmax(slb, lo / dj); sub = fmin(sub, hi / dj); }
+      else if (dj < 0) { slb = fmax(slb, hi / dj); sub = fmin(sub, lo / dj); }
+    }
+    par(PF::SLB) = slb; par(PF::SUB) = sub; par(PF::CS) = cs;
+    par(PF::CCONST) = p[NQ] * h * (double)N;
+    UNR for (int i = 0; i < NX; ++i) { par(PF::XLB + i) = lbx[i]; par(PF::XUB + i) = ubx[i]; }
+    UNR for (int a = 0; a < NU; ++a) {
+      par(PF::ULB + a) = in.lbu[(long long)pid * NU + a];
+      par(PF::UUB + a) = in.ubu[(long long)pid * NU + a];
+    }
+    UNR for (int j = 0; j < NQ; ++j) {
+      par(PF::QNLB + j) = lbxe[j]; par(PF::QNUB + j) = ubxe[j]; par(PF::VFIN + j) = lbxe[NQ + j];
+      par(PF::NU_ + j) = 0.0; par(PF::WNU + j) = 0.0;
+    }
+    par(PF::WBND) = 0.0;
+    const double* xg = in.xg + (long long)pid * (in.nmax + 1) * NXR;
+    const double* ug = in.ug + (long long)pid * in.nmax * NU;
+    double s = 0.0;
+    UNR for (int j = 0; j < NQ; ++j) s += dir[j] * xg[NQ + j];
+    par(PF::S) = s;
+    for (int k = 0; k <= N; ++k) {
+      double* X = w.X + (long long)k * FX * w.S + slot;
+      double* LL = w.LL + (long long)k * FZ * w.S + slot;
+      double* LU = w.LU + (long long)k * FZ * w.S + slot;
+      UNR for (int i = 0; i < NX; ++i) X[i * w.S] = xg[(long long)k * NXR + i];
+      UNR for (int i = 0; i < NZ; ++i) { LL[i * w.S] = 0.0; LU[i * w.S] = 0.0; }
+      if (k < N) {
+        double* U = w.U + (long long)k * FU * w.S + slot;
+        double* PI = w.PI + (long long)k * FPI * w.S + slot;
+        double* WPI = w.WPI + (long long)k * FX * w.S + slot;
+        UNR for (int a = 0; a < NU; ++a) U[a * w.S] = ug[(long long)k * NU + a];
+        UNR for (int i = 0; i < NX; ++i) { PI[i * w.S] = 0.0; WPI[i * w.S] = 0.0; }
+      }
+    }
+  }
+
+  __device__ void store_result(const Inputs& in, int pid, int status, int sqp_it, int qp_tot) {
+    constexpr int NXR = NX + 1;
+    double* xo = in.xo + (long long)pid * (in.nmax + 1) * NXR;
+    double* uo = in.uo + (long long)pid * in.nmax * NU;
+    const double s = par(PF::S), h = par(PF::H);
+    for (int k = 0; k <= N; ++k) {
+      const double* X = w.X + (long long)k * FX * w.S + slot;
+      UNR for (int i = 0; i < NX; ++i) {
+        const double v = (k == 0) ? (i < NQ ? par(PF::Q0 + i) : s * par(PF::DIR + (i - NQ + (i < NQ ? NQ : 0))))
+                                  : X[i * w.S];
+        xo[(long long)k * NXR + i] = v;
+      }
+      xo[(long long)k * NXR + NX] = h;
+      if (k < N) {
+        const double* U = w.U + (long long)k * FU * w.S + slot;
+        UNR for (int a = 0; a < NU; ++a) uo[(long long)k * NU + a] = U[a * w.S];
+      }
+    }
+    in.status[pid] = status;
+    in.cost[pid] = par(PF::CS) * s + par(PF::CCONST);
+    in.sqp_iter[pid] = sqp_it;
+    in.qp_iter[pid] = qp_tot;
+  }
+
+  __device__ __forceinline__ void x0_of(double (&x)[NX], double sv) const {
+    UNR for (int j = 0; j < NQ; ++j) { x[j] = par(PF::Q0 + j); x[NQ + j] = sv * par(PF::DIR + j); }
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  // linearisation (ERK4 + sensitivities, defects) fused with the NLP residuals
+  // ---------------------------------------------------------------------------------------------
+  __device__ void linearize(double& rstat, double& req, double& rineq, double& rcomp) {
+    double st = 0, eq = 0, in = 0, cp = 0;
+    const double h = par(PF::H);
+    // sweep 1: ERK4 + sensitivities, defects (registers: integrator only)
+    {
+      double xk[NX];
+      x0_of(xk, par(PF::S));
+      for (int k = 0; k < Nw; ++k) {
+        if (k >= N) continue;
+        double uk[NU], x1[NX];
+        UNR for (int a = 0; a < NU; ++a) uk[a] = at(w.U, FU, k, a);
+        rk4_sens<NQ>(h, xk, uk, x1, [&](int i, int c, double v) {
+          if (c < NX) at(w.A, FA, k, i * NX + c) = v;
+          else at(w.Bm, FB, k, i * NU + (c - NX)) = v;
+        });
+        UNR for (int i = 0; i < NX; ++i) {
+          const double xn = at(w.X, FX, k + 1, i);
+          const double b = x1[i] - xn;
+          at(w.BD, FX, k, i) = b;
+          eq = fmax(eq, fabs(b));
+          xk[i] = xn;
+        }
+      }
+    }
+    // sweep 2: NLP residuals with the current multipliers
+    double pprev[NX];
+    UNR for (int i = 0; i < NX; ++i) pprev[i] = 0.0;
+    for (int k = 0; k < Nw; ++k) {
+      if (k >= N) continue;
+      double pik[NX];
+      UNR for (int i = 0; i < NX; ++i) pik[i] = at(w.PI, FPI, k, i);
+      double z[NZ], lb[NZ], ub[NZ];
+      bool bx[NZ];
+      stage_box(k, z, lb, ub, bx);
+      if (k == 0) {
+        // F0 = [A0 g, B0] with g = [0; dir]
+        UNR for (int i = 0; i < NX; ++i) {
+          double t = 0.0;
+          UNR for (int j = 0; j < NQ; ++j) t += at(w.A, FA, 0, i * NX + NQ + j) * par(PF::DIR + j);
+          at0(w.F0, i * M0) = t;
+          UNR for (int a = 0; a < NU; ++a) at0(w.F0, i * M0 + 1 + a) = at(w.Bm, FB, 0, i * NU + a);
+        }
+        UNR for (int c = 0; c < M0; ++c) {
+          double gr = (c == 0 ? par(PF::CS) : 0.0) - at(w.LL, FZ, 0, c) + at(w.LU, FZ, 0, c);
+          UNR for (int r = 0; r < NX; ++r) gr += at0(w.F0, r * M0 + c) * pik[r];
+          st = fmax(st, fabs(gr));
+        }
+      } else {
+        UNR for (int c = 0; c < NZ; ++c) {
+          double gr = -at(w.LL, FZ, k, c) + at(w.LU, FZ, k, c);
+          if (c < NX) {
+            UNR for (int r = 0; r < NX; ++r) gr += at(w.A, FA, k, r * NX + c) * pik[r];
+            gr -= pprev[c];
+          } else {
+            UNR for (int r = 0; r < NX; ++r) gr += at(w.Bm, FB, k, r * NU + (c - NX)) * pik[r];
+          }
+          st = fmax(st, fabs(gr));
+        }
+      }
+      UNR for (int c = 0; c < NZ; ++c) {
+        if (!bx[c]) continue;
+        const double ll = at(w.LL, FZ, k, c), lu = at(w.LU, FZ, k, c);
+        in = fmax(in, fmax(lb[c] - z[c], z[c] - ub[c]));
+        cp = fmax(cp, fmax(fabs(ll * (z[c] - lb[c])), fabs(lu * (ub[c] - z[c]))));
+      }
+      UNR for (int i = 0; i < NX; ++i) pprev[i] = pik[i];
+    }
+    // terminal stage (per-lane N)
+    {
+      double z[NZ], lb[NZ], ub[NZ];
+      bool bx[NZ];
+      stage_box<false>(N, z, lb, ub, bx);
+      UNR for (int c = 0; c < NX; ++c) {
+        double gr = -atv(w.LL, FZ, N, c) + atv(w.LU, FZ, N, c) - pprev[c];
+        if (c >= NQ) {
+          gr += par(PF::NU_ + c - NQ);
+          eq = fmax(eq, fabs(z[c] - par(PF::VFIN + c - NQ)));
+        }
+        st = fmax(st, fabs(gr));
+        if (bx[c]) {
+          const double ll = atv(w.LL, FZ, N, c), lu = atv(w.LU, FZ, N, c);
+          in = fmax(in, fmax(lb[c] - z[c], z[c] - ub[c]));
+          cp = fmax(cp, fmax(fabs(ll * (z[c] - lb[c])), fabs(lu * (ub[c] - z[c]))));
+        }
+      }
+    }
+    rstat = st; req = eq; rineq = in; rcomp = cp;
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  // interior-point QP
+  // ---------------------------------------------------------------------------------------------
+  __device__ __forceinline__ double cgrad(int k, int i) const { return (k == 0 && i == 0) ? par(PF::CS) : 0.0; }
+
+  // initial point, initial residuals
+  __device__ void qp_init() {
+    rd0 = 0.0; e00 = 0.0; nbox = 0.0;
+    double musum = 0.0;
+    double dprev[NZ];
+    for (int k = 0; k <= Nw; ++k) {
+      if (k > N) continue;
+      double z[NZ], lb[NZ], ub[NZ];
+      bool bx[NZ];
+      stage_box(k, z, lb, ub, bx);
+      double dz[NZ];
+      UNR for (int i = 0; i < NZ; ++i) {
+        double ql = 0.0, qu = 0.0, d0 = 0.0;
+        if (bx[i]) {
+          const double L = lb[i] - z[i], U = ub[i] - z[i], del = o.push * (U - L);
+          d0 = fmin(fmax(0.0, L + del), U - del);
+          ql = o.mu0 / (d0 - L);
+          qu = o.mu0 / (U - d0);
+          musum += o.mu0 + o.mu0;
+          nbox += 2.0;
+        }
+        dz[i] = d0;
+        at(w.DZ, FZ, k, i) = d0;
+        at(w.QL, FZ, k, i) = ql;
+        at(w.QU, FZ, k, i) = qu;
+        rd0 = fmax(rd0, fabs(o.lm * d0 + cgrad(k, i) - ql + qu));
+      }
+      if (k > 0) {
+        // residual of stage k-1 dynamics at the initial point
+        const int kp = k - 1;
+        UNR for (int i = 0; i < NX; ++i) {
+          double t = at(w.BD, FX, kp, i) - dz[i];
+          if (kp == 0) {
+            UNR for (int a = 0; a < M0; ++a) t += at0(w.F0, i * M0 + a) * dprev[a];
+          } else {
+            UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, kp, i * NX + q) * dprev[q];
+            UNR for (int a = 0; a < NU; ++a) t += at(w.Bm, FB, kp, i * NU + a) * dprev[NX + a];
+          }
+          at(w.E0, FX, kp, i) = t;
+          e00 = fmax(e00, fabs(t));
+        }
+      }
+      UNR for (int i = 0; i < NZ; ++i) dprev[i] = dz[i];
+    }
+    UNR for (int j = 0; j < NQ; ++j) {
+      const double e = par(PF::VFIN + j) - atv(w.X, FX, N, NQ + j) - dprev[NQ + j];
+      par(PF::E0N + j) = e;
+      e00 = fmax(e00, fabs(e));
+      par(PF::QNU + j) = 0.0;
+    }
+    mu = musum / nbox;
+    rs = 1.0;
+  }
+
+  struct CompState { double tl, tu, ql, qu, dz; bool bx; };
+
+  template <bool U = true>
+  __device__ __forceinline__ void comp_states(int k, CompState (&c)[NZ]) const {
+    double z[NZ], lb[NZ], ub[NZ];
+    bool bx[NZ];
+    stage_box<U>(k, z, lb, ub, bx);
+    UNR for (int i = 0; i < NZ; ++i) {
+      const double dz = atk<U>(w.DZ, FZ, k, i);
+      c[i].dz = dz;
+      c[i].bx = bx[i];
+      c[i].ql = atk<U>(w.QL, FZ, k, i);
+      c[i].qu = atk<U>(w.QU, FZ, k, i);
+      c[i].tl = dz - (lb[i] - z[i]);
+      c[i].tu = (ub[i] - z[i]) - dz;
+    }
+  }
+
+  // corrector complementarity right-hand sides from the affine direction da
+  __device__ __forceinline__ static void corr_rhs(const CompState& c, double da, double smu, double& rl, double& ru) {
+    const double dlla = -c.ql - c.ql * da / c.tl, dlua = -c.qu + c.qu * da / c.tu;
+    rl = smu - c.tl * c.ql - da * dlla;
+    ru = smu - c.tu * c.qu + da * dlua;
+  }
+
+  // H and g of stage k; corr: corrector RHS with the stored DAFF
+  template <bool U = true>
+  __device__ __forceinline__ void hess_grad(int k, bool corr, double smu, double (&H)[NZ], double (&g)[NZ]) const {
+    CompState c[NZ];
+    comp_states<U>(k, c);
+    UNR for (int i = 0; i < NZ; ++i) {
+      H[i] = o.lm;
+      g[i] = o.lm * c[i].dz + cgrad(k, i);
+      if (c[i].bx) {
+        H[i] += c[i].ql / c[i].tl + c[i].qu / c[i].tu;
+        if (corr) {
+          double rl, ru;
+          corr_rhs(c[i], atk<U>(w.DAFF, FZ, k, i), smu, rl, ru);
+          g[i] += -c[i].ql - rl / c[i].tl + c[i].qu + ru / c[i].tu;
+        }
+      }
+    }
+  }
+
+  // backward Riccati sweep; FACTOR: full factorisation (stores K, LR, M, Y, PE) + vector pass;
+  // otherwise vector pass only, reusing the factors.  Returns false on a failed Cholesky.  Leaves
+  // the stage-0 open-loop step in w0 and the terminal multiplier in nun.
+  template <bool FACTOR>
+  __device__ bool backward(bool corr, double smu, double (&Sc)[NQ * NQ], double (&lin_e)[NQ], double (&w0)[M0],
+                           double (&nun)[NQ]) {
+    bool ok = true;
+    double P[NX * NX], p[NX], Pi[NX * NQ], lin[NQ];
+    {
+      double H[NZ], g[NZ];
+      hess_grad<false>(N, corr, smu, H, g);
+      UNR for (int i = 0; i < NX; ++i) {
+        UNR for (int j = 0; j < NX; ++j) P[i * NX + j] = (i == j) ? H[i] : 0.0;
+        p[i] = g[i];
+        UNR for (int j = 0; j < NQ; ++j) Pi[i * NQ + j] = (i == NQ + j) ? 1.0 : 0.0;
+      }
+    }
+    UNR for (int j = 0; j < NQ; ++j) lin[j] = 0.0;
+    if (FACTOR) {
+      UNR for (int j = 0; j < NQ * NQ; ++j) Sc[j] = 0.0;
+      UNR for (int j = 0; j < NQ; ++j) lin_e[j] = 0.0;
+    }
+    for (int k = Nw - 1; k >= 1; --k) {
+      if (k >= N) continue;
+      double H[NZ], g[NZ];
+      hess_grad(k, corr, smu, H, g);
+      double Pe[NX], Lr[NU * NU], Yk[NU * NQ];
+      double Bk[NX * NU];
+      UNR for (int i = 0; i < NX * NU; ++i) Bk[i] = at(w.Bm, FB, k, i);
+      double BP[NU * NX];
+      if (FACTOR) {
+        // Pe = P e ; lin_e += Pi' e
+        UNR for (int i = 0; i < NX; ++i) {
+          double t = 0.0;
+          UNR for (int j = 0; j < NX; ++j) t += P[i * NX + j] * (rs * at(w.E0, FX, k, j));
+          Pe[i] = t;
+          at(w.PE, FX, k, i) = t;
+        }
+        UNR for (int j = 0; j < NQ; ++j) {
+          double t = 0.0;
+          UNR for (int i = 0; i < NX; ++i) t += Pi[i * NQ + j] * (rs * at(w.E0, FX, k, i));
+          lin_e[j] += t;
+        }
+        // BP = B' P ; Ru = BP B + diag(Hu)
+        UNR for (int a = 0; a < NU; ++a)
+          UNR for (int j = 0; j < NX; ++j) {
+            double t = 0.0;
+            UNR for (int i = 0; i < NX; ++i) t += Bk[i * NU + a] * P[i * NX + j];
+            BP[a * NX + j] = t;
+          }
+        UNR for (int a = 0; a < NU; ++a)
+          UNR for (int c = 0; c <= a; ++c) {
+            double t = (a == c) ? H[NX + a] : 0.0;
+            UNR for (int i = 0; i < NX; ++i) t += BP[a * NX + i] * Bk[i * NU + c];
+            Lr[a * NU + c] = t;
+            Lr[c * NU + a] = t;
+          }
+        ok = ok && chol<NU>(Lr);
+        UNR for (int i = 0; i < NU * NU; ++i) at(w.LR, FLR, k, i) = Lr[i];
+        // Y = B' Pi ; M = Ru^-1 Y ; S += Y' M
+        UNR for (int a = 0; a < NU; ++a)
+          UNR for (int j = 0; j < NQ; ++j) {
+            double t = 0.0;
+            UNR for (int i = 0; i < NX; ++i) t += Bk[i * NU + a] * Pi[i * NQ + j];
+            Yk[a * NQ + j] = t;
+            at(w.Y, FM, k, a * NQ + j) = t;
+          }
+        UNR for (int j = 0; j < NQ; ++j) {
+          double col[NU];
+          UNR for (int a = 0; a < NU; ++a) col[a] = Yk[a * NQ + j];
+          chol_solve<NU>(Lr, col);
+          UNR for (int a = 0; a < NU; ++a) at(w.M, FM, k, a * NQ + j) = col[a];
+          UNR for (int i = 0; i < NQ; ++i) {
+            double t = 0.0;
+            UNR for (int a = 0; a < NU; ++a) t += Yk[a * NQ + i] * col[a];
+            Sc[i * NQ + j] += t;
+          }
+        }
+      } else {
+        UNR for (int i = 0; i < NX; ++i) Pe[i] = at(w.PE, FX, k, i);
+        UNR for (int i = 0; i < NU * NU; ++i) Lr[i] = at(w.LR, FLR, k, i);
+        UNR for (int i = 0; i < NU * NQ; ++i) Yk[i] = at(w.Y, FM, k, i);
+      }
+      // vector pass part 1: v = Pe + p ; r = g_u + B' v ; kf = -Ru^-1 r
+      double v[NX], r[NU], kf[NU];
+      UNR for (int i = 0; i < NX; ++i) v[i] = Pe[i] + p[i];
+      UNR for (int a = 0; a < NU; ++a) {
+        double t = g[NX + a];
+        UNR for (int i = 0; i < NX; ++i) t += Bk[i * NU + a] * v[i];
+        r[a] = t;
+        kf[a] = t;
+      }
+      chol_solve<NU>(Lr, kf);
+      UNR for (int a = 0; a < NU; ++a) {
+        kf[a] = -kf[a];
+        at(w.KF, FU, k, a) = kf[a];
+      }
+      UNR for (int j = 0; j < NQ; ++j) {
+        double t = 0.0;
+        UNR for (int a = 0; a < NU; ++a) t += Yk[a * NQ + j] * kf[a];
+        lin[j] += t;
+      }
+      double Kk[NU * NX];
+      if (FACTOR) {
+        // W = L^-1 (BP A) ; K = -L^-T W
+        double W[NU * NX];
+        UNR for (int j = 0; j < NX; ++j) {
+          double col[NU];
+          UNR for (int a = 0; a < NU; ++a) {
+            double t = 0.0;
+            UNR for (int i = 0; i < NX; ++i) t += BP[a * NX + i] * at(w.A, FA, k, i * NX + j);
+            col[a] = t;
+          }
+          // forward substitution only (W), then back substitution (K)
+          UNR for (int a = 0; a < NU; ++a) {
+            double t = col[a];
+            UNR for (int q = 0; q < a; ++q) t -= Lr[a * NU + q] * col[q];
+            col[a] = t / Lr[a * NU + a];
+          }
+          UNR for (int a = 0; a < NU; ++a) W[a * NX + j] = col[a];
+          UNR for (int a = NU - 1; a >= 0; --a) {
+            double t = col[a];
+            UNR for (int q = a + 1; q < NU; ++q) t -= Lr[q * NU + a] * col[q];
+            col[a] = t / Lr[a * NU + a];
+          }
+          UNR for (int a = 0; a < NU; ++a) {
+            Kk[a * NX + j] = -col[a];
+            at(w.K, FK, k, a * NX + j) = -col[a];
+          }
+        }
+        // Pn = diag(Hx) - W'W + A' P A   (A streamed column by column)
+        double Pn[NX * NX];
+        UNR for (int i = 0; i < NX; ++i)
+          UNR for (int j = 0; j <= i; ++j) {
+            double t = (i == j) ? H[i] : 0.0;
+            UNR for (int a = 0; a < NU; ++a) t -= W[a * NX + i] * W[a * NX + j];
+            Pn[i * NX + j] = t;
+          }
+        UNR for (int j = 0; j < NX; ++j) {
+          double Aj[NX], t[NX];
+          UNR for (int q = 0; q < NX; ++q) Aj[q] = at(w.A, FA, k, q * NX + j);
+          UNR for (int i = 0; i < NX; ++i) {
+            double s = 0.0;
+            UNR for (int q = 0; q < NX; ++q) s += P[i * NX + q] * Aj[q];
+            t[i] = s;
+          }
+          UNR for (int i = j; i < NX; ++i) {
+            double s = 0.0;
+            UNR for (int q = 0; q < NX; ++q) s += at(w.A, FA, k, q * NX + i) * t[q];
+            Pn[i * NX + j] += s;
+          }
+        }
+        // Pi <- A'Pi + K'Y
+        double Pin[NX * NQ];
+        UNR for (int i = 0; i < NX; ++i)
+          UNR for (int j = 0; j < NQ; ++j) {
+            double t = 0.0;
+            UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, k, q * NX + i) * Pi[q * NQ + j];
+            UNR for (int a = 0; a < NU; ++a) t += Kk[a * NX + i] * Yk[a * NQ + j];
+            Pin[i * NQ + j] = t;
+          }
+        UNR for (int i = 0; i < NX * NQ; ++i) Pi[i] = Pin[i];
+        UNR for (int i = 0; i < NX; ++i)
+          UNR for (int j = 0; j <= i; ++j) { P[i * NX + j] = Pn[i * NX + j]; P[j * NX + i] = Pn[i * NX + j]; }
+      } else {
+        UNR for (int i = 0; i < NU * NX; ++i) Kk[i] = at(w.K, FK, k, i);
+      }
+      // vector pass part 2: p = g_x + A' v + K' r
+      UNR for (int i = 0; i < NX; ++i) {
+        double t = g[i];
+        UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, k, q * NX + i) * v[q];
+        UNR for (int a = 0; a < NU; ++a) t += Kk[a * NX + i] * r[a];
+        p[i] = t;
+      }
+    }
+    // stage 0: controls (s, u0), F0 = [A0 g, B0]
+    {
+      double H[NZ], g[NZ];
+      hess_grad(0, corr, smu, H, g);
+      double F[NX * M0], Pe[NX], Lr[M0 * M0], Yk[M0 * NQ];
+      UNR for (int i = 0; i < NX * M0; ++i) F[i] = at0(w.F0, i);
+      if (FACTOR) {
+        UNR for (int i = 0; i < NX; ++i) {
+          double t = 0.0;
+          UNR for (int j = 0; j < NX; ++j) t += P[i * NX + j] * (rs * at(w.E0, FX, 0, j));
+          Pe[i] = t;
+          at0(w.PE0, i) = t;
+        }
+        UNR for (int j = 0; j < NQ; ++j) {
+          double t = 0.0;
+          UNR for (int i = 0; i < NX; ++i) t += Pi[i * NQ + j] * (rs * at(w.E0, FX, 0, i));
+          lin_e[j] += t;
+        }
+        double BP[M0 * NX];
+        UNR for (int a = 0; a < M0; ++a)
+          UNR for (int j = 0; j < NX; ++j) {
+            double t = 0.0;
+            UNR for (int i = 0; i < NX; ++i) t += F[i * M0 + a] * P[i * NX + j];
+            BP[a * NX + j] = t;
+          }
+        UNR for (int a = 0; a < M0; ++a)
+          UNR for (int c = 0; c <= a; ++c) {
+            double t = (a == c) ? H[a] : 0.0;
+            UNR for (int i = 0; i < NX; ++i) t += BP[a * NX + i] * F[i * M0 + c];
+            Lr[a * M0 + c] = t;
+            Lr[c * M0 + a] = t;
+          }
+        ok = ok && chol<M0>(Lr);
+        UNR for (int i = 0; i < M0 * M0; ++i) at0(w.LR0, i) = Lr[i];
+        UNR for (int a = 0; a < M0; ++a)
+          UNR for (int j = 0; j < NQ; ++j) {
+            double t = 0.0;
+            UNR for (int i = 0; i < NX; ++i) t += F[i * M0 + a] * Pi[i * NQ + j];
+            Yk[a * NQ + j] = t;
+            at0(w.Y0, a * NQ + j) = t;
+          }
+        UNR for (int j = 0; j < NQ; ++j) {
+          double col[M0];
+          UNR for (int a = 0; a < M0; ++a) col[a] = Yk[a * NQ + j];
+          chol_solve<M0>(Lr, col);
+          UNR for (int a = 0; a < M0; ++a) at0(w.M0, a * NQ + j) = col[a];
+          UNR for (int i = 0; i < NQ; ++i) {
+            double t = 0.0;
+            UNR for (int a = 0; a < M0; ++a) t += Yk[a * NQ + i] * col[a];
+            Sc[i * NQ + j] += t;
+          }
+        }
+      } else {
+        UNR for (int i = 0; i < NX; ++i) Pe[i] = at0(w.PE0, i);
+        UNR for (int i = 0; i < M0 * M0; ++i) Lr[i] = at0(w.LR0, i);
+        UNR for (int i = 0; i < M0 * NQ; ++i) Yk[i] = at0(w.Y0, i);
+      }
+      double v[NX];
+      UNR for (int i = 0; i < NX; ++i) v[i] = Pe[i] + p[i];
+      UNR for (int a = 0; a < M0; ++a) {
+        double t = g[a];
+        UNR for (int i = 0; i < NX; ++i) t += F[i * M0 + a] * v[i];
+        w0[a] = t;
+      }
+      chol_solve<M0>(Lr, w0);
+      UNR for (int a = 0; a < M0; ++a) w0[a] = -w0[a];
+      UNR for (int j = 0; j < NQ; ++j) {
+        double t = 0.0;
+        UNR for (int a = 0; a < M0; ++a) t += Yk[a * NQ + j] * w0[a];
+        lin[j] += t;
+      }
+    }
+    // terminal multiplier: nu = S^-1 (E d_N^0 - e_N)
+    {
+      double Sl[NQ * NQ], rhs_[NQ];
+      UNR for (int i = 0; i < NQ * NQ; ++i) Sl[i] = Sc[i];
+      ok = ok && chol<NQ>(Sl);
+      UNR for (int j = 0; j < NQ; ++j) rhs_[j] = lin[j] + lin_e[j] - rs * par(PF::E0N + j);
+      chol_solve<NQ>(Sl, rhs_);
+      UNR for (int j = 0; j < NQ; ++j) nun[j] = rhs_[j];
+    }
+    return ok;
+  }
+
+  __device__ __forceinline__ static double stb(double t, double dt) { return dt < 0.0 ? -t / dt : INFINITY; }
+
+  // forward sweep.  CORR == false: stores DAFF, returns the affine step length and the mu_aff
+  // polynomial; CORR == true: stores D, returns alpha_max of the combined step.
+  template <bool CORR>
+  __device__ void forward(double smu, const double (&w0in)[M0], const double (&nun)[NQ], double& amax, double& c0,
+                          double& c1, double& c2) {
+    amax = CORR ? 1.0 / o.tau : 1.0;
+    c0 = c1 = c2 = 0.0;
+    double* dst = CORR ? w.D : w.DAFF;
+    double dx[NX];
+    for (int k = 0; k <= Nw; ++k) {
+      if (k > N) continue;
+      double d[NZ];
+      if (k == 0) {
+        double w0[M0];
+        UNR for (int a = 0; a < M0; ++a) {
+          double t = w0in[a];
+          UNR for (int j = 0; j < NQ; ++j) t -= at0(w.M0, a * NQ + j) * nun[j];
+          w0[a] = t;
+        }
+        UNR for (int i = 0; i < NZ; ++i) d[i] = i < M0 ? w0[i < M0 ? i : 0] : 0.0;
+        UNR for (int i = 0; i < NX; ++i) {
+          double t = rs * at(w.E0, FX, 0, i);
+          UNR for (int a = 0; a < M0; ++a) t += at0(w.F0, i * M0 + a) * w0[a];
+          dx[i] = t;
+        }
+      } else if (k < N) {
+        double du[NU];
+        UNR for (int a = 0; a < NU; ++a) {
+          double t = at(w.KF, FU, k, a);
+          UNR for (int i = 0; i < NX; ++i) t += at(w.K, FK, k, a * NX + i) * dx[i];
+          UNR for (int j = 0; j < NQ; ++j) t -= at(w.M, FM, k, a * NQ + j) * nun[j];
+          du[a] = t;
+        }
+        UNR for (int i = 0; i < NX; ++i) d[i] = dx[i];
+        UNR for (int a = 0; a < NU; ++a) d[NX + a] = du[a];
+        double dn[NX];
+        UNR for (int i = 0; i < NX; ++i) {
+          double t = rs * at(w.E0, FX, k, i);
+          UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, k, i * NX + q) * dx[q];
+          UNR for (int a = 0; a < NU; ++a) t += at(w.Bm, FB, k, i * NU + a) * du[a];
+          dn[i] = t;
+        }
+        UNR for (int i = 0; i < NX; ++i) dx[i] = dn[i];
+      } else {
+        UNR for (int i = 0; i < NZ; ++i) d[i] = i < NX ? dx[i < NX ? i : 0] : 0.0;
+      }
+      CompState c[NZ];
+      comp_states(k, c);
+      UNR for (int i = 0; i < NZ; ++i) {
+        at(dst, FZ, k, i) = d[i];
+        if (!c[i].bx) continue;
+        double dll, dlu;
+        if (!CORR) {
+          dll = -c[i].ql - c[i].ql * d[i] / c[i].tl;
+          dlu = -c[i].qu + c[i].qu * d[i] / c[i].tu;
+          c0 += c[i].tl * c[i].ql + c[i].tu * c[i].qu;
+          c1 += c[i].tl * dll + d[i] * c[i].ql + c[i].tu * dlu - d[i] * c[i].qu;
+          c2 += d[i] * dll - d[i] * dlu;
+        } else {
+          double rl, ru;
+          corr_rhs(c[i], at(w.DAFF, FZ, k, i), smu, rl, ru);
+          dll = (rl - c[i].ql * d[i]) / c[i].tl;
+          dlu = (ru + c[i].qu * d[i]) / c[i].tu;
+        }
+        amax = fmin(amax, stb(c[i].tl, d[i]));
+        amax = fmin(amax, stb(c[i].tu, -d[i]));
+        amax = fmin(amax, stb(c[i].ql, dll));
+        amax = fmin(amax, stb(c[i].qu, dlu));
+      }
+    }
+  }
+
+  // apply the step; recompute mu of the new iterate
+  __device__ void update_iterate(double alpha, double smu) {
+    double musum = 0.0;
+    for (int k = 0; k <= Nw; ++k) {
+      if (k > N) continue;
+      CompState c[NZ];
+      comp_states(k, c);
+      UNR for (int i = 0; i < NZ; ++i) {
+        const double d = at(w.D, FZ, k, i);
+        at(w.DZ, FZ, k, i) = c[i].dz + alpha * d;
+        if (!c[i].bx) continue;
+        double rl, ru;
+        corr_rhs(c[i], at(w.DAFF, FZ, k, i), smu, rl, ru);
+        const double dll = (rl - c[i].ql * d) / c[i].tl, dlu = (ru + c[i].qu * d) / c[i].tu;
+        const double qln = c[i].ql + alpha * dll, qun = c[i].qu + alpha * dlu;
+        at(w.QL, FZ, k, i) = qln;
+        at(w.QU, FZ, k, i) = qun;
+        musum += (c[i].tl + alpha * d) * qln + (c[i].tu - alpha * d) * qun;
+      }
+    }
+    mu = musum / nbox;
+  }
+
+  // returns 0 converged, 1 max iter, -1 failure; iterations in its
+  __device__ int qp_solve(int& its) {
+    qp_init();
+    int status = 1;
+    int it = 0;
+    double Sc[NQ * NQ], lin_e[NQ], w0[M0], nun[NQ];
+    for (; it < o.qp_max_iter; ++it) {
+      if (!isfinite(mu)) { status = -1; break; }
+      if (mu < o.qp_tol_comp && rs * rd0 < o.qp_tol_stat && rs * e00 < o.qp_tol_eq) { status = 0; break; }
+      // predictor
+      if (!backward<true>(false, 0.0, Sc, lin_e, w0, nun)) { status = -1; break; }
+      double aa, c0, c1, c2;
+      forward<false>(0.0, w0, nun, aa, c0, c1, c2);
+      const double muaff = (c0 + aa * (c1 + aa * c2)) / nbox;
+      double sig = muaff / mu;
+      sig = fmin(1.0, sig * sig * sig);
+      const double smu = sig * mu;
+      // corrector
+      if (!backward<false>(true, smu, Sc, lin_e, w0, nun)) { status = -1; break; }
+      double amax;
+      forward<true>(smu, w0, nun, amax, c0, c1, c2);
+      const double alpha = fmin(1.0, o.tau * amax);
+      update_iterate(alpha, smu);
+      UNR for (int j = 0; j < NQ; ++j) par(PF::QNU + j) += alpha * (nun[j] - par(PF::QNU + j));
+      rs *= (1.0 - alpha);
+    }
+    its = it;
+    if (status < 0) return -1;
+    // costate recovery: pi_{N-1} = lm dz_N - ql + qu + E'nu ; pi_{k-1} = lm dz_k - ql + qu + A_k' pi_k
+    double lam[NX];
+    bool fin = true;
+    UNR for (int i = 0; i < NX; ++i) {
+      const double dz = atv(w.DZ, FZ, N, i);
+      lam[i] = o.lm * dz - atv(w.QL, FZ, N, i) + atv(w.QU, FZ, N, i) + (i >= NQ ? par(PF::QNU + (i >= NQ ? i - NQ : 0)) : 0.0);
+      fin = fin && isfinite(dz);
+    }
+    for (int k = Nw - 1; k >= 0; --k) {
+      if (k >= N) continue;
+      UNR for (int i = 0; i < NX; ++i) at(w.QPI, FPI, k, i) = lam[i];
+      if (k == 0) break;
+      double ln[NX];
+      UNR for (int i = 0; i < NX; ++i) {
+        const double dz = at(w.DZ, FZ, k, i);
+        double t = o.lm * dz - at(w.QL, FZ, k, i) + at(w.QU, FZ, k, i);
+        UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, k, q * NX + i) * lam[q];
+        ln[i] = t;
+      }
+      UNR for (int i = 0; i < NX; ++i) lam[i] = ln[i];
+    }
+    if (!fin) return -1;
+    return status;
+  }
+
+  // ---------------------------------------------------------------------------------------------
+  // merit line search + update
+  // ---------------------------------------------------------------------------------------------
+  __device__ __forceinline__ static double wupd(double wv, double lam) {
+    const double a = fabs(lam), b = 0.5 * (wv + a);
+    return a > b ? a : b;
+  }
+
+  // merit(alpha) = cost + sum w_pi |defect| + w_nu |v_N - v_fin| + w_bnd * bound violation
+  __device__ double merit(double alpha) const {
+    const double h = par(PF::H);
+    const double sv = par(PF::S) + alpha * at(w.DZ, FZ, 0, 0);
+    double val = par(PF::CS) * sv + par(PF::CCONST);
+    double viol = 0.0;
+    double xk[NX], uk[NU];
+    x0_of(xk, sv);
+    for (int k = 0; k <= Nw; ++k) {
+      if (k > N) continue;
+      double z[NZ], lb[NZ], ub[NZ];
+      bool bx[NZ];
+      stage_box(k, z, lb, ub, bx);
+      double dzk[NZ];
+      UNR for (int i = 0; i < NZ; ++i) {
+        dzk[i] = at(w.DZ, FZ, k, i);
+        if (!bx[i]) continue;
+        const double v = z[i] + alpha * dzk[i];
+        viol += fmax(0.0, lb[i] - v) + fmax(0.0, v - ub[i]);
+      }
+      if (k > 0) {
+        double phi[NX];
+        rk4<NQ>(h, xk, uk, phi);
+        UNR for (int i = 0; i < NX; ++i) {
+          const double xn = z[i] + alpha * dzk[i];
+          val += at(w.WPI, FX, k - 1, i) * fabs(phi[i] - xn);
+          xk[i] = xn;
+        }
+      }
+      if (k < N) {
+        if (k == 0) {
+          UNR for (int a = 0; a < NU; ++a) uk[a] = z[1 + a] + alpha * dzk[1 + a];
+        } else {
+          UNR for (int a = 0; a < NU; ++a) uk[a] = z[NX + a] + alpha * dzk[NX + a];
+        }
+      }
+    }
+    UNR for (int j = 0; j < NQ; ++j) val += par(PF::WNU + j) * fabs(xk[NQ + j] - par(PF::VFIN + j));
+    return val + par(PF::WBND) * viol;
+  }
+
+  __device__ void update_weights() {
+    double lmax = 0.0;
+    for (int k = 0; k <= Nw; ++k) {
+      if (k > N) continue;
+      if (k < N) {
+        UNR for (int i = 0; i < NX; ++i) at(w.WPI, FX, k, i) = wupd(at(w.WPI, FX, k, i), at(w.QPI, FPI, k, i));
+      }
+      UNR for (int i = 0; i < NZ; ++i) lmax = fmax(lmax, fmax(at(w.QL, FZ, k, i), at(w.QU, FZ, k, i)));
+    }
+    UNR for (int j = 0; j < NQ; ++j) par(PF::WNU + j) = wupd(par(PF::WNU + j), par(PF::QNU + j));
+    par(PF::WBND) = wupd(par(PF::WBND), lmax);
+  }
+
+  __device__ void apply_step(double alpha) {
+    par(PF::S) += alpha * at(w.DZ, FZ, 0, 0);
+    for (int k = 0; k <= Nw; ++k) {
+      if (k > N) continue;
+      if (k == 0) {
+        UNR for (int a = 0; a < NU; ++a) at(w.U, FU, 0, a) += alpha * at(w.DZ, FZ, 0, 1 + a);
+      } else {
+        UNR for (int i = 0; i < NX; ++i) at(w.X, FX, k, i) += alpha * at(w.DZ, FZ, k, i);
+        if (k < N) {
+          UNR for (int a = 0; a < NU; ++a) at(w.U, FU, k, a) += alpha * at(w.DZ, FZ, k, NX + a);
+        }
+      }
+      UNR for (int i = 0; i < NZ; ++i) {
+        double& ll = at(w.LL, FZ, k, i);
+        double& lu = at(w.LU, FZ, k, i);
+        ll += alpha * (at(w.QL, FZ, k, i) - ll);
+        lu += alpha * (at(w.QU, FZ, k, i) - lu);
+      }
+      if (k < N) {
+        UNR for (int i = 0; i < NX; ++i) {
+          double& pi = at(w.PI, FPI, k, i);
+          pi += alpha * (at(w.QPI, FPI, k, i) - pi);
+        }
+      }
+    }
+    UNR for (int j = 0; j < NQ; ++j) par(PF::NU_ + j) += alpha * (par(PF::QNU + j) - par(PF::NU_ + j));
+  }
+};
+
+// -------------------------------------------------------------------------------------------------
+// persistent kernel
+// -------------------------------------------------------------------------------------------------
+template <int NQ>
+__global__ __launch_bounds__(256) void sqp_kernel(Work w, Opts o, Inputs in) {
+  const unsigned slot = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  Lane<NQ> L(w, o, slot);
+  int pid = -1;          // problem held by this lane (-1 none, -2 queue exhausted)
+  int it = 0, qtot = 0;
+  while (pid != -2) {
+    // wave-aggregated dequeue for lanes without a problem
+    const unsigned long long need = __ballot(pid == -1);
+    if (need) {
+      const int leader = __ffsll((unsigned long long)need) - 1;
+      unsigned int base = 0;
+      if (lane == leader) base = atomicAdd(in.head, (unsigned int)__popcll(need));
+      base = __shfl(base, leader);
+      if (pid == -1) {
+        const unsigned int rank = __popcll(need & ((1ull << lane) - 1ull));
+        const unsigned int cand = base + rank;
+        if (cand < (unsigned int)in.B) {
+          pid = (int)cand;
+          L.load(in, pid);
+          it = 0;
+          qtot = 0;
+        } else {
+          pid = -2;
+        }
+      }
+    }
+    if (pid < 0) continue;
+    L.Nw = wave_max(L.N);
+    double rstat, req, rineq, rcomp;
+    L.linearize(rstat, req, rineq, rcomp);
+    int status = -1;
+    if (!isfinite(rstat) || !isfinite(req)) status = 1;
+    else if (rstat < o.tol_stat && req < o.tol_eq && rineq < o.tol_ineq && rcomp < o.tol_comp) status = 0;
+    else if (it >= o.max_iter) status = 2;
+    if (status < 0) {
+      int qit = 0;
+      const int qs = L.qp_solve(qit);
+      qtot += qit;
+      if (qs < 0) {
+        status = 4;
+      } else {
+        L.update_weights();
+        const double phi0 = L.merit(0.0);
+        double alpha = 1.0;
+        for (;;) {
+          const double pa = L.merit(alpha);
+          if (pa < phi0) break;
+          if (alpha * o.alpha_red < o.alpha_min) break;
+          alpha *= o.alpha_red;
+        }
+        L.apply_step(alpha);
+        ++it;
+        if (!isfinite(L.par(Par<NQ>::S))) status = 1;
+      }
+    }
+    if (status >= 0) {
+      L.store_result(in, pid, status, it, qtot);
+      pid = -1;
+    }
+  }
+}
+
+#ifdef VBOC_PHASE_TEST
+// diagnostic: one kernel per phase to read each phase's register allocation
+template <int NQ, int PH>
+__global__ __launch_bounds__(256) void phase_kernel(Work w, Opts o, Inputs in) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  L.N = in.N[L.slot];
+  L.Nw = wave_max(L.N);
+  double a = 0, b = 0, c = 0, d = 0;
+  double Sc[NQ * NQ] = {}, le[NQ] = {}, w0[NQ + 1] = {}, nun[NQ] = {};
+  int it = 0;
+  if (PH == 0) L.linearize(a, b, c, d);
+  if (PH == 1) L.qp_init();
+  if (PH == 2) L.template backward<true>(false, 0.0, Sc, le, w0, nun);
+  if (PH == 3) L.template backward<false>(true, 0.5, Sc, le, w0, nun);
+  if (PH == 4) L.template forward<false>(0.0, w0, nun, a, b, c, d);
+  if (PH == 5) L.template forward<true>(0.1, w0, nun, a, b, c, d);
+  if (PH == 6) L.update_iterate(0.5, 0.1);
+  if (PH == 7) a = L.merit(0.3);
+  if (PH == 8) L.apply_step(0.3);
+  if (PH == 9) L.load(in, L.slot);
+  if (PH == 10) it = L.qp_solve(it);
+  in.cost[L.slot] = a + b + c + d + Sc[0] + le[0] + w0[0] + nun[0] + it;
+}
+template __global__ void phase_kernel<3, 0>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 1>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 2>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 3>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 4>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 5>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 6>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 7>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 8>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 9>(Work, Opts, Inputs);
+template __global__ void phase_kernel<3, 10>(Work, Opts, Inputs);
+#endif
+
+// -------------------------------------------------------------------------------------------------
+// twin integrator (SYM<sys>INIT.acados_integrator): one RK4 step of length T per problem
+// -------------------------------------------------------------------------------------------------
+template <int NQ>
+__global__ __launch_bounds__(256) void rk4_kernel(int B, double T, const double* __restrict__ x,
+                                                  const double* __restrict__ u, double* __restrict__ xo) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  constexpr int NX = 2 * NQ;
+  double xi[NX], ui[NQ], x1[NX];
+  UNR for (int i = 0; i < NX; ++i) xi[i] = x[(long long)b * NX + i];
+  UNR for (int a = 0; a < NQ; ++a) ui[a] = u[(long long)b * NQ + a];
+  rk4<NQ>(T, xi, ui, x1);
+  UNR for (int i = 0; i < NX; ++i) xo[(long long)b * NX + i] = x1[i];
+}
+
+}  // namespace vboc
+
+// =================================================================================================
+// C ABI
+// =================================================================================================
+using namespace vboc;
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess) return fail(VBOC_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+struct vboc_solver {
+  int nq, nmax, device;
+  long long slots;
+  Opts o;
+  Work w;
+  void* pool = nullptr;
+  size_t pool_bytes = 0;
+  unsigned int* head = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int launches = 0;
+  // host staging for vboc_solve_batch_host
+  void* stage = nullptr;
+  size_t stage_bytes = 0;
+};
+
+static void default_opts(Opts& o) {
+  o.tol_stat = 1e-3; o.tol_eq = 1e-6; o.tol_ineq = 1e-6; o.tol_comp = 1e-6;
+  o.qp_tol_stat = 1e-3; o.qp_tol_eq = 1e-8; o.qp_tol_comp = 1e-8;
+  o.alpha_min = 1e-2; o.alpha_red = 0.3; o.lm = 1e-5;
+  o.mu0 = 1.0; o.push = 1e-2; o.tau = 0.995;
+  o.max_iter = 1000; o.qp_max_iter = 100;
+}
+
+static int par_count(int nq) {
+  return nq == 1 ? Par<1>::COUNT : (nq == 2 ? Par<2>::COUNT : Par<3>::COUNT);
+}
+
+static size_t work_doubles_per_slot(int nq, int nmax) {
+  const int NX = 2 * nq, NU = nq, NZ = 3 * nq, M0 = nq + 1;
+  const size_t per_stage = NX /*X*/ + NU + NX /*PI*/ + 2 * NZ + NX /*WPI*/ + NX * NX + NX * NU + NX +
+                           3 * NZ + NX /*E0*/ + NU * NX + NU + NU * NU + 2 * NU * nq + NX /*PE*/ + 2 * NZ + NX;
+  const size_t per_slot = NX * M0 + M0 * M0 + 2 * M0 * nq + NX + par_count(nq);
+  return per_stage * (size_t)(nmax + 1) + per_slot;
+}
+
+extern "C" {
+
+const char* vboc_last_error(void) { return g_err.c_str(); }
+
+int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
+  if (!out) return fail(VBOC_ERR_ARG, "vboc_create: out is NULL");
+  *out = nullptr;
+  if (nq < 1 || nq > 3) return fail(VBOC_ERR_ARG, "vboc_create: nq must be 1, 2 or 3");
+  if (nmax < 1) return fail(VBOC_ERR_ARG, "vboc_create: nmax must be >= 1");
+  HIPCHK(hipSetDevice(device));
+  vboc_solver* h = new vboc_solver();
+  h->nq = nq; h->nmax = nmax; h->device = device;
+  default_opts(h->o);
+  if (slots <= 0) slots = 64 * 1024;
+  if (slots > (1 << 30)) return fail(VBOC_ERR_ARG, "vboc_create: too many slots");
+  slots = ((slots + 255) / 256) * 256;
+  h->slots = slots;
+  const size_t per_slot = work_doubles_per_slot(nq, nmax);
+  h->pool_bytes = per_slot * (size_t)slots * sizeof(double);
+  hipError_t e = hipMalloc(&h->pool, h->pool_bytes);
+  if (e != hipSuccess) {
+    delete h;
+    return fail(VBOC_ERR_NOMEM, std::string("vboc_create: hipMalloc workspace: ") + hipGetErrorString(e));
+  }
+  e = hipMalloc((void**)&h->head, 256);
+  if (e != hipSuccess) {
+    (void)hipFree(h->pool);
+    delete h;
+    return fail(VBOC_ERR_NOMEM, "vboc_create: hipMalloc queue");
+  }
+  (void)hipEventCreate(&h->ev0);
+  (void)hipEventCreate(&h->ev1);
+  // carve the workspace
+  const int NX = 2 * nq, NU = nq, NZ = 3 * nq, M0 = nq + 1;
+  const size_t st = (size_t)(nmax + 1) * slots;
+  double* p = (double*)h->pool;
+  auto take = [&](size_t fields_per_stage) { double* r = p; p += fields_per_stage * st; return r; };
+  auto take0 = [&](size_t fields) { double* r = p; p += fields * (size_t)slots; return r; };
+  Work& w = h->w;
+  w.S = slots;
+  w.X = take(NX); w.U = take(NU); w.PI = take(NX); w.LL = take(NZ); w.LU = take(NZ); w.WPI = take(NX);
+  w.A = take(NX * NX); w.Bm = take(NX * NU); w.BD = take(NX);
+  w.DZ = take(NZ); w.QL = take(NZ); w.QU = take(NZ); w.E0 = take(NX);
+  w.K = take(NU * NX); w.KF = take(NU); w.LR = take(NU * NU); w.M = take(NU * nq); w.Y = take(NU * nq);
+  w.PE = take(NX); w.D = take(NZ); w.DAFF = take(NZ); w.QPI = take(NX);
+  w.F0 = take0(NX * M0); w.LR0 = take0(M0 * M0); w.M0 = take0(M0 * nq); w.Y0 = take0(M0 * nq); w.PE0 = take0(NX);
+  w.PAR = take0(par_count(nq));
+  if ((size_t)((char*)p - (char*)h->pool) != h->pool_bytes) {
+    vboc_destroy(h);
+    return fail(VBOC_ERR_ARG, "vboc_create: internal workspace size mismatch");
+  }
+  *out = h;
+  return VBOC_OK;
+}
+
+int vboc_destroy(vboc_handle h) {
+  if (!h) return VBOC_OK;
+  (void)hipSetDevice(h->device);
+  if (h->pool) (void)hipFree(h->pool);
+  if (h->head) (void)hipFree(h->head);
+  if (h->stage) (void)hipFree(h->stage);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  delete h;
+  return VBOC_OK;
+}
+
+int vboc_set_option(vboc_handle h, const char* f, double v) {
+  if (!h || !f) return fail(VBOC_ERR_ARG, "vboc_set_option: NULL argument");
+  Opts& o = h->o;
+  const std::string s(f);
+  if (s == "nlp_solver_tol_stat") o.tol_stat = v;
+  else if (s == "nlp_solver_tol_eq") o.tol_eq = v;
+  else if (s == "nlp_solver_tol_ineq") o.tol_ineq = v;
+  else if (s == "nlp_solver_tol_comp") o.tol_comp = v;
+  else if (s == "nlp_solver_max_iter") o.max_iter = (int)v;
+  else if (s == "qp_solver_iter_max") o.qp_max_iter = (int)v;
+  else if (s == "qp_solver_tol_stat") o.qp_tol_stat = v;
+  else if (s == "qp_solver_tol_eq") o.qp_tol_eq = v;
+  else if (s == "qp_solver_tol_comp") o.qp_tol_comp = v;
+  else if (s == "levenberg_marquardt") o.lm = v;
+  else if (s == "alpha_min") o.alpha_min = v;
+  else if (s == "alpha_reduction") o.alpha_red = v;
+  else if (s == "ipm_mu0") o.mu0 = v;
+  else if (s == "ipm_push") o.push = v;
+  else if (s == "ipm_tau") o.tau = v;
+  else return fail(VBOC_ERR_ARG, "vboc_set_option: unknown field '" + s + "'");
+  return VBOC_OK;
+}
+
+int vboc_get_option(vboc_handle h, const char* f, double* v) {
+  if (!h || !f || !v) return fail(VBOC_ERR_ARG, "vboc_get_option: NULL argument");
+  const Opts& o = h->o;
+  const std::string s(f);
+  if (s == "nlp_solver_tol_stat") *v = o.tol_stat;
+  else if (s == "nlp_solver_tol_eq") *v = o.tol_eq;
+  else if (s == "nlp_solver_tol_ineq") *v = o.tol_ineq;
+  else if (s == "nlp_solver_tol_comp") *v = o.tol_comp;
+  else if (s == "nlp_solver_max_iter") *v = o.max_iter;
+  else if (s == "qp_solver_iter_max") *v = o.qp_max_iter;
+  else if (s == "qp_solver_tol_stat") *v = o.qp_tol_stat;
+  else if (s == "qp_solver_tol_eq") *v = o.qp_tol_eq;
+  else if (s == "qp_solver_tol_comp") *v = o.qp_tol_comp;
+  else if (s == "levenberg_marquardt") *v = o.lm;
+  else if (s == "alpha_min") *v = o.alpha_min;
+  else if (s == "alpha_reduction") *v = o.alpha_red;
+  else if (s == "ipm_mu0") *v = o.mu0;
+  else if (s == "ipm_push") *v = o.push;
+  else if (s == "ipm_tau") *v = o.tau;
+  else if (s == "slots") *v = (double)h->slots;
+  else if (s == "workspace_bytes") *v = (double)h->pool_bytes;
+  else return fail(VBOC_ERR_ARG, "vboc_get_option: unknown field '" + s + "'");
+  return VBOC_OK;
+}
+
+int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_solve_batch: NULL argument");
+  if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_solve_batch: B < 0");
+  if (b->nmax > h->nmax || b->nmax < 1)
+    return fail(VBOC_ERR_ARG, "vboc_solve_batch: batch nmax exceeds the handle's nmax");
+  if (b->B == 0) { h->launches = 0; return VBOC_OK; }
+  const void* ptrs[] = {b->N, b->x_guess, b->u_guess, b->p, b->lbx, b->ubx, b->lbu, b->ubu, b->lbx_0, b->ubx_0,
+                        b->lbx_e, b->ubx_e, b->status, b->x_out, b->u_out, b->cost, b->sqp_iter, b->qp_iter};
+  for (const void* q : ptrs)
+    if (!q) return fail(VBOC_ERR_ARG, "vboc_solve_batch: NULL array in batch");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  Inputs in;
+  in.B = b->B; in.nmax = b->nmax; in.N = b->N;
+  in.xg = b->x_guess; in.ug = b->u_guess; in.p = b->p; in.lbx = b->lbx; in.ubx = b->ubx; in.lbu = b->lbu;
+  in.ubu = b->ubu; in.lbx0 = b->lbx_0; in.ubx0 = b->ubx_0; in.lbxe = b->lbx_e; in.ubxe = b->ubx_e;
+  in.status = b->status; in.xo = b->x_out; in.uo = b->u_out; in.cost = b->cost; in.sqp_iter = b->sqp_iter;
+  in.qp_iter = b->qp_iter; in.head = h->head;
+  HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
+  // lanes: never more than the problems (rounded to whole workgroups), never more than the slots
+  long long lanes = ((long long)b->B + 255) / 256 * 256;
+  if (lanes > h->slots) lanes = h->slots;
+  Work w = h->w;  // same carve, S = full slot stride
+  const dim3 grid((unsigned)(lanes / 256)), block(256);
+  HIPCHK(hipEventRecord(h->ev0, st));
+  switch (h->nq) {
+    case 1: hipLaunchKernelGGL(sqp_kernel<1>, grid, block, 0, st, w, h->o, in); break;
+    case 2: hipLaunchKernelGGL(sqp_kernel<2>, grid, block, 0, st, w, h->o, in); break;
+    default: hipLaunchKernelGGL(sqp_kernel<3>, grid, block, 0, st, w, h->o, in); break;
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(h->ev1, st));
+  h->launches = 1;
+  return VBOC_OK;
+}
+
+int vboc_last_kernel_ms(vboc_handle h, double* ms, int* launches) {
+  if (!h || !ms) return fail(VBOC_ERR_ARG, "vboc_last_kernel_ms: NULL argument");
+  float f = 0.0f;
+  HIPCHK(hipEventSynchronize(h->ev1));
+  HIPCHK(hipEventElapsedTime(&f, h->ev0, h->ev1));
+  *ms = f;
+  if (launches) *launches = h->launches;
+  return VBOC_OK;
+}
+
+int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_solve_batch_host: NULL argument");
+  if (b->B == 0) return VBOC_OK;
+  HIPCHK(hipSetDevice(h->device));
+  const int nq = h->nq, NXR = 2 * nq + 1, NU = nq, NP = nq + 1;
+  const size_t B = b->B, Nn = b->nmax;
+  const size_t sz_xg = B * (Nn + 1) * NXR, sz_ug = B * Nn * NU;
+  const size_t dbl = sz_xg * 2 + sz_ug * 2 + B * NP + B * NXR * 6 + B * NU * 2 + B /*cost*/;
+  const size_t ints = B * 4;
+  const size_t need = dbl * sizeof(double) + ints * sizeof(int) + 256;
+  if (need > h->stage_bytes) {
+    if (h->stage) (void)hipFree(h->stage);
+    h->stage = nullptr;
+    h->stage_bytes = 0;
+    hipError_t e = hipMalloc(&h->stage, need);
+    if (e != hipSuccess) return fail(VBOC_ERR_NOMEM, "vboc_solve_batch_host: hipMalloc staging");
+    h->stage_bytes = need;
+  }
+  double* d = (double*)h->stage;
+  hipError_t cerr = hipSuccess;
+  auto put = [&](const double* src, size_t n) -> double* {
+    double* r = d;
+    d += n;
+    if (src && cerr == hipSuccess) cerr = hipMemcpy(r, src, n * sizeof(double), hipMemcpyHostToDevice);
+    return r;
+  };
+  vboc_batch_t db = *b;
+  db.x_guess = put(b->x_guess, sz_xg);
+  db.u_guess = put(b->u_guess, sz_ug);
+  db.p = put(b->p, B * NP);
+  db.lbx = put(b->lbx, B * NXR); db.ubx = put(b->ubx, B * NXR);
+  db.lbu = put(b->lbu, B * NU); db.ubu = put(b->ubu, B * NU);
+  db.lbx_0 = put(b->lbx_0, B * NXR); db.ubx_0 = put(b->ubx_0, B * NXR);
+  db.lbx_e = put(b->lbx_e, B * NXR); db.ubx_e = put(b->ubx_e, B * NXR);
+  db.x_out = put(b->x_out, sz_xg);    // copy in so rows beyond N stay as the caller had them
+  db.u_out = put(b->u_out, sz_ug);
+  db.cost = put(nullptr, B);
+  int* ip = (int*)d;
+  db.N = ip; ip += B;
+  db.status = ip; ip += B;
+  db.sqp_iter = ip; ip += B;
+  db.qp_iter = ip; ip += B;
+  HIPCHK(cerr);
+  HIPCHK(hipMemcpy((void*)db.N, b->N, B * sizeof(int), hipMemcpyHostToDevice));
+  int rc = vboc_solve_batch(h, &db, nullptr);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(b->x_out, db.x_out, sz_xg * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(b->u_out, db.u_out, sz_ug * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(b->cost, db.cost, B * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(b->status, db.status, B * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(b->sqp_iter, db.sqp_iter, B * sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(b->qp_iter, db.qp_iter, B * sizeof(int), hipMemcpyDeviceToHost));
+  return VBOC_OK;
+}
+
+int vboc_rk4_batch(int nq, int B, double T, const double* x, const double* u, double* x_out, void* stream) {
+  if (nq < 1 || nq > 3 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_batch: bad nq/B");
+  if (B == 0) return VBOC_OK;
+  if (!x || !u || !x_out) return fail(VBOC_ERR_ARG, "vboc_rk4_batch: NULL array");
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((B + 255) / 256), block(256);
+  switch (nq) {
+    case 1: hipLaunchKernelGGL(rk4_kernel<1>, grid, block, 0, st, B, T, x, u, x_out); break;
+    case 2: hipLaunchKernelGGL(rk4_kernel<2>, grid, block, 0, st, B, T, x, u, x_out); break;
+    default: hipLaunchKernelGGL(rk4_kernel<3>, grid, block, 0, st, B, T, x, u, x_out); break;
+  }
+  HIPCHK(hipGetLastError());
+  return VBOC_OK;
+}
+
+int vboc_rk4_batch_host(int nq, int B, double T, const double* x, const double* u, double* x_out) {
+  if (nq < 1 || nq > 3 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_batch_host: bad nq/B");
+  if (B == 0) return VBOC_OK;
+  const size_t nx = 2 * nq;
+  double *dx = nullptr, *du = nullptr, *dxo = nullptr;
+  HIPCHK(hipMalloc(&dx, B * nx * sizeof(double)));
+  HIPCHK(hipMalloc(&du, B * nq * sizeof(double)));
+  HIPCHK(hipMalloc(&dxo, B * nx * sizeof(double)));
+  HIPCHK(hipMemcpy(dx, x, B * nx * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(du, u, B * nq * sizeof(double), hipMemcpyHostToDevice));
+  int rc = vboc_rk4_batch(nq, B, T, dx, du, dxo, nullptr);
+  if (rc == 0) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(x_out, dxo, B * nx * sizeof(double), hipMemcpyDeviceToHost));
+  }
+  (void)hipFree(dx);
+  (void)hipFree(du);
+  (void)hipFree(dxo);
+  return rc;
+}
+
+}  // extern "C"

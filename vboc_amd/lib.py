@@ -1,0 +1,191 @@
+"""ctypes binding of libvboc_amd.so (the C ABI declared in include/vboc.h).
+
+The product path: every solve goes through the HIP library.  There is no CPU fallback - if the
+library is missing or cannot be loaded, `load()` raises.  PyTorch is used only for device memory
+and streams (`solve_device`).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libvboc_amd.so")
+SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
+
+EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
+           "vboc_solve_batch_host", "vboc_rk4_batch", "vboc_rk4_batch_host", "vboc_last_kernel_ms",
+           "vboc_last_error")
+
+STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure"}
+
+
+class VbocError(RuntimeError):
+    pass
+
+
+class Batch(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("nmax", ctypes.c_int), ("N", ctypes.c_void_p),
+                ("x_guess", ctypes.c_void_p), ("u_guess", ctypes.c_void_p), ("p", ctypes.c_void_p),
+                ("lbx", ctypes.c_void_p), ("ubx", ctypes.c_void_p), ("lbu", ctypes.c_void_p),
+                ("ubu", ctypes.c_void_p), ("lbx_0", ctypes.c_void_p), ("ubx_0", ctypes.c_void_p),
+                ("lbx_e", ctypes.c_void_p), ("ubx_e", ctypes.c_void_p), ("status", ctypes.c_void_p),
+                ("x_out", ctypes.c_void_p), ("u_out", ctypes.c_void_p), ("cost", ctypes.c_void_p),
+                ("sqp_iter", ctypes.c_void_p), ("qp_iter", ctypes.c_void_p)]
+
+
+def build(verbose=False):
+    """hipcc the solver for gfx950 into vboc_amd/libvboc_amd.so (in-tree)."""
+    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-o", LIB_PATH, SRC]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise VbocError(f"{LIB_PATH} not built - run __graft_entry__.build() (no CPU fallback exists)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name in EXPORTS:
+        getattr(lib, name)  # raises AttributeError if a symbol is missing
+    lib.vboc_last_error.restype = ctypes.c_char_p
+    lib.vboc_create.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_void_p)]
+    lib.vboc_destroy.argtypes = [ctypes.c_void_p]
+    lib.vboc_set_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_double]
+    lib.vboc_get_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
+    lib.vboc_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch), ctypes.c_void_p]
+    lib.vboc_solve_batch_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch)]
+    lib.vboc_rk4_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.vboc_rk4_batch_host.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p]
+    lib.vboc_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_int)]
+    _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise VbocError(f"vboc error {rc}: {load().vboc_last_error().decode()}")
+
+
+FIELDS_IN = ("x_guess", "u_guess", "p", "lbx", "ubx", "lbu", "ubu", "lbx0", "ubx0", "lbxe", "ubxe")
+_CFIELD = {"lbx0": "lbx_0", "ubx0": "ubx_0", "lbxe": "lbx_e", "ubxe": "ubx_e"}
+
+
+class Solver:
+    """One HIP solver handle (one device, horizons up to nmax)."""
+
+    def __init__(self, nq, nmax, slots=0, device=0, **options):
+        self.lib = load()
+        self.nq, self.nmax = int(nq), int(nmax)
+        h = ctypes.c_void_p()
+        _check(self.lib.vboc_create(self.nq, self.nmax, int(slots), int(device), ctypes.byref(h)))
+        self.h = h
+        self.device = device
+        for k, v in options.items():
+            self.set_option(k, v)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.vboc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, field, value):
+        _check(self.lib.vboc_set_option(self.h, field.encode(), float(value)))
+
+    def get_option(self, field):
+        v = ctypes.c_double()
+        _check(self.lib.vboc_get_option(self.h, field.encode(), ctypes.byref(v)))
+        return v.value
+
+    # -- host path --------------------------------------------------------------------------------
+    def solve_host(self, batch):
+        """batch: dict with N, x_guess[B,nmax+1,nx], u_guess[B,nmax,nu], p, bounds (ics.Batch).
+        Returns dict(status, x, u, cost, sqp_iter, qp_iter)."""
+        N = np.ascontiguousarray(batch["N"], dtype=np.int32)
+        B = N.shape[0]
+        arrs = {k: np.ascontiguousarray(batch[k], dtype=np.float64) for k in FIELDS_IN}
+        nmax = arrs["x_guess"].shape[1] - 1
+        x_out = np.array(arrs["x_guess"], copy=True)
+        u_out = np.array(arrs["u_guess"], copy=True)
+        status = np.zeros(B, np.int32)
+        sqp_iter = np.zeros(B, np.int32)
+        qp_iter = np.zeros(B, np.int32)
+        cost = np.zeros(B, np.float64)
+        b = Batch(B=B, nmax=nmax, N=N.ctypes.data, status=status.ctypes.data,
+                  x_out=x_out.ctypes.data, u_out=u_out.ctypes.data, cost=cost.ctypes.data,
+                  sqp_iter=sqp_iter.ctypes.data, qp_iter=qp_iter.ctypes.data)
+        for k, a in arrs.items():
+            setattr(b, _CFIELD.get(k, k), a.ctypes.data)
+        _check(self.lib.vboc_solve_batch_host(self.h, ctypes.byref(b)))
+        return dict(status=status, x=x_out, u=u_out, cost=cost, sqp_iter=sqp_iter, qp_iter=qp_iter)
+
+    # -- device path (torch tensors resident in HBM) ---------------------------------------------
+    def solve_device(self, tb, out=None, stream=None):
+        """tb: dict of torch cuda tensors (float64 / int32 for N).  Asynchronous on `stream`
+        (default: torch's current stream).  Returns the output tensor dict."""
+        import torch
+        N = tb["N"]
+        B = N.shape[0]
+        nmax = tb["x_guess"].shape[1] - 1
+        if out is None:
+            out = dict(x=tb["x_guess"].clone(), u=tb["u_guess"].clone(),
+                       status=torch.empty(B, dtype=torch.int32, device=N.device),
+                       cost=torch.empty(B, dtype=torch.float64, device=N.device),
+                       sqp_iter=torch.empty(B, dtype=torch.int32, device=N.device),
+                       qp_iter=torch.empty(B, dtype=torch.int32, device=N.device))
+        b = Batch(B=B, nmax=nmax, N=N.data_ptr(), status=out["status"].data_ptr(),
+                  x_out=out["x"].data_ptr(), u_out=out["u"].data_ptr(), cost=out["cost"].data_ptr(),
+                  sqp_iter=out["sqp_iter"].data_ptr(), qp_iter=out["qp_iter"].data_ptr())
+        for k in FIELDS_IN:
+            t = tb[k]
+            assert t.is_cuda and t.dtype == torch.float64 and t.is_contiguous(), k
+            setattr(b, _CFIELD.get(k, k), t.data_ptr())
+        st = stream if stream is not None else torch.cuda.current_stream()
+        _check(self.lib.vboc_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        return out
+
+    def last_kernel_ms(self):
+        ms = ctypes.c_double()
+        n = ctypes.c_int()
+        _check(self.lib.vboc_last_kernel_ms(self.h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+
+def rk4_host(nq, T, x, u):
+    lib = load()
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    B = x.shape[0]
+    xo = np.zeros_like(x)
+    _check(lib.vboc_rk4_batch_host(int(nq), B, float(T), x.ctypes.data, u.ctypes.data, xo.ctypes.data))
+    return xo
+
+
+def rk4_device(nq, T, x, u, stream=None):
+    import torch
+    lib = load()
+    xo = torch.empty_like(x)
+    st = stream if stream is not None else torch.cuda.current_stream()
+    _check(lib.vboc_rk4_batch(int(nq), x.shape[0], float(T), x.data_ptr(), u.data_ptr(), xo.data_ptr(),
+                              ctypes.c_void_p(st.cuda_stream)))
+    return xo
