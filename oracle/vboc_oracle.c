@@ -578,7 +578,12 @@ static int newton_solve(prob_t* P, int factor, double* nu_new) {
 /* interior-point QP                                                                           */
 /* ------------------------------------------------------------------------------------------ */
 
-static double step_to_boundary(double t, double dt) { return dt < 0.0 ? -t / dt : INFINITY; }
+/* fraction-to-boundary ratio test: running minimum of t / (-dt) over dt < 0, kept as n / d so
+   that only the winning ratio is divided (the GPU kernel uses the same comparison) */
+typedef struct { double n, d; } minratio_t;
+static void mr_add(minratio_t* m, double t, double dt) {
+  if (dt < 0.0 && t * m->d < m->n * (-dt)) { m->n = t; m->d = -dt; }
+}
 
 /* returns 0 converged, 1 max-iter (usable step), -1 failure */
 static int qp_solve(prob_t* P, int* iters) {
@@ -653,34 +658,35 @@ static int qp_solve(prob_t* P, int* iters) {
       for (int i = 0; i < nz_of(P, k); ++i) {
         double H = rho, g = rho * s->dz[i] + cost_grad(P, k, i);
         if (isfinite(s->Lb[i])) {
-          double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i];
-          H += s->ql[i] / tl + s->qu[i] / tu;
+          double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu;
+          H += s->ql[i] * itl + s->qu[i] * itu;
         }
         s->H[i] = H; s->g[i] = g;
       }
     }
     if (newton_solve(P, 1, nu_new)) { status = -1; break; }
-    double aa = 1.0;
+    minratio_t ma = {1.0, 1.0};
     for (int k = 0; k <= N; ++k) {
       stage_t* s = &P->st[k];
       for (int i = 0; i < nz_of(P, k); ++i) {
         s->daff[i] = s->d[i];
         if (!isfinite(s->Lb[i])) continue;
-        double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], d = s->d[i];
-        double dll = -s->ql[i] - s->ql[i] * d / tl, dlu = -s->qu[i] + s->qu[i] * d / tu;
-        aa = fmin(aa, step_to_boundary(tl, d));
-        aa = fmin(aa, step_to_boundary(tu, -d));
-        aa = fmin(aa, step_to_boundary(s->ql[i], dll));
-        aa = fmin(aa, step_to_boundary(s->qu[i], dlu));
+        double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu, d = s->d[i];
+        double dll = -s->ql[i] - s->ql[i] * d * itl, dlu = -s->qu[i] + s->qu[i] * d * itu;
+        mr_add(&ma, tl, d);
+        mr_add(&ma, tu, -d);
+        mr_add(&ma, s->ql[i], dll);
+        mr_add(&ma, s->qu[i], dlu);
       }
     }
+    const double aa = ma.n / ma.d;
     double muaff = 0.0;
     for (int k = 0; k <= N; ++k) {
       stage_t* s = &P->st[k];
       for (int i = 0; i < nz_of(P, k); ++i) {
         if (!isfinite(s->Lb[i])) continue;
-        double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], d = s->d[i];
-        double dll = -s->ql[i] - s->ql[i] * d / tl, dlu = -s->qu[i] + s->qu[i] * d / tu;
+        double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu, d = s->d[i];
+        double dll = -s->ql[i] - s->ql[i] * d * itl, dlu = -s->qu[i] + s->qu[i] * d * itu;
         muaff += (tl + aa * d) * (s->ql[i] + aa * dll) + (tu - aa * d) * (s->qu[i] + aa * dlu);
       }
     }
@@ -694,41 +700,42 @@ static int qp_solve(prob_t* P, int* iters) {
       stage_t* s = &P->st[k];
       for (int i = 0; i < nz_of(P, k); ++i) {
         if (!isfinite(s->Lb[i])) continue;
-        double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], d = s->daff[i];
-        double dll = -s->ql[i] - s->ql[i] * d / tl, dlu = -s->qu[i] + s->qu[i] * d / tu;
+        double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu, d = s->daff[i];
+        double dll = -s->ql[i] - s->ql[i] * d * itl, dlu = -s->qu[i] + s->qu[i] * d * itu;
         double rl = smu - tl * s->ql[i] - d * dll;
         double ru = smu - tu * s->qu[i] + d * dlu;
-        s->g[i] = rho * s->dz[i] + cost_grad(P, k, i) - s->ql[i] - rl / tl + s->qu[i] + ru / tu;
+        s->g[i] = rho * s->dz[i] + cost_grad(P, k, i) - s->ql[i] - rl * itl + s->qu[i] + ru * itu;
       }
     }
     if (newton_solve(P, 0, nu_new)) { status = -1; break; }
-    double amax = 1.0 / o->ipm_tau;
+    minratio_t mx = {1.0, o->ipm_tau};
     for (int k = 0; k <= N; ++k) {
       stage_t* s = &P->st[k];
       for (int i = 0; i < nz_of(P, k); ++i) {
         if (!isfinite(s->Lb[i])) continue;
-        double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], d = s->d[i], da = s->daff[i];
-        double dlla = -s->ql[i] - s->ql[i] * da / tl, dlua = -s->qu[i] + s->qu[i] * da / tu;
+        double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu, d = s->d[i], da = s->daff[i];
+        double dlla = -s->ql[i] - s->ql[i] * da * itl, dlua = -s->qu[i] + s->qu[i] * da * itu;
         double rl = smu - tl * s->ql[i] - da * dlla;
         double ru = smu - tu * s->qu[i] + da * dlua;
-        double dll = (rl - s->ql[i] * d) / tl, dlu = (ru + s->qu[i] * d) / tu;
-        amax = fmin(amax, step_to_boundary(tl, d));
-        amax = fmin(amax, step_to_boundary(tu, -d));
-        amax = fmin(amax, step_to_boundary(s->ql[i], dll));
-        amax = fmin(amax, step_to_boundary(s->qu[i], dlu));
+        double dll = (rl - s->ql[i] * d) * itl, dlu = (ru + s->qu[i] * d) * itu;
+        mr_add(&mx, tl, d);
+        mr_add(&mx, tu, -d);
+        mr_add(&mx, s->ql[i], dll);
+        mr_add(&mx, s->qu[i], dlu);
       }
     }
+    const double amax = mx.n / mx.d;
     double alpha = fmin(1.0, o->ipm_tau * amax);
     for (int k = 0; k <= N; ++k) {
       stage_t* s = &P->st[k];
       for (int i = 0; i < nz_of(P, k); ++i) {
         double d = s->d[i];
         if (isfinite(s->Lb[i])) {
-          double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], da = s->daff[i];
-          double dlla = -s->ql[i] - s->ql[i] * da / tl, dlua = -s->qu[i] + s->qu[i] * da / tu;
+          double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu, da = s->daff[i];
+          double dlla = -s->ql[i] - s->ql[i] * da * itl, dlua = -s->qu[i] + s->qu[i] * da * itu;
           double rl = smu - tl * s->ql[i] - da * dlla;
           double ru = smu - tu * s->qu[i] + da * dlua;
-          double dll = (rl - s->ql[i] * d) / tl, dlu = (ru + s->qu[i] * d) / tu;
+          double dll = (rl - s->ql[i] * d) * itl, dlu = (ru + s->qu[i] * d) * itu;
           s->ql[i] += alpha * dll;
           s->qu[i] += alpha * dlu;
         }

@@ -1,0 +1,32 @@
+"""Throughput probe: one batched solve at several sizes (diagnostic)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from vboc_amd import lib  # noqa: E402
+from vboc_amd.ics import data_generation_ics, heldout_ics  # noqa: E402
+
+nq = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [4096]
+slots = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+law = sys.argv[4] if len(sys.argv) > 4 else "dg"
+max_iter = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+for B in sizes:
+    b = (data_generation_ics if law == "dg" else heldout_ics)(nq, np.arange(B))
+    s = lib.Solver(nq, int(b["N"].max()), slots=slots)
+    if max_iter:
+        s.set_option("nlp_solver_max_iter", max_iter)
+    t = time.time()
+    g = s.solve_host(b)
+    tw = time.time() - t
+    ms, nl = s.last_kernel_ms()
+    it = g["sqp_iter"]
+    print(f"nq={nq} law={law} B={B} slots={s.get_option('slots'):.0f}: wall {tw:.2f}s device {ms:.1f} ms "
+          f"launches {nl} -> {B / (ms / 1e3):.0f} solves/s | ok {np.mean(g['status'] == 0):.4f} "
+          f"sqp mean {it.mean():.1f} p99 {np.percentile(it, 99):.0f} max {it.max()} | qp/sqp "
+          f"{g['qp_iter'].sum() / max(1, it.sum()):.1f}", flush=True)
+    s.close()

@@ -15,6 +15,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#ifndef VBOC_SENS_GROUP
+#define VBOC_SENS_GROUP 1
+#endif
+
 namespace vboc {
 
 template <int NQ>
@@ -181,25 +185,112 @@ __device__ __forceinline__ void rk4(double h, const double* x, const double* u, 
   for (int i = 0; i < NX; ++i) x1[i] = x[i] + h / 6.0 * (acc[i] + k[i]);
 }
 
+// Nominal model quantities at one point, reused by Jacobian-vector products (JVP) along
+// tangent directions: the sensitivities never form the Jacobian (lower register pressure).
+template <int NQ>
+struct ModelPoint {
+  double L[NQ * NQ];       // Cholesky factor of M(theta) (chain) / unused (pendulum)
+  double sd[NQ][NQ];       // sin(th_j - th_k)
+  double cd[NQ][NQ];       // cos(th_j - th_k)
+  double cth[NQ];          // cos th_j
+  double acc[NQ], om[NQ];
+};
+
+template <int NQ>
+__device__ __forceinline__ void model_point(const double* th, const double* om, const double* u, ModelPoint<NQ>& mp) {
+  if constexpr (NQ == 1) {
+    constexpr double pm = 0.5, pd = 0.3, pb = 0.01, g = 9.81;
+    constexpr double inv = 1.0 / (pd * pd * pm);
+    double sn, cs;
+    sincos(th[0], &sn, &cs);
+    mp.cth[0] = cs;
+    mp.om[0] = om[0];
+    mp.acc[0] = (pm * g * pd * sn + u[0] - pb * om[0]) * inv;
+  } else {
+    using C = Chain<NQ>;
+    double sth[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) { sincos(th[j], &sth[j], &mp.cth[j]); mp.om[j] = om[j]; }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      mp.sd[j][j] = 0.0;
+      mp.cd[j][j] = 1.0;
+#pragma unroll
+      for (int k = 0; k < j; ++k) {
+        const double sv = sth[j] * mp.cth[k] - mp.cth[j] * sth[k];
+        const double cv = mp.cth[j] * mp.cth[k] + sth[j] * sth[k];
+        mp.sd[j][k] = sv; mp.sd[k][j] = -sv;
+        mp.cd[j][k] = cv; mp.cd[k][j] = cv;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NQ; ++j)
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) mp.L[j * NQ + k] = C::a(j, k) * mp.cd[j][k];
+    chol<NQ>(mp.L);
+    double r[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      double cor = 0.0;
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) cor += C::a(j, k) * mp.sd[j][k] * om[k] * om[k];
+      r[j] = u[j] - cor - C::g * C::mu(j) * C::l * sth[j];
+    }
+    chol_solve<NQ>(mp.L, r);
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) mp.acc[j] = r[j];
+  }
+}
+
+// d acc along (dth, dom, du):  M^-1 (du - dcor - dgrav - dM acc)
+template <int NQ>
+__device__ __forceinline__ void model_jvp(const ModelPoint<NQ>& mp, const double* dth, const double* dom,
+                                          const double* du, double* dacc) {
+  if constexpr (NQ == 1) {
+    constexpr double pm = 0.5, pd = 0.3, pb = 0.01, g = 9.81;
+    constexpr double inv = 1.0 / (pd * pd * pm);
+    dacc[0] = (pm * g * pd * mp.cth[0] * dth[0] + du[0] - pb * dom[0]) * inv;
+  } else {
+    using C = Chain<NQ>;
+    double r[NQ];
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) {
+      double t = du[j] - C::g * C::mu(j) * C::l * mp.cth[j] * dth[j];
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) {
+        if (k == j) continue;
+        const double dd = dth[j] - dth[k];
+        t -= C::a(j, k) * (mp.cd[j][k] * dd * mp.om[k] * mp.om[k] + 2.0 * mp.sd[j][k] * mp.om[k] * dom[k]);
+        t += C::a(j, k) * mp.sd[j][k] * dd * mp.acc[k];
+      }
+      r[j] = t;
+    }
+    chol_solve<NQ>(mp.L, r);
+#pragma unroll
+    for (int j = 0; j < NQ; ++j) dacc[j] = r[j];
+  }
+}
+
 // RK4 step with forward sensitivities = exact derivative of the discrete map (ACADOS ERK
-// forward VDE).  Sensitivity columns are propagated in groups of NQ directions (theta block,
-// omega block, u block) to bound register pressure; each group re-runs the nominal stages.
-// Outputs x1 (NX); sensitivity entry (i, c), c < NX for A = dx1/dx, c >= NX for B = dx1/du, is
-// handed to store(i, c, value) (the caller writes it straight to its HBM slot).
-template <int NQ, class Store>
-__device__ __forceinline__ void rk4_sens(double h, const double* x, const double* u, double* x1, Store store) {
-  constexpr int NX = 2 * NQ;
+// forward VDE).  The NX + NU sensitivity columns are propagated as Jacobian-vector products in
+// groups of G tangent directions; each group re-runs the nominal stages (more arithmetic, far
+// fewer live registers - the sweep is latency-bound, not FLOP-bound).  Outputs x1 (NX);
+// sensitivity entry (i, c), c < NX for A = dx1/dx, c >= NX for B = dx1/du -> store(i, c, v).
+template <int NQ, int G, class Store>
+__device__ __forceinline__ void rk4_sens_g(double h, const double* x, const double* u, double* x1, Store store) {
+  constexpr int NX = 2 * NQ, NC = NX + NQ, NG = NC / G;
+  static_assert(NC % G == 0, "group size must divide the column count");
 #pragma unroll 1
-  for (int grp = 0; grp < 3; ++grp) {
-    // tangent T (NX x NQ): columns of d X / d (x_grp or u)
-    double T[NX][NQ], Ts[NX][NQ], X[NX], ks[NX];
+  for (int grp = 0; grp < NG; ++grp) {
+    const int c0 = grp * G;
+    double T[NX][G], Ts[NX][G], X[NX], ks[NX];
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
       X[i] = x[i];
       ks[i] = 0.0;
 #pragma unroll
-      for (int c = 0; c < NQ; ++c) {
-        T[i][c] = (grp < 2 && i == grp * NQ + c) ? 1.0 : 0.0;
+      for (int c = 0; c < G; ++c) {
+        T[i][c] = (i == c0 + c) ? 1.0 : 0.0;
         Ts[i][c] = 0.0;
       }
     }
@@ -207,34 +298,37 @@ __device__ __forceinline__ void rk4_sens(double h, const double* x, const double
     for (int st = 0; st < 4; ++st) {
       const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
       const double cnext = (st < 2) ? 0.5 * h : h;
-      double k[NX], Jth[NQ * NQ], Jom[NQ * NQ], Ju[NQ * NQ];
+      ModelPoint<NQ> mp;
+      model_point<NQ>(X, X + NQ, u, mp);
+      double k[NX];
 #pragma unroll
-      for (int j = 0; j < NQ; ++j) k[j] = X[NQ + j];
-      model_eval<NQ, true>(X, X + NQ, u, k + NQ, Jth, Jom, Ju);
-      double dk[NX][NQ];
+      for (int j = 0; j < NQ; ++j) { k[j] = X[NQ + j]; k[NQ + j] = mp.acc[j]; }
+      double dk[NX][G];
 #pragma unroll
-      for (int j = 0; j < NQ; ++j)
+      for (int c = 0; c < G; ++c) {
+        double dth[NQ], dom[NQ], du[NQ], da[NQ];
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-          dk[j][c] = T[NQ + j][c];
-          double t = (grp == 2 ? Ju[j * NQ + c] : 0.0);
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) t += Jth[j * NQ + q] * T[q][c] + Jom[j * NQ + q] * T[NQ + q][c];
-          dk[NQ + j][c] = t;
+        for (int j = 0; j < NQ; ++j) {
+          dth[j] = T[j][c];
+          dom[j] = T[NQ + j][c];
+          du[j] = (c0 + c == NX + j) ? 1.0 : 0.0;
         }
+        model_jvp<NQ>(mp, dth, dom, du, da);
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) { dk[j][c] = dom[j]; dk[NQ + j][c] = da[j]; }
+      }
 #pragma unroll
       for (int i = 0; i < NX; ++i) {
         ks[i] += wgt * k[i];
 #pragma unroll
-        for (int c = 0; c < NQ; ++c) Ts[i][c] += wgt * dk[i][c];
+        for (int c = 0; c < G; ++c) Ts[i][c] += wgt * dk[i][c];
       }
       if (st < 3) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
           X[i] = x[i] + cnext * k[i];
 #pragma unroll
-          for (int c = 0; c < NQ; ++c)
-            T[i][c] = ((grp < 2 && i == grp * NQ + c) ? 1.0 : 0.0) + cnext * dk[i][c];
+          for (int c = 0; c < G; ++c) T[i][c] = ((i == c0 + c) ? 1.0 : 0.0) + cnext * dk[i][c];
         }
       }
     }
@@ -245,12 +339,14 @@ __device__ __forceinline__ void rk4_sens(double h, const double* x, const double
 #pragma unroll
     for (int i = 0; i < NX; ++i) {
 #pragma unroll
-      for (int c = 0; c < NQ; ++c) {
-        const double v = ((grp < 2 && i == grp * NQ + c) ? 1.0 : 0.0) + h / 6.0 * Ts[i][c];
-        store(i, grp * NQ + c, v);
-      }
+      for (int c = 0; c < G; ++c) store(i, c0 + c, ((i == c0 + c) ? 1.0 : 0.0) + h / 6.0 * Ts[i][c]);
     }
   }
+}
+
+template <int NQ, class Store>
+__device__ __forceinline__ void rk4_sens(double h, const double* x, const double* u, double* x1, Store store) {
+  rk4_sens_g<NQ, VBOC_SENS_GROUP, Store>(h, x, u, x1, store);
 }
 
 }  // namespace vboc

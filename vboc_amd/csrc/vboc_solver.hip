@@ -31,6 +31,11 @@
 #include "model.h"
 
 #define UNR _Pragma("unroll")
+#ifdef VBOC_WAVES
+#define VBOC_WPE __attribute__((amdgpu_waves_per_eu(VBOC_WAVES, VBOC_WAVES)))
+#else
+#define VBOC_WPE
+#endif
 
 namespace vboc {
 
@@ -68,18 +73,27 @@ struct Par {
   enum : int {
     H = 0, Q0 = 1, DIR = Q0 + NQ, SLB = DIR + NQ, SUB, CS, CCONST, XLB, XUB = XLB + NX, ULB = XUB + NX,
     UUB = ULB + NU, QNLB = UUB + NU, QNUB = QNLB + NQ, VFIN = QNUB + NQ, S = VFIN + NQ, NU_ = S + 1,
-    WNU = NU_ + NQ, WBND = WNU + NQ, E0N = WBND + 1, QNU = E0N + NQ, COUNT = QNU + NQ
+    WNU = NU_ + NQ, WBND = WNU + NQ, E0N = WBND + 1, QNU = E0N + NQ,
+    // interior-point scalars carried between the per-sweep kernels
+    RS = QNU + NQ, RD0, E00, MU, NBOX, SMU, ALPHA, SC, LINE = SC + NQ * NQ, W0 = LINE + NQ, NUN = W0 + NQ + 1,
+    COUNT = NUN + NQ
   };
 };
 
 // Force a wave-uniform pointer into SGPRs.  Opaque to loop strength reduction, so each access
 // becomes `global_load ... vOFF, s[base]` with ONE shared per-lane offset register instead of a
 // 64-bit per-field VGPR induction pointer.  Only for pointers that ARE uniform.
-__device__ __forceinline__ double* uptr(double* p) {
+// Global-address-space double: loads/stores through it are `global_*` (never `flat_*`, which
+// would be ordered against LDS/scratch and drained with vmcnt(0) lgkmcnt(0) one by one).
+typedef __attribute__((address_space(1))) double gdouble;
+
+__device__ __forceinline__ gdouble* gptr(double* p) { return (gdouble*)(unsigned long long)p; }
+
+__device__ __forceinline__ gdouble* uptr(double* p) {
   const unsigned long long v = (unsigned long long)p;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  return (double*)(((unsigned long long)hi << 32) | lo);
+  return (gdouble*)(((unsigned long long)hi << 32) | lo);
 }
 
 __device__ __forceinline__ int wave_max(int v) {
@@ -97,27 +111,42 @@ struct Lane {
   const Work& w;
   const Opts& o;
   const unsigned slot;
+  const int wv;   // wave index (wave-uniform, SGPR)
+  const int ln;   // lane in wave
   int N;    // this lane's horizon
   int Nw;   // wave-uniform: largest horizon of the wave's active lanes (SGPR)
   // QP scalars (registers only while the QP runs)
   double rs, rd0, e00, mu, nbox;
 
-  __device__ Lane(const Work& w_, const Opts& o_, unsigned slot_) : w(w_), o(o_), slot(slot_), N(0), Nw(0) {}
+  __device__ Lane(const Work& w_, const Opts& o_, unsigned slot_)
+      : w(w_), o(o_), slot(slot_), wv(__builtin_amdgcn_readfirstlane((int)(slot_ >> 6))), ln((int)(slot_ & 63u)),
+        N(0), Nw(0) {}
 
-  // k wave-uniform -> SGPR address + one VGPR offset
-  __device__ __forceinline__ double& at(double* base, int F, int k, int f) const {
-    return uptr(base + ((long long)k * F + f) * w.S)[slot];
+  // Wave-tiled, field-paired SoA: element (stage k, field f) of lane `ln` of wave `wv` lives at
+  //   base[((k * SW + wv) * FP + f / 2) * 128 + ln * 2 + f % 2],  SW = S / 64, FP = ceil(F / 2).
+  // A wave-instruction covering fields (2p, 2p+1) reads 64 x 16 B = 1 KiB contiguous
+  // (global_load_dwordx4), and one base register per (array, stage) serves 8 fields through
+  // immediate offsets.
+  static constexpr int fp(int F) { return (F + 1) / 2; }
+  __device__ __forceinline__ gdouble* stage_base(double* base, int F, int k) const {
+    return gptr(base) + (((long long)k * (w.S >> 6) + wv) * fp(F)) * 128 + ln * 2;
   }
-  // k per lane (the terminal stage N)
-  __device__ __forceinline__ double& atv(double* base, int F, int k, int f) const {
-    return (base + ((long long)k * F + f) * w.S)[slot];
+  __device__ __forceinline__ gdouble& at(double* base, int F, int k, int f) const {
+    return stage_base(base, F, k)[(f >> 1) * 128 + (f & 1)];
+  }
+  // k per lane (the terminal stage N) - same formula, per-lane arithmetic
+  __device__ __forceinline__ gdouble& atv(double* base, int F, int k, int f) const {
+    return stage_base(base, F, k)[(f >> 1) * 128 + (f & 1)];
   }
   template <bool U>
-  __device__ __forceinline__ double& atk(double* base, int F, int k, int f) const {
-    return U ? at(base, F, k, f) : atv(base, F, k, f);
+  __device__ __forceinline__ gdouble& atk(double* base, int F, int k, int f) const {
+    return stage_base(base, F, k)[(f >> 1) * 128 + (f & 1)];
   }
-  __device__ __forceinline__ double& at0(double* base, int f) const { return uptr(base + (long long)f * w.S)[slot]; }
-  __device__ __forceinline__ double& par(int f) const { return at0(w.PAR, f); }
+  // per-slot arrays (no stage index)
+  __device__ __forceinline__ gdouble& at0(double* base, int F, int f) const {
+    return (gptr(base) + ((long long)wv * fp(F)) * 128 + ln * 2)[(f >> 1) * 128 + (f & 1)];
+  }
+  __device__ __forceinline__ gdouble& par(int f) const { return at0(w.PAR, PF::COUNT, f); }
 
   // ---------------------------------------------------------------------------------------------
   // stage component view: value, bounds, boxed flag of the NZ step components of stage k
@@ -197,17 +226,11 @@ struct Lane {
     UNR for (int j = 0; j < NQ; ++j) s += dir[j] * xg[NQ + j];
     par(PF::S) = s;
     for (int k = 0; k <= N; ++k) {
-      double* X = w.X + (long long)k * FX * w.S + slot;
-      double* LL = w.LL + (long long)k * FZ * w.S + slot;
-      double* LU = w.LU + (long long)k * FZ * w.S + slot;
-      UNR for (int i = 0; i < NX; ++i) X[i * w.S] = xg[(long long)k * NXR + i];
-      UNR for (int i = 0; i < NZ; ++i) { LL[i * w.S] = 0.0; LU[i * w.S] = 0.0; }
+      UNR for (int i = 0; i < NX; ++i) atv(w.X, FX, k, i) = xg[(long long)k * NXR + i];
+      UNR for (int i = 0; i < NZ; ++i) { atv(w.LL, FZ, k, i) = 0.0; atv(w.LU, FZ, k, i) = 0.0; }
       if (k < N) {
-        double* U = w.U + (long long)k * FU * w.S + slot;
-        double* PI = w.PI + (long long)k * FPI * w.S + slot;
-        double* WPI = w.WPI + (long long)k * FX * w.S + slot;
-        UNR for (int a = 0; a < NU; ++a) U[a * w.S] = ug[(long long)k * NU + a];
-        UNR for (int i = 0; i < NX; ++i) { PI[i * w.S] = 0.0; WPI[i * w.S] = 0.0; }
+        UNR for (int a = 0; a < NU; ++a) atv(w.U, FU, k, a) = ug[(long long)k * NU + a];
+        UNR for (int i = 0; i < NX; ++i) { atv(w.PI, FPI, k, i) = 0.0; atv(w.WPI, FX, k, i) = 0.0; }
       }
     }
   }
@@ -218,16 +241,14 @@ struct Lane {
     double* uo = in.uo + (long long)pid * in.nmax * NU;
     const double s = par(PF::S), h = par(PF::H);
     for (int k = 0; k <= N; ++k) {
-      const double* X = w.X + (long long)k * FX * w.S + slot;
       UNR for (int i = 0; i < NX; ++i) {
         const double v = (k == 0) ? (i < NQ ? par(PF::Q0 + i) : s * par(PF::DIR + (i - NQ + (i < NQ ? NQ : 0))))
-                                  : X[i * w.S];
+                                  : (double)atv(w.X, FX, k, i);
         xo[(long long)k * NXR + i] = v;
       }
       xo[(long long)k * NXR + NX] = h;
       if (k < N) {
-        const double* U = w.U + (long long)k * FU * w.S + slot;
-        UNR for (int a = 0; a < NU; ++a) uo[(long long)k * NU + a] = U[a * w.S];
+        UNR for (int a = 0; a < NU; ++a) uo[(long long)k * NU + a] = atv(w.U, FU, k, a);
       }
     }
     in.status[pid] = status;
@@ -241,12 +262,10 @@ struct Lane {
   }
 
   // ---------------------------------------------------------------------------------------------
-  // linearisation (ERK4 + sensitivities, defects) fused with the NLP residuals
+  // linearisation: sweep 1 = ERK4 + sensitivities + defects, sweep 2 = NLP residuals
   // ---------------------------------------------------------------------------------------------
-  __device__ void linearize(double& rstat, double& req, double& rineq, double& rcomp) {
-    double st = 0, eq = 0, in = 0, cp = 0;
+  __device__ void sens() {
     const double h = par(PF::H);
-    // sweep 1: ERK4 + sensitivities, defects (registers: integrator only)
     {
       double xk[NX];
       x0_of(xk, par(PF::S));
@@ -255,6 +274,8 @@ struct Lane {
         double uk[NU], x1[NX];
         UNR for (int a = 0; a < NU; ++a) uk[a] = at(w.U, FU, k, a);
         rk4_sens<NQ>(h, xk, uk, x1, [&](int i, int c, double v) {
+          // A (NX x NX) and B (NX x NU) are adjacent per stage in column-major-of-(i,c) order
+          // through two field tables; c is wave-uniform so the select stays scalar.
           if (c < NX) at(w.A, FA, k, i * NX + c) = v;
           else at(w.Bm, FB, k, i * NU + (c - NX)) = v;
         });
@@ -262,18 +283,24 @@ struct Lane {
           const double xn = at(w.X, FX, k + 1, i);
           const double b = x1[i] - xn;
           at(w.BD, FX, k, i) = b;
-          eq = fmax(eq, fabs(b));
           xk[i] = xn;
         }
       }
     }
-    // sweep 2: NLP residuals with the current multipliers
+  }
+
+  // sweep 2: NLP residuals with the current multipliers (defects from sweep 1)
+  __device__ void residuals(double& rstat, double& req, double& rineq, double& rcomp) {
+    double st = 0, eq = 0, in = 0, cp = 0;
     double pprev[NX];
     UNR for (int i = 0; i < NX; ++i) pprev[i] = 0.0;
     for (int k = 0; k < Nw; ++k) {
       if (k >= N) continue;
       double pik[NX];
-      UNR for (int i = 0; i < NX; ++i) pik[i] = at(w.PI, FPI, k, i);
+      UNR for (int i = 0; i < NX; ++i) {
+        pik[i] = at(w.PI, FPI, k, i);
+        eq = fmax(eq, fabs((double)at(w.BD, FX, k, i)));
+      }
       double z[NZ], lb[NZ], ub[NZ];
       bool bx[NZ];
       stage_box(k, z, lb, ub, bx);
@@ -282,12 +309,12 @@ struct Lane {
         UNR for (int i = 0; i < NX; ++i) {
           double t = 0.0;
           UNR for (int j = 0; j < NQ; ++j) t += at(w.A, FA, 0, i * NX + NQ + j) * par(PF::DIR + j);
-          at0(w.F0, i * M0) = t;
-          UNR for (int a = 0; a < NU; ++a) at0(w.F0, i * M0 + 1 + a) = at(w.Bm, FB, 0, i * NU + a);
+          at0(w.F0, NX * M0, i * M0) = t;
+          UNR for (int a = 0; a < NU; ++a) at0(w.F0, NX * M0, i * M0 + 1 + a) = at(w.Bm, FB, 0, i * NU + a);
         }
         UNR for (int c = 0; c < M0; ++c) {
           double gr = (c == 0 ? par(PF::CS) : 0.0) - at(w.LL, FZ, 0, c) + at(w.LU, FZ, 0, c);
-          UNR for (int r = 0; r < NX; ++r) gr += at0(w.F0, r * M0 + c) * pik[r];
+          UNR for (int r = 0; r < NX; ++r) gr += at0(w.F0, NX * M0, r * M0 + c) * pik[r];
           st = fmax(st, fabs(gr));
         }
       } else {
@@ -370,7 +397,7 @@ struct Lane {
         UNR for (int i = 0; i < NX; ++i) {
           double t = at(w.BD, FX, kp, i) - dz[i];
           if (kp == 0) {
-            UNR for (int a = 0; a < M0; ++a) t += at0(w.F0, i * M0 + a) * dprev[a];
+            UNR for (int a = 0; a < M0; ++a) t += at0(w.F0, NX * M0, i * M0 + a) * dprev[a];
           } else {
             UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, kp, i * NX + q) * dprev[q];
             UNR for (int a = 0; a < NU; ++a) t += at(w.Bm, FB, kp, i * NU + a) * dprev[NX + a];
@@ -389,9 +416,19 @@ struct Lane {
     }
     mu = musum / nbox;
     rs = 1.0;
+    qp_store_scalars();
   }
 
-  struct CompState { double tl, tu, ql, qu, dz; bool bx; };
+  struct CompState { double tl, tu, itl, itu, ql, qu, dz; bool bx; };
+
+  // running minimum of t / (-dt) over dt < 0 without a division per candidate (value n / d, d > 0)
+  struct MinRatio {
+    double n, d;
+    __device__ __forceinline__ void add(double t, double dt) {
+      if (dt < 0.0 && t * d < n * (-dt)) { n = t; d = -dt; }
+    }
+    __device__ __forceinline__ double value() const { return n / d; }
+  };
 
   template <bool U = true>
   __device__ __forceinline__ void comp_states(int k, CompState (&c)[NZ]) const {
@@ -406,12 +443,14 @@ struct Lane {
       c[i].qu = atk<U>(w.QU, FZ, k, i);
       c[i].tl = dz - (lb[i] - z[i]);
       c[i].tu = (ub[i] - z[i]) - dz;
+      c[i].itl = bx[i] ? 1.0 / c[i].tl : 0.0;
+      c[i].itu = bx[i] ? 1.0 / c[i].tu : 0.0;
     }
   }
 
   // corrector complementarity right-hand sides from the affine direction da
   __device__ __forceinline__ static void corr_rhs(const CompState& c, double da, double smu, double& rl, double& ru) {
-    const double dlla = -c.ql - c.ql * da / c.tl, dlua = -c.qu + c.qu * da / c.tu;
+    const double dlla = -c.ql - c.ql * da * c.itl, dlua = -c.qu + c.qu * da * c.itu;
     rl = smu - c.tl * c.ql - da * dlla;
     ru = smu - c.tu * c.qu + da * dlua;
   }
@@ -425,11 +464,11 @@ struct Lane {
       H[i] = o.lm;
       g[i] = o.lm * c[i].dz + cgrad(k, i);
       if (c[i].bx) {
-        H[i] += c[i].ql / c[i].tl + c[i].qu / c[i].tu;
+        H[i] += c[i].ql * c[i].itl + c[i].qu * c[i].itu;
         if (corr) {
           double rl, ru;
           corr_rhs(c[i], atk<U>(w.DAFF, FZ, k, i), smu, rl, ru);
-          g[i] += -c[i].ql - rl / c[i].tl + c[i].qu + ru / c[i].tu;
+          g[i] += -c[i].ql - rl * c[i].itl + c[i].qu + ru * c[i].itu;
         }
       }
     }
@@ -459,23 +498,28 @@ struct Lane {
     }
     for (int k = Nw - 1; k >= 1; --k) {
       if (k >= N) continue;
+      // load block: stage matrices first (independent of the recursion), then the IPM state
+      double Ak[NX * NX], Bk[NX * NU], e[NX];
+      UNR for (int i = 0; i < NX * NX; ++i) Ak[i] = at(w.A, FA, k, i);
+      UNR for (int i = 0; i < NX * NU; ++i) Bk[i] = at(w.Bm, FB, k, i);
+      if (FACTOR) {
+        UNR for (int i = 0; i < NX; ++i) e[i] = rs * at(w.E0, FX, k, i);
+      }
       double H[NZ], g[NZ];
       hess_grad(k, corr, smu, H, g);
       double Pe[NX], Lr[NU * NU], Yk[NU * NQ];
-      double Bk[NX * NU];
-      UNR for (int i = 0; i < NX * NU; ++i) Bk[i] = at(w.Bm, FB, k, i);
       double BP[NU * NX];
       if (FACTOR) {
         // Pe = P e ; lin_e += Pi' e
         UNR for (int i = 0; i < NX; ++i) {
           double t = 0.0;
-          UNR for (int j = 0; j < NX; ++j) t += P[i * NX + j] * (rs * at(w.E0, FX, k, j));
+          UNR for (int j = 0; j < NX; ++j) t += P[i * NX + j] * e[j];
           Pe[i] = t;
           at(w.PE, FX, k, i) = t;
         }
         UNR for (int j = 0; j < NQ; ++j) {
           double t = 0.0;
-          UNR for (int i = 0; i < NX; ++i) t += Pi[i * NQ + j] * (rs * at(w.E0, FX, k, i));
+          UNR for (int i = 0; i < NX; ++i) t += Pi[i * NQ + j] * e[i];
           lin_e[j] += t;
         }
         // BP = B' P ; Ru = BP B + diag(Hu)
@@ -545,7 +589,7 @@ struct Lane {
           double col[NU];
           UNR for (int a = 0; a < NU; ++a) {
             double t = 0.0;
-            UNR for (int i = 0; i < NX; ++i) t += BP[a * NX + i] * at(w.A, FA, k, i * NX + j);
+            UNR for (int i = 0; i < NX; ++i) t += BP[a * NX + i] * Ak[i * NX + j];
             col[a] = t;
           }
           // forward substitution only (W), then back substitution (K)
@@ -575,7 +619,7 @@ struct Lane {
           }
         UNR for (int j = 0; j < NX; ++j) {
           double Aj[NX], t[NX];
-          UNR for (int q = 0; q < NX; ++q) Aj[q] = at(w.A, FA, k, q * NX + j);
+          UNR for (int q = 0; q < NX; ++q) Aj[q] = Ak[q * NX + j];
           UNR for (int i = 0; i < NX; ++i) {
             double s = 0.0;
             UNR for (int q = 0; q < NX; ++q) s += P[i * NX + q] * Aj[q];
@@ -583,7 +627,7 @@ struct Lane {
           }
           UNR for (int i = j; i < NX; ++i) {
             double s = 0.0;
-            UNR for (int q = 0; q < NX; ++q) s += at(w.A, FA, k, q * NX + i) * t[q];
+            UNR for (int q = 0; q < NX; ++q) s += Ak[q * NX + i] * t[q];
             Pn[i * NX + j] += s;
           }
         }
@@ -592,7 +636,7 @@ struct Lane {
         UNR for (int i = 0; i < NX; ++i)
           UNR for (int j = 0; j < NQ; ++j) {
             double t = 0.0;
-            UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, k, q * NX + i) * Pi[q * NQ + j];
+            UNR for (int q = 0; q < NX; ++q) t += Ak[q * NX + i] * Pi[q * NQ + j];
             UNR for (int a = 0; a < NU; ++a) t += Kk[a * NX + i] * Yk[a * NQ + j];
             Pin[i * NQ + j] = t;
           }
@@ -605,7 +649,7 @@ struct Lane {
       // vector pass part 2: p = g_x + A' v + K' r
       UNR for (int i = 0; i < NX; ++i) {
         double t = g[i];
-        UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, k, q * NX + i) * v[q];
+        UNR for (int q = 0; q < NX; ++q) t += Ak[q * NX + i] * v[q];
         UNR for (int a = 0; a < NU; ++a) t += Kk[a * NX + i] * r[a];
         p[i] = t;
       }
@@ -615,13 +659,13 @@ struct Lane {
       double H[NZ], g[NZ];
       hess_grad(0, corr, smu, H, g);
       double F[NX * M0], Pe[NX], Lr[M0 * M0], Yk[M0 * NQ];
-      UNR for (int i = 0; i < NX * M0; ++i) F[i] = at0(w.F0, i);
+      UNR for (int i = 0; i < NX * M0; ++i) F[i] = at0(w.F0, NX * M0, i);
       if (FACTOR) {
         UNR for (int i = 0; i < NX; ++i) {
           double t = 0.0;
           UNR for (int j = 0; j < NX; ++j) t += P[i * NX + j] * (rs * at(w.E0, FX, 0, j));
           Pe[i] = t;
-          at0(w.PE0, i) = t;
+          at0(w.PE0, NX, i) = t;
         }
         UNR for (int j = 0; j < NQ; ++j) {
           double t = 0.0;
@@ -643,19 +687,19 @@ struct Lane {
             Lr[c * M0 + a] = t;
           }
         ok = ok && chol<M0>(Lr);
-        UNR for (int i = 0; i < M0 * M0; ++i) at0(w.LR0, i) = Lr[i];
+        UNR for (int i = 0; i < M0 * M0; ++i) at0(w.LR0, M0 * M0, i) = Lr[i];
         UNR for (int a = 0; a < M0; ++a)
           UNR for (int j = 0; j < NQ; ++j) {
             double t = 0.0;
             UNR for (int i = 0; i < NX; ++i) t += F[i * M0 + a] * Pi[i * NQ + j];
             Yk[a * NQ + j] = t;
-            at0(w.Y0, a * NQ + j) = t;
+            at0(w.Y0, M0 * NQ, a * NQ + j) = t;
           }
         UNR for (int j = 0; j < NQ; ++j) {
           double col[M0];
           UNR for (int a = 0; a < M0; ++a) col[a] = Yk[a * NQ + j];
           chol_solve<M0>(Lr, col);
-          UNR for (int a = 0; a < M0; ++a) at0(w.M0, a * NQ + j) = col[a];
+          UNR for (int a = 0; a < M0; ++a) at0(w.M0, M0 * NQ, a * NQ + j) = col[a];
           UNR for (int i = 0; i < NQ; ++i) {
             double t = 0.0;
             UNR for (int a = 0; a < M0; ++a) t += Yk[a * NQ + i] * col[a];
@@ -663,9 +707,9 @@ struct Lane {
           }
         }
       } else {
-        UNR for (int i = 0; i < NX; ++i) Pe[i] = at0(w.PE0, i);
-        UNR for (int i = 0; i < M0 * M0; ++i) Lr[i] = at0(w.LR0, i);
-        UNR for (int i = 0; i < M0 * NQ; ++i) Yk[i] = at0(w.Y0, i);
+        UNR for (int i = 0; i < NX; ++i) Pe[i] = at0(w.PE0, NX, i);
+        UNR for (int i = 0; i < M0 * M0; ++i) Lr[i] = at0(w.LR0, M0 * M0, i);
+        UNR for (int i = 0; i < M0 * NQ; ++i) Yk[i] = at0(w.Y0, M0 * NQ, i);
       }
       double v[NX];
       UNR for (int i = 0; i < NX; ++i) v[i] = Pe[i] + p[i];
@@ -694,14 +738,12 @@ struct Lane {
     return ok;
   }
 
-  __device__ __forceinline__ static double stb(double t, double dt) { return dt < 0.0 ? -t / dt : INFINITY; }
-
   // forward sweep.  CORR == false: stores DAFF, returns the affine step length and the mu_aff
   // polynomial; CORR == true: stores D, returns alpha_max of the combined step.
   template <bool CORR>
   __device__ void forward(double smu, const double (&w0in)[M0], const double (&nun)[NQ], double& amax, double& c0,
                           double& c1, double& c2) {
-    amax = CORR ? 1.0 / o.tau : 1.0;
+    MinRatio mr{CORR ? 1.0 : 1.0, CORR ? o.tau : 1.0};
     c0 = c1 = c2 = 0.0;
     double* dst = CORR ? w.D : w.DAFF;
     double dx[NX];
@@ -709,33 +751,45 @@ struct Lane {
       if (k > N) continue;
       double d[NZ];
       if (k == 0) {
+        double F[NX * M0], e[NX], Mk[M0 * NQ];
+        UNR for (int i = 0; i < NX * M0; ++i) F[i] = at0(w.F0, NX * M0, i);
+        UNR for (int i = 0; i < M0 * NQ; ++i) Mk[i] = at0(w.M0, M0 * NQ, i);
+        UNR for (int i = 0; i < NX; ++i) e[i] = at(w.E0, FX, 0, i);
         double w0[M0];
         UNR for (int a = 0; a < M0; ++a) {
           double t = w0in[a];
-          UNR for (int j = 0; j < NQ; ++j) t -= at0(w.M0, a * NQ + j) * nun[j];
+          UNR for (int j = 0; j < NQ; ++j) t -= Mk[a * NQ + j] * nun[j];
           w0[a] = t;
         }
         UNR for (int i = 0; i < NZ; ++i) d[i] = i < M0 ? w0[i < M0 ? i : 0] : 0.0;
         UNR for (int i = 0; i < NX; ++i) {
-          double t = rs * at(w.E0, FX, 0, i);
-          UNR for (int a = 0; a < M0; ++a) t += at0(w.F0, i * M0 + a) * w0[a];
+          double t = rs * e[i];
+          UNR for (int a = 0; a < M0; ++a) t += F[i * M0 + a] * w0[a];
           dx[i] = t;
         }
       } else if (k < N) {
+        // load block: everything this stage needs, independent of the recursion
+        double Kk[NU * NX], kf[NU], Mk[NU * NQ], Ak[NX * NX], Bk[NX * NU], e[NX];
+        UNR for (int i = 0; i < NU * NX; ++i) Kk[i] = at(w.K, FK, k, i);
+        UNR for (int a = 0; a < NU; ++a) kf[a] = at(w.KF, FU, k, a);
+        UNR for (int i = 0; i < NU * NQ; ++i) Mk[i] = at(w.M, FM, k, i);
+        UNR for (int i = 0; i < NX * NX; ++i) Ak[i] = at(w.A, FA, k, i);
+        UNR for (int i = 0; i < NX * NU; ++i) Bk[i] = at(w.Bm, FB, k, i);
+        UNR for (int i = 0; i < NX; ++i) e[i] = at(w.E0, FX, k, i);
         double du[NU];
         UNR for (int a = 0; a < NU; ++a) {
-          double t = at(w.KF, FU, k, a);
-          UNR for (int i = 0; i < NX; ++i) t += at(w.K, FK, k, a * NX + i) * dx[i];
-          UNR for (int j = 0; j < NQ; ++j) t -= at(w.M, FM, k, a * NQ + j) * nun[j];
+          double t = kf[a];
+          UNR for (int i = 0; i < NX; ++i) t += Kk[a * NX + i] * dx[i];
+          UNR for (int j = 0; j < NQ; ++j) t -= Mk[a * NQ + j] * nun[j];
           du[a] = t;
         }
         UNR for (int i = 0; i < NX; ++i) d[i] = dx[i];
         UNR for (int a = 0; a < NU; ++a) d[NX + a] = du[a];
         double dn[NX];
         UNR for (int i = 0; i < NX; ++i) {
-          double t = rs * at(w.E0, FX, k, i);
-          UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, k, i * NX + q) * dx[q];
-          UNR for (int a = 0; a < NU; ++a) t += at(w.Bm, FB, k, i * NU + a) * du[a];
+          double t = rs * e[i];
+          UNR for (int q = 0; q < NX; ++q) t += Ak[i * NX + q] * dx[q];
+          UNR for (int a = 0; a < NU; ++a) t += Bk[i * NU + a] * du[a];
           dn[i] = t;
         }
         UNR for (int i = 0; i < NX; ++i) dx[i] = dn[i];
@@ -744,28 +798,33 @@ struct Lane {
       }
       CompState c[NZ];
       comp_states(k, c);
+      double da[NZ];
+      if (CORR) {
+        UNR for (int i = 0; i < NZ; ++i) da[i] = at(w.DAFF, FZ, k, i);
+      }
       UNR for (int i = 0; i < NZ; ++i) {
         at(dst, FZ, k, i) = d[i];
         if (!c[i].bx) continue;
         double dll, dlu;
         if (!CORR) {
-          dll = -c[i].ql - c[i].ql * d[i] / c[i].tl;
-          dlu = -c[i].qu + c[i].qu * d[i] / c[i].tu;
+          dll = -c[i].ql - c[i].ql * d[i] * c[i].itl;
+          dlu = -c[i].qu + c[i].qu * d[i] * c[i].itu;
           c0 += c[i].tl * c[i].ql + c[i].tu * c[i].qu;
           c1 += c[i].tl * dll + d[i] * c[i].ql + c[i].tu * dlu - d[i] * c[i].qu;
           c2 += d[i] * dll - d[i] * dlu;
         } else {
           double rl, ru;
-          corr_rhs(c[i], at(w.DAFF, FZ, k, i), smu, rl, ru);
-          dll = (rl - c[i].ql * d[i]) / c[i].tl;
-          dlu = (ru + c[i].qu * d[i]) / c[i].tu;
+          corr_rhs(c[i], da[i], smu, rl, ru);
+          dll = (rl - c[i].ql * d[i]) * c[i].itl;
+          dlu = (ru + c[i].qu * d[i]) * c[i].itu;
         }
-        amax = fmin(amax, stb(c[i].tl, d[i]));
-        amax = fmin(amax, stb(c[i].tu, -d[i]));
-        amax = fmin(amax, stb(c[i].ql, dll));
-        amax = fmin(amax, stb(c[i].qu, dlu));
+        mr.add(c[i].tl, d[i]);
+        mr.add(c[i].tu, -d[i]);
+        mr.add(c[i].ql, dll);
+        mr.add(c[i].qu, dlu);
       }
     }
+    amax = mr.value();
   }
 
   // apply the step; recompute mu of the new iterate
@@ -781,7 +840,7 @@ struct Lane {
         if (!c[i].bx) continue;
         double rl, ru;
         corr_rhs(c[i], at(w.DAFF, FZ, k, i), smu, rl, ru);
-        const double dll = (rl - c[i].ql * d) / c[i].tl, dlu = (ru + c[i].qu * d) / c[i].tu;
+        const double dll = (rl - c[i].ql * d) * c[i].itl, dlu = (ru + c[i].qu * d) * c[i].itu;
         const double qln = c[i].ql + alpha * dll, qun = c[i].qu + alpha * dlu;
         at(w.QL, FZ, k, i) = qln;
         at(w.QU, FZ, k, i) = qun;
@@ -791,35 +850,64 @@ struct Lane {
     mu = musum / nbox;
   }
 
-  // returns 0 converged, 1 max iter, -1 failure; iterations in its
-  __device__ int qp_solve(int& its) {
-    qp_init();
-    int status = 1;
-    int it = 0;
+  // ---- interior-point iteration, one sweep per kernel (state in PAR between launches) ----------
+  __device__ void qp_store_scalars() {
+    par(PF::RS) = rs; par(PF::RD0) = rd0; par(PF::E00) = e00; par(PF::MU) = mu; par(PF::NBOX) = nbox;
+  }
+  __device__ void qp_load_scalars() {
+    rs = par(PF::RS); rd0 = par(PF::RD0); e00 = par(PF::E00); mu = par(PF::MU); nbox = par(PF::NBOX);
+  }
+  // convergence test at the top of an iteration: 1 continue, 0 converged, -1 failure
+  __device__ int qp_check() const {
+    if (!isfinite(mu)) return -1;
+    if (mu < o.qp_tol_comp && rs * rd0 < o.qp_tol_stat && rs * e00 < o.qp_tol_eq) return 0;
+    return 1;
+  }
+  // predictor factorisation + vector pass; false on failure
+  __device__ bool qp_factor() {
     double Sc[NQ * NQ], lin_e[NQ], w0[M0], nun[NQ];
-    for (; it < o.qp_max_iter; ++it) {
-      if (!isfinite(mu)) { status = -1; break; }
-      if (mu < o.qp_tol_comp && rs * rd0 < o.qp_tol_stat && rs * e00 < o.qp_tol_eq) { status = 0; break; }
-      // predictor
-      if (!backward<true>(false, 0.0, Sc, lin_e, w0, nun)) { status = -1; break; }
-      double aa, c0, c1, c2;
-      forward<false>(0.0, w0, nun, aa, c0, c1, c2);
-      const double muaff = (c0 + aa * (c1 + aa * c2)) / nbox;
-      double sig = muaff / mu;
-      sig = fmin(1.0, sig * sig * sig);
-      const double smu = sig * mu;
-      // corrector
-      if (!backward<false>(true, smu, Sc, lin_e, w0, nun)) { status = -1; break; }
-      double amax;
-      forward<true>(smu, w0, nun, amax, c0, c1, c2);
-      const double alpha = fmin(1.0, o.tau * amax);
-      update_iterate(alpha, smu);
-      UNR for (int j = 0; j < NQ; ++j) par(PF::QNU + j) += alpha * (nun[j] - par(PF::QNU + j));
-      rs *= (1.0 - alpha);
-    }
-    its = it;
-    if (status < 0) return -1;
-    // costate recovery: pi_{N-1} = lm dz_N - ql + qu + E'nu ; pi_{k-1} = lm dz_k - ql + qu + A_k' pi_k
+    if (!backward<true>(false, 0.0, Sc, lin_e, w0, nun)) return false;
+    UNR for (int i = 0; i < NQ * NQ; ++i) par(PF::SC + i) = Sc[i];
+    UNR for (int j = 0; j < NQ; ++j) { par(PF::LINE + j) = lin_e[j]; par(PF::NUN + j) = nun[j]; }
+    UNR for (int a = 0; a < M0; ++a) par(PF::W0 + a) = w0[a];
+    return true;
+  }
+  __device__ void qp_fpred() {
+    double w0[M0], nun[NQ], aa, c0, c1, c2;
+    UNR for (int a = 0; a < M0; ++a) w0[a] = par(PF::W0 + a);
+    UNR for (int j = 0; j < NQ; ++j) nun[j] = par(PF::NUN + j);
+    forward<false>(0.0, w0, nun, aa, c0, c1, c2);
+    const double muaff = (c0 + aa * (c1 + aa * c2)) / nbox;
+    double sig = muaff / mu;
+    sig = fmin(1.0, sig * sig * sig);
+    par(PF::SMU) = sig * mu;
+  }
+  __device__ bool qp_bcorr() {
+    double Sc[NQ * NQ], lin_e[NQ], w0[M0], nun[NQ];
+    UNR for (int i = 0; i < NQ * NQ; ++i) Sc[i] = par(PF::SC + i);
+    UNR for (int j = 0; j < NQ; ++j) lin_e[j] = par(PF::LINE + j);
+    if (!backward<false>(true, par(PF::SMU), Sc, lin_e, w0, nun)) return false;
+    UNR for (int j = 0; j < NQ; ++j) par(PF::NUN + j) = nun[j];
+    UNR for (int a = 0; a < M0; ++a) par(PF::W0 + a) = w0[a];
+    return true;
+  }
+  __device__ void qp_fcorr() {
+    double w0[M0], nun[NQ], amax, c0, c1, c2;
+    UNR for (int a = 0; a < M0; ++a) w0[a] = par(PF::W0 + a);
+    UNR for (int j = 0; j < NQ; ++j) nun[j] = par(PF::NUN + j);
+    forward<true>(par(PF::SMU), w0, nun, amax, c0, c1, c2);
+    par(PF::ALPHA) = fmin(1.0, o.tau * amax);
+  }
+  __device__ void qp_update() {
+    const double alpha = par(PF::ALPHA);
+    update_iterate(alpha, par(PF::SMU));
+    UNR for (int j = 0; j < NQ; ++j) par(PF::QNU + j) += alpha * (par(PF::NUN + j) - par(PF::QNU + j));
+    rs *= (1.0 - alpha);
+    par(PF::RS) = rs;
+    par(PF::MU) = mu;
+  }
+  // costate recovery: pi_{N-1} = lm dz_N - ql + qu + E'nu ; pi_{k-1} = lm dz_k - ql + qu + A_k' pi_k
+  __device__ bool qp_costate() {
     double lam[NX];
     bool fin = true;
     UNR for (int i = 0; i < NX; ++i) {
@@ -830,7 +918,7 @@ struct Lane {
     for (int k = Nw - 1; k >= 0; --k) {
       if (k >= N) continue;
       UNR for (int i = 0; i < NX; ++i) at(w.QPI, FPI, k, i) = lam[i];
-      if (k == 0) break;
+      if (k == 0) continue;
       double ln[NX];
       UNR for (int i = 0; i < NX; ++i) {
         const double dz = at(w.DZ, FZ, k, i);
@@ -840,8 +928,7 @@ struct Lane {
       }
       UNR for (int i = 0; i < NX; ++i) lam[i] = ln[i];
     }
-    if (!fin) return -1;
-    return status;
+    return fin;
   }
 
   // ---------------------------------------------------------------------------------------------
@@ -919,14 +1006,14 @@ struct Lane {
         }
       }
       UNR for (int i = 0; i < NZ; ++i) {
-        double& ll = at(w.LL, FZ, k, i);
-        double& lu = at(w.LU, FZ, k, i);
+        gdouble& ll = at(w.LL, FZ, k, i);
+        gdouble& lu = at(w.LU, FZ, k, i);
         ll += alpha * (at(w.QL, FZ, k, i) - ll);
         lu += alpha * (at(w.QU, FZ, k, i) - lu);
       }
       if (k < N) {
         UNR for (int i = 0; i < NX; ++i) {
-          double& pi = at(w.PI, FPI, k, i);
+          gdouble& pi = at(w.PI, FPI, k, i);
           pi += alpha * (at(w.QPI, FPI, k, i) - pi);
         }
       }
@@ -936,107 +1023,189 @@ struct Lane {
 };
 
 // -------------------------------------------------------------------------------------------------
-// persistent kernel
+// phase kernels.  Each slot (lane) holds one problem at a time; per-slot integer state:
+//   IS_PID  problem id (-1 free, -2 queue exhausted)   IS_IT   SQP iterations so far
+//   IS_QIT  QP iterations so far                        IS_N    horizon
+//   IS_PH   phase: 0 free, 1 linearise, 2 QP, 3 line search
+// One SQP iteration = refill -> sens -> resid -> qp -> ls (host loop, vboc_solve_batch).
 // -------------------------------------------------------------------------------------------------
+enum { IS_PID = 0, IS_IT, IS_QIT, IS_N, IS_PH, IS_QST, IS_QCUR, IS_COUNT };
+
+struct SlotState {
+  int* ist;          // [IS_COUNT][S]
+  unsigned* done;    // problems finished
+  unsigned* qp_active;  // lanes whose QP is still iterating
+  long long S;
+  __device__ __forceinline__ int& operator()(int f, unsigned slot) const { return ist[(long long)f * S + slot]; }
+};
+
 template <int NQ>
-__global__ __launch_bounds__(256) void sqp_kernel(Work w, Opts o, Inputs in) {
+__device__ __forceinline__ void finish(Lane<NQ>& L, const Inputs& in, const SlotState& ss, int status) {
+  const unsigned sl = L.slot;
+  L.store_result(in, ss(IS_PID, sl), status, ss(IS_IT, sl), ss(IS_QIT, sl));
+  ss(IS_PID, sl) = -1;
+  ss(IS_PH, sl) = 0;
+  atomicAdd(ss.done, 1u);
+}
+
+// lanes without a problem pull the next one (wave-aggregated atomicAdd on the queue head)
+template <int NQ>
+__global__ __launch_bounds__(256) void k_refill(Work w, Opts o, Inputs in, SlotState ss) {
   const unsigned slot = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = threadIdx.x & 63;
+  int pid = ss(IS_PID, slot);
+  const unsigned long long need = __ballot(pid == -1);
+  if (!need) return;
+  const int leader = __ffsll((unsigned long long)need) - 1;
+  unsigned int base = 0;
+  if (lane == leader) base = atomicAdd(in.head, (unsigned int)__popcll(need));
+  base = __shfl(base, leader);
+  if (pid != -1) return;
+  const unsigned int cand = base + (unsigned)__popcll(need & ((1ull << lane) - 1ull));
+  if (cand >= (unsigned int)in.B) {
+    ss(IS_PID, slot) = -2;
+    return;
+  }
   Lane<NQ> L(w, o, slot);
-  int pid = -1;          // problem held by this lane (-1 none, -2 queue exhausted)
-  int it = 0, qtot = 0;
-  while (pid != -2) {
-    // wave-aggregated dequeue for lanes without a problem
-    const unsigned long long need = __ballot(pid == -1);
-    if (need) {
-      const int leader = __ffsll((unsigned long long)need) - 1;
-      unsigned int base = 0;
-      if (lane == leader) base = atomicAdd(in.head, (unsigned int)__popcll(need));
-      base = __shfl(base, leader);
-      if (pid == -1) {
-        const unsigned int rank = __popcll(need & ((1ull << lane) - 1ull));
-        const unsigned int cand = base + rank;
-        if (cand < (unsigned int)in.B) {
-          pid = (int)cand;
-          L.load(in, pid);
-          it = 0;
-          qtot = 0;
-        } else {
-          pid = -2;
-        }
-      }
-    }
-    if (pid < 0) continue;
-    L.Nw = wave_max(L.N);
-    double rstat, req, rineq, rcomp;
-    L.linearize(rstat, req, rineq, rcomp);
-    int status = -1;
-    if (!isfinite(rstat) || !isfinite(req)) status = 1;
-    else if (rstat < o.tol_stat && req < o.tol_eq && rineq < o.tol_ineq && rcomp < o.tol_comp) status = 0;
-    else if (it >= o.max_iter) status = 2;
-    if (status < 0) {
-      int qit = 0;
-      const int qs = L.qp_solve(qit);
-      qtot += qit;
-      if (qs < 0) {
-        status = 4;
-      } else {
-        L.update_weights();
-        const double phi0 = L.merit(0.0);
-        double alpha = 1.0;
-        for (;;) {
-          const double pa = L.merit(alpha);
-          if (pa < phi0) break;
-          if (alpha * o.alpha_red < o.alpha_min) break;
-          alpha *= o.alpha_red;
-        }
-        L.apply_step(alpha);
-        ++it;
-        if (!isfinite(L.par(Par<NQ>::S))) status = 1;
-      }
-    }
-    if (status >= 0) {
-      L.store_result(in, pid, status, it, qtot);
-      pid = -1;
-    }
+  L.load(in, (int)cand);
+  ss(IS_PID, slot) = (int)cand;
+  ss(IS_IT, slot) = 0;
+  ss(IS_QIT, slot) = 0;
+  ss(IS_N, slot) = L.N;
+  ss(IS_PH, slot) = 1;
+}
+
+// common prologue: horizon, wave-uniform sweep bound; false if this lane is not in phase `ph`
+template <int NQ>
+__device__ __forceinline__ bool prologue(Lane<NQ>& L, const SlotState& ss, int ph) {
+  const bool act = ss(IS_PH, L.slot) == ph;
+  L.N = act ? ss(IS_N, L.slot) : 0;
+  L.Nw = wave_max(L.N);
+  return act;
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_sens(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!prologue(L, ss, 1)) return;
+  L.sens();
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_resid(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!prologue(L, ss, 1)) return;
+  double rstat, req, rineq, rcomp;
+  L.residuals(rstat, req, rineq, rcomp);
+  int status = -1;
+  if (!isfinite(rstat) || !isfinite(req)) status = 1;
+  else if (rstat < o.tol_stat && req < o.tol_eq && rineq < o.tol_ineq && rcomp < o.tol_comp) status = 0;
+  else if (ss(IS_IT, L.slot) >= o.max_iter) status = 2;
+  if (status >= 0) finish(L, in, ss, status);
+  else ss(IS_PH, L.slot) = 2;
+}
+
+// ---- interior-point sweeps: IS_QST = 1 running, 0 converged, 2 max iter, -1 failed ----------------
+template <int NQ>
+__device__ __forceinline__ bool qp_prologue(Lane<NQ>& L, const SlotState& ss) {
+  const bool act = ss(IS_PH, L.slot) == 2 && ss(IS_QST, L.slot) == 1;
+  L.N = act ? ss(IS_N, L.slot) : 0;
+  L.Nw = wave_max(L.N);
+  if (act) L.qp_load_scalars();
+  return act;
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_qp_init(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!prologue(L, ss, 2)) return;
+  L.qp_init();
+  ss(IS_QST, L.slot) = 1;
+  ss(IS_QCUR, L.slot) = 0;
+  atomicAdd(ss.qp_active, 1u);
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_qp_factor(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!qp_prologue(L, ss)) return;
+  int st = L.qp_check();
+  if (st == 1 && ss(IS_QCUR, L.slot) >= o.qp_max_iter) st = 2;
+  if (st == 1 && !L.qp_factor()) st = -1;
+  if (st != 1) {
+    ss(IS_QST, L.slot) = st;
+    atomicSub(ss.qp_active, 1u);
   }
 }
 
-#ifdef VBOC_PHASE_TEST
-// diagnostic: one kernel per phase to read each phase's register allocation
-template <int NQ, int PH>
-__global__ __launch_bounds__(256) void phase_kernel(Work w, Opts o, Inputs in) {
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_qp_fpred(Work w, Opts o, Inputs in, SlotState ss) {
   Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
-  L.N = in.N[L.slot];
-  L.Nw = wave_max(L.N);
-  double a = 0, b = 0, c = 0, d = 0;
-  double Sc[NQ * NQ] = {}, le[NQ] = {}, w0[NQ + 1] = {}, nun[NQ] = {};
-  int it = 0;
-  if (PH == 0) L.linearize(a, b, c, d);
-  if (PH == 1) L.qp_init();
-  if (PH == 2) L.template backward<true>(false, 0.0, Sc, le, w0, nun);
-  if (PH == 3) L.template backward<false>(true, 0.5, Sc, le, w0, nun);
-  if (PH == 4) L.template forward<false>(0.0, w0, nun, a, b, c, d);
-  if (PH == 5) L.template forward<true>(0.1, w0, nun, a, b, c, d);
-  if (PH == 6) L.update_iterate(0.5, 0.1);
-  if (PH == 7) a = L.merit(0.3);
-  if (PH == 8) L.apply_step(0.3);
-  if (PH == 9) L.load(in, L.slot);
-  if (PH == 10) it = L.qp_solve(it);
-  in.cost[L.slot] = a + b + c + d + Sc[0] + le[0] + w0[0] + nun[0] + it;
+  if (!qp_prologue(L, ss)) return;
+  L.qp_fpred();
 }
-template __global__ void phase_kernel<3, 0>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 1>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 2>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 3>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 4>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 5>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 6>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 7>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 8>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 9>(Work, Opts, Inputs);
-template __global__ void phase_kernel<3, 10>(Work, Opts, Inputs);
-#endif
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_qp_bcorr(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!qp_prologue(L, ss)) return;
+  if (!L.qp_bcorr()) {
+    ss(IS_QST, L.slot) = -1;
+    atomicSub(ss.qp_active, 1u);
+  }
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_qp_fcorr(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!qp_prologue(L, ss)) return;
+  L.qp_fcorr();
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_qp_update(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!qp_prologue(L, ss)) return;
+  L.qp_update();
+  ss(IS_QCUR, L.slot) += 1;
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_qp_fin(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!prologue(L, ss, 2)) return;
+  ss(IS_QIT, L.slot) += ss(IS_QCUR, L.slot);
+  const int qs = ss(IS_QST, L.slot);
+  if (qs < 0 || !L.qp_costate()) finish(L, in, ss, 4);
+  else ss(IS_PH, L.slot) = 3;
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) VBOC_WPE void k_ls(Work w, Opts o, Inputs in, SlotState ss) {
+  Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
+  if (!prologue(L, ss, 3)) return;
+  L.update_weights();
+  const double phi0 = L.merit(0.0);
+  double alpha = 1.0;
+  for (;;) {
+    const double pa = L.merit(alpha);
+    if (pa < phi0) break;
+    if (alpha * o.alpha_red < o.alpha_min) break;
+    alpha *= o.alpha_red;
+  }
+  L.apply_step(alpha);
+  ss(IS_IT, L.slot) += 1;
+  if (!isfinite((double)L.par(Par<NQ>::S))) finish(L, in, ss, 1);
+  else ss(IS_PH, L.slot) = 1;
+}
+
+__global__ void k_slots_init(int* ist, long long S) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= S) return;
+  ist[IS_PID * S + i] = -1;
+  ist[IS_PH * S + i] = 0;
+  ist[IS_N * S + i] = 0;
+}
 
 // -------------------------------------------------------------------------------------------------
 // twin integrator (SYM<sys>INIT.acados_integrator): one RK4 step of length T per problem
@@ -1078,7 +1247,9 @@ struct vboc_solver {
   Work w;
   void* pool = nullptr;
   size_t pool_bytes = 0;
-  unsigned int* head = nullptr;
+  unsigned int* head = nullptr;     // [0] queue head, [1] problems finished
+  int* ist = nullptr;               // per-slot integer state [IS_COUNT][slots]
+  unsigned int* host_done = nullptr;  // pinned mirror of head[1]
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int launches = 0;
   // host staging for vboc_solve_batch_host
@@ -1098,12 +1269,50 @@ static int par_count(int nq) {
   return nq == 1 ? Par<1>::COUNT : (nq == 2 ? Par<2>::COUNT : Par<3>::COUNT);
 }
 
+static inline size_t ev(size_t f) { return (f + 1) & ~(size_t)1; }  // fields rounded up to pairs
+
 static size_t work_doubles_per_slot(int nq, int nmax) {
-  const int NX = 2 * nq, NU = nq, NZ = 3 * nq, M0 = nq + 1;
-  const size_t per_stage = NX /*X*/ + NU + NX /*PI*/ + 2 * NZ + NX /*WPI*/ + NX * NX + NX * NU + NX +
-                           3 * NZ + NX /*E0*/ + NU * NX + NU + NU * NU + 2 * NU * nq + NX /*PE*/ + 2 * NZ + NX;
-  const size_t per_slot = NX * M0 + M0 * M0 + 2 * M0 * nq + NX + par_count(nq);
+  const size_t NX = 2 * nq, NU = nq, NZ = 3 * nq, M0 = nq + 1;
+  const size_t per_stage = ev(NX) /*X*/ + ev(NU) + ev(NX) /*PI*/ + 2 * ev(NZ) + ev(NX) /*WPI*/ + ev(NX * NX) +
+                           ev(NX * NU) + ev(NX) + 3 * ev(NZ) + ev(NX) /*E0*/ + ev(NU * NX) + ev(NU) + ev(NU * NU) +
+                           2 * ev(NU * nq) + ev(NX) /*PE*/ + 2 * ev(NZ) + ev(NX);
+  const size_t per_slot = ev(NX * M0) + ev(M0 * M0) + 2 * ev(M0 * nq) + ev(NX) + ev(par_count(nq));
   return per_stage * (size_t)(nmax + 1) + per_slot;
+}
+
+// One SQP iteration of every resident problem: refill, linearise, QP (host-driven interior-point
+// loop, one kernel per sweep, exits once no lane is iterating), line search + update.
+template <int NQ>
+static hipError_t launch_round(vboc_solver* h, dim3 grid, dim3 block, hipStream_t st, const Work& w, const Opts& o,
+                               const Inputs& in, const SlotState& ss) {
+  hipLaunchKernelGGL(k_refill<NQ>, grid, block, 0, st, w, o, in, ss);
+  hipLaunchKernelGGL(k_sens<NQ>, grid, block, 0, st, w, o, in, ss);
+  hipLaunchKernelGGL(k_resid<NQ>, grid, block, 0, st, w, o, in, ss);
+  hipError_t e = hipMemsetAsync(ss.qp_active, 0, sizeof(unsigned), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_qp_init<NQ>, grid, block, 0, st, w, o, in, ss);
+  h->launches += 5;
+  for (int it = 0; it <= o.qp_max_iter; ++it) {
+    hipLaunchKernelGGL(k_qp_factor<NQ>, grid, block, 0, st, w, o, in, ss);
+    ++h->launches;
+    // poll the active-lane counter (one host sync) from the 6th iteration on, every other one
+    if (it >= 6 && (it & 1) == 0) {
+      e = hipMemcpyAsync(h->host_done + 1, ss.qp_active, sizeof(unsigned), hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return e;
+      if (h->host_done[1] == 0) break;
+    }
+    if (it == o.qp_max_iter) break;
+    hipLaunchKernelGGL(k_qp_fpred<NQ>, grid, block, 0, st, w, o, in, ss);
+    hipLaunchKernelGGL(k_qp_bcorr<NQ>, grid, block, 0, st, w, o, in, ss);
+    hipLaunchKernelGGL(k_qp_fcorr<NQ>, grid, block, 0, st, w, o, in, ss);
+    hipLaunchKernelGGL(k_qp_update<NQ>, grid, block, 0, st, w, o, in, ss);
+    h->launches += 4;
+  }
+  hipLaunchKernelGGL(k_qp_fin<NQ>, grid, block, 0, st, w, o, in, ss);
+  hipLaunchKernelGGL(k_ls<NQ>, grid, block, 0, st, w, o, in, ss);
+  h->launches += 2;
+  return hipGetLastError();
 }
 
 extern "C" {
@@ -1131,10 +1340,11 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
     return fail(VBOC_ERR_NOMEM, std::string("vboc_create: hipMalloc workspace: ") + hipGetErrorString(e));
   }
   e = hipMalloc((void**)&h->head, 256);
+  if (e == hipSuccess) e = hipMalloc((void**)&h->ist, sizeof(int) * IS_COUNT * (size_t)slots);
+  if (e == hipSuccess) e = hipHostMalloc((void**)&h->host_done, 64);
   if (e != hipSuccess) {
-    (void)hipFree(h->pool);
-    delete h;
-    return fail(VBOC_ERR_NOMEM, "vboc_create: hipMalloc queue");
+    vboc_destroy(h);
+    return fail(VBOC_ERR_NOMEM, "vboc_create: hipMalloc queue / slot state");
   }
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);
@@ -1142,8 +1352,8 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   const int NX = 2 * nq, NU = nq, NZ = 3 * nq, M0 = nq + 1;
   const size_t st = (size_t)(nmax + 1) * slots;
   double* p = (double*)h->pool;
-  auto take = [&](size_t fields_per_stage) { double* r = p; p += fields_per_stage * st; return r; };
-  auto take0 = [&](size_t fields) { double* r = p; p += fields * (size_t)slots; return r; };
+  auto take = [&](size_t fields_per_stage) { double* r = p; p += ev(fields_per_stage) * st; return r; };
+  auto take0 = [&](size_t fields) { double* r = p; p += ev(fields) * (size_t)slots; return r; };
   Work& w = h->w;
   w.S = slots;
   w.X = take(NX); w.U = take(NU); w.PI = take(NX); w.LL = take(NZ); w.LU = take(NZ); w.WPI = take(NX);
@@ -1166,6 +1376,8 @@ int vboc_destroy(vboc_handle h) {
   (void)hipSetDevice(h->device);
   if (h->pool) (void)hipFree(h->pool);
   if (h->head) (void)hipFree(h->head);
+  if (h->ist) (void)hipFree(h->ist);
+  if (h->host_done) (void)hipHostFree(h->host_done);
   if (h->stage) (void)hipFree(h->stage);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -1244,16 +1456,35 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   long long lanes = ((long long)b->B + 255) / 256 * 256;
   if (lanes > h->slots) lanes = h->slots;
   Work w = h->w;  // same carve, S = full slot stride
+  SlotState ss{h->ist, h->head + 1, h->head + 2, h->slots};
   const dim3 grid((unsigned)(lanes / 256)), block(256);
   HIPCHK(hipEventRecord(h->ev0, st));
-  switch (h->nq) {
-    case 1: hipLaunchKernelGGL(sqp_kernel<1>, grid, block, 0, st, w, h->o, in); break;
-    case 2: hipLaunchKernelGGL(sqp_kernel<2>, grid, block, 0, st, w, h->o, in); break;
-    default: hipLaunchKernelGGL(sqp_kernel<3>, grid, block, 0, st, w, h->o, in); break;
+  hipLaunchKernelGGL(k_slots_init, dim3((unsigned)((h->slots + 255) / 256)), block, 0, st, h->ist, h->slots);
+  // One SQP iteration of every resident problem per round; finished slots refill from the queue.
+  // The finished-problem counter is read back every `chunk` rounds (one host sync per chunk).
+  const int chunk = 4;
+  long long rounds = 0;
+  h->launches = 1;
+  for (;;) {
+    for (int r = 0; r < chunk; ++r) {
+      hipError_t le;
+      switch (h->nq) {
+        case 1: le = launch_round<1>(h, grid, block, st, w, h->o, in, ss); break;
+        case 2: le = launch_round<2>(h, grid, block, st, w, h->o, in, ss); break;
+        default: le = launch_round<3>(h, grid, block, st, w, h->o, in, ss); break;
+      }
+      if (le != hipSuccess) return fail(VBOC_ERR_HIP, std::string("vboc_solve_batch: ") + hipGetErrorString(le));
+    }
+    rounds += chunk;
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h->host_done, h->head + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (*h->host_done >= (unsigned)b->B) break;
+    if (rounds > 4LL * (h->o.max_iter + 2) * ((b->B + lanes - 1) / lanes + 1))
+      return fail(VBOC_ERR_HIP, "vboc_solve_batch: solver did not drain (internal error)");
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(h->ev1, st));
-  h->launches = 1;
   return VBOC_OK;
 }
 
