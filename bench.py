@@ -1,0 +1,177 @@
+"""VBOC boundary OCP solves/sec - triple pendulum, 1..8 MI355X (BASELINE.json metric).
+
+One step = one batched solve of B boundary OCPs (the first solve of `data_generation`,
+VBOC/triplependulum_vboc.py:32-110: IC law, straight-line guess, N = 100) on each GPU, inputs
+already resident in HBM, followed (N > 1) by the RCCL all-gather of the boundary states x0 that
+feeds the NN fit (configs[3]).  Problem ids are a global counter (Philox per id), so rank r solves
+ids [(step * world + r) * B, ... + B): per-GPU work is fixed as N grows (weak scaling).
+
+Output: ONE JSON line on rank 0 (contract in the task statement), with
+  roofline     dominant kernel k_qp_factor (Riccati factorisation sweep): algorithmic bytes per
+               launch / average launch duration, both measured live over the timed region with HIP
+               events on the solve stream (vboc_kernel_stats); bound "hbm", peak 8 TB/s.
+  cpu_baseline the oracle's C restatement (oracle/, test infrastructure) on a bounded sample of the
+               same workload on the host's cores, rank 0, N = 1 only.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def make_batch(nq, ids, device):
+    import torch
+    from vboc_amd.ics import data_generation_ics
+    b = data_generation_ics(nq, ids)
+    keys = ("N", "x_guess", "u_guess", "p", "lbx", "ubx", "lbu", "ubu", "lbx0", "ubx0", "lbxe", "ubxe")
+    return {k: torch.as_tensor(np.ascontiguousarray(b[k]), device=device) for k in keys}, b
+
+
+def cpu_baseline(nq, B, seconds, threads):
+    """Oracle (CPU FP64 restatement) on the first problems of the workload for ~`seconds`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from vboc_amd.ics import data_generation_ics
+    done, t_total, n = 0, 0.0, max(threads, 8)
+    start = 0
+    while t_total < seconds and start < B:
+        b = data_generation_ics(nq, np.arange(start, start + n))
+        t0 = time.time()
+        oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                           b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], nthreads=threads)
+        t_total += time.time() - t0
+        done += n
+        start += n
+        n = min(4 * n, max(threads, 8) * 64)
+    return done / t_total, done, t_total
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=100_000, help="problems per GPU per step (configs[2]: 100k)")
+    ap.add_argument("--nq", type=int, default=3)
+    ap.add_argument("--slots", type=int, default=65536)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from vboc_amd import lib
+    nq, B = args.nq, args.batch
+    solver = lib.Solver(nq, 100, slots=args.slots, device=local)
+    solver.set_option("profile_kernels", 1)
+    stream = torch.cuda.current_stream(device)
+
+    def ids_for(step):
+        base = (step * world + rank) * B
+        return np.arange(base, base + B, dtype=np.int64)
+
+    # inputs for every step generated and copied to HBM before any timing
+    batches = [make_batch(nq, ids_for(s), device)[0] for s in range(args.warmup + args.steps)]
+    outs = []
+
+    def run_step(tb):
+        out = solver.solve_device(tb, stream=stream)
+        if world > 1:
+            x0 = out["x"][:, 0, :].contiguous()
+            gathered = torch.empty((world,) + tuple(x0.shape), dtype=x0.dtype, device=device)
+            dist.all_gather_into_tensor(gathered, x0)
+            out["gathered"] = gathered
+        return out
+
+    for s in range(args.warmup):
+        run_step(batches[s])
+    torch.cuda.synchronize(device)
+
+    fact_ms, fact_launch, fact_bytes = 0.0, 0, 0.0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        outs.append(run_step(batches[args.warmup + s]))
+        ms, nl, by = solver.kernel_stats()
+        fact_ms += ms
+        fact_launch += nl
+        fact_bytes += by
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    status = torch.cat([o["status"] for o in outs]).cpu().numpy()
+    sqp = torch.cat([o["sqp_iter"] for o in outs]).cpu().numpy()
+    total = world * args.steps * B
+    value = total / elapsed
+    avg_launch_ms = fact_ms / max(1, fact_launch)
+    achieved_gbs = (fact_bytes / max(1, fact_launch)) / (avg_launch_ms * 1e-3) / 1e9 if fact_launch else None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = len(os.sched_getaffinity(0))
+        threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+        v, n, t = cpu_baseline(nq, B, args.cpu_seconds, threads)
+        cpu = {"value": round(v, 2), "unit": "solves/s", "cores": threads, "kind": "port",
+               "sample": f"first {n} problems of the same workload (oracle/vboc_oracle.c, OpenMP, {t:.1f} s)"}
+
+    if rank == 0:
+        line = {
+            "metric": "VBOC boundary OCP solves/sec, triple pendulum, 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "solves/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Philox-seeded ICs by the reference's data_generation law)",
+            "config": {"workload": f"{'triple' if nq == 3 else nq}-pendulum data_generation first OCP solve, "
+                                   f"N=100, {B} ICs per GPU per step (configs[2]; configs[3] at 8 GPUs)",
+                       "problems_per_gpu": B, "horizon": 100, "parallelism": f"dp{world}",
+                       "allgather": world > 1},
+            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1) if achieved_gbs else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4) if achieved_gbs else None,
+                         "traffic": None, "kernel": "k_qp_factor<3>",
+                         "avg_launch_ms": round(avg_launch_ms, 4), "launches": fact_launch},
+            "cpu_baseline": cpu,
+            "solver": {"status_ok_frac": round(float(np.mean(status == 0)), 4),
+                       "sqp_iter_mean": round(float(sqp.mean()), 1), "sqp_iter_max": int(sqp.max())},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

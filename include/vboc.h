@@ -35,10 +35,12 @@
  *   lbx_0/ubx_0[b][nx]   stage-0 bounds q_init_lb/ub       (:180-181)
  *   lbx_e/ubx_e[b][nx]   terminal bounds q_fin_lb/ub       (:183-184)
  *   The stage-0 general constraint C = [0 | I - d d^T | 0], d = p[:nq], lg = ug = 0 (:174-178) is
- *   implied (as in OCP_solve).  Requirements (checked, VBOC_ERR_UNSUPPORTED otherwise): dt fixed
- *   (lb == ub on the dt column everywhere), stage-0 positions fixed, terminal velocities fixed.
+ *   implied (as in OCP_solve).  Requirements, checked per problem: dt fixed (lb == ub on the dt
+ *   column everywhere), stage-0 positions fixed, terminal velocities fixed, 1 <= N[b] <= nmax;
+ *   a problem outside them gets status 5 and is not solved.
  * Outputs:
- *   status[b]            0 success, 1 NaN, 2 max iter, 4 QP failure (ACADOS codes)
+ *   status[b]            0 success, 1 NaN, 2 max iter, 4 QP failure (ACADOS codes),
+ *                        5 unsupported problem structure
  *   x_out[b][nmax+1][nx], u_out[b][nmax][nu]  solution (rows beyond N[b] untouched)
  *   cost[b]              NLP cost at the solution (= get_cost())
  *   sqp_iter[b], qp_iter[b]  iteration counters (qp_iter summed over SQP iterations)
@@ -96,7 +98,9 @@ int vboc_destroy(vboc_handle h);
 int vboc_set_option(vboc_handle h, const char* field, double value);
 int vboc_get_option(vboc_handle h, const char* field, double* value);
 
-/* Batched solve, every pointer a DEVICE pointer (inputs resident in HBM); asynchronous on stream. */
+/* Batched solve, every pointer a DEVICE pointer (inputs resident in HBM).  Kernels are enqueued on
+ * `stream`; the call returns when every problem of the batch is finished (the SQP/IPM loops are
+ * host-driven and poll a device counter on that stream). */
 int vboc_solve_batch(vboc_handle h, const vboc_batch_t* batch, void* stream);
 /* Same with HOST pointers: staged through the handle's device buffers; synchronous. */
 int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* batch);
@@ -109,6 +113,12 @@ int vboc_rk4_batch_host(int nq, int B, double T, const double* x, const double* 
 /* Device time of the last vboc_solve_batch* call's solver kernel in milliseconds (HIP events on
  * the call's stream) and the number of kernel launches it used. */
 int vboc_last_kernel_ms(vboc_handle h, double* ms, int* launches);
+
+/* Dominant-kernel accounting of the last solve (enable with vboc_set_option(h, "profile_kernels", 1)):
+ * summed device time of the factorisation-sweep launches (HIP events recorded on the solve's
+ * stream around every k_qp_factor launch), their number, and the algorithmic HBM bytes they had
+ * to move (lane-stages factorised x bytes per stage; DESIGN.md "Roofline"). */
+int vboc_kernel_stats(vboc_handle h, double* factor_ms, long long* factor_launches, double* factor_bytes);
 
 const char* vboc_last_error(void);
 

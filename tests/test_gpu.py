@@ -1,0 +1,174 @@
+"""GPU parity tests: the HIP solver (through the C ABI) against the CPU oracle on the same seeded
+inputs, plus size-independent properties at larger sizes.  All marked `gpu`.
+
+Tolerances (FP64 everywhere): identical algorithm, different operation order / FMA contraction /
+libm, so results agree to rounding except where a rounding-level difference flips an SQP decision
+(line-search acceptance); then both runs still converge to a KKT point within the solver
+tolerance.  Stated bars:
+  * status agreement >= 98% of problems, SQP-iteration agreement >= 95%;
+  * problems converged on both: |cost_gpu - cost_cpu| median <= 1e-9, max <= 2e-3 (nlp tol_stat
+    1e-3); boundary state x0 the same bar;
+  * twin RK4 step vs the golden vectors from the reference expressions: 1e-13.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle(nq, b, **opts):
+    import oracle
+    o = oracle.default_opts(**opts)
+    return oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                              b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], opts=o)
+
+
+def _gpu(nq, b, **opts):
+    from vboc_amd import lib
+    s = lib.Solver(nq, int(np.max(b["N"])), slots=1024)
+    for k, v in opts.items():
+        s.set_option(k, v)
+    try:
+        return s.solve_host(b)
+    finally:
+        s.close()
+
+
+def _compare(nq, b, max_iter):
+    g = _gpu(nq, b, nlp_solver_max_iter=max_iter)
+    xo, uo, r = _oracle(nq, b, max_iter=max_iter)
+    assert np.mean(g["status"] == r["status"]) >= 0.98, (g["status"], r["status"])
+    assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= 0.95
+    both = (g["status"] == 0) & (r["status"] == 0)
+    assert both.sum() >= 0.5 * len(both)
+    dc = np.abs(g["cost"] - r["cost"])[both]
+    dx = np.abs(g["x"][:, 0, :2 * nq] - xo[:, 0, :2 * nq]).max(axis=1)[both]
+    assert np.median(dc) <= 1e-9 and dc.max() <= 2e-3, (np.median(dc), dc.max())
+    assert np.median(dx) <= 1e-9 and dx.max() <= 2e-3
+    # dt column and untouched rows follow the reference layout
+    for i in np.where(both)[0][:8]:
+        N = b["N"][i]
+        np.testing.assert_array_equal(g["x"][i, :N + 1, 2 * nq], b["lbx"][i, 2 * nq])
+    return g, r
+
+
+@pytest.mark.parametrize("nq,law,B", [(1, "heldout", 256), (2, "dg", 128), (3, "heldout", 96), (3, "dg", 96)])
+def test_parity_with_oracle(nq, law, B):
+    from vboc_amd.ics import data_generation_ics, heldout_ics
+    b = (data_generation_ics if law == "dg" else heldout_ics)(nq, np.arange(B))
+    _compare(nq, b, max_iter=200 if nq == 3 else 1000)
+
+
+def test_parity_ragged_horizons():
+    """Per-problem horizons inside one batch (the drivers' N+1 extensions / verification OCPs)."""
+    from vboc_amd.ics import data_generation_ics
+    parts = []
+    for j, N in enumerate((37, 100, 103, 64)):
+        parts.append(data_generation_ics(3, np.arange(16 * j, 16 * j + 16), N=N))
+    Nmax = 103
+    b = {}
+    for k in parts[0]:
+        if k in ("joint_sel", "vel_sel"):
+            continue
+        arrs = []
+        for p in parts:
+            a = p[k]
+            if k == "x_guess":
+                a = np.concatenate([a, np.repeat(a[:, -1:], Nmax + 1 - a.shape[1], 1)], 1)
+            if k == "u_guess":
+                a = np.concatenate([a, np.zeros((a.shape[0], Nmax - a.shape[1], a.shape[2]))], 1)
+            arrs.append(a)
+        b[k] = np.concatenate(arrs)
+    _compare(3, b, max_iter=150)
+
+
+def test_twin_integrator_matches_golden():
+    import os
+    from vboc_amd import lib
+    for nq in (1, 2, 3):
+        g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"dynamics_{nq}.npz"))
+        x1 = lib.rk4_host(nq, float(g["rk4_T"]), g["x"][:, :2 * nq], g["u"])
+        np.testing.assert_allclose(x1, g["rk4_x1"], rtol=1e-13, atol=1e-13)
+
+
+def test_device_path_equals_host_path():
+    import torch
+    from vboc_amd import lib
+    from vboc_amd.ics import heldout_ics
+    b = heldout_ics(2, np.arange(64))
+    s = lib.Solver(2, 100, slots=256)
+    host = s.solve_host(b)
+    dev = {k: torch.as_tensor(np.ascontiguousarray(b[k]), device="cuda") for k in lib.FIELDS_IN + ("N",)}
+    out = s.solve_device(dev)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), host["status"])
+    np.testing.assert_array_equal(out["x"].cpu().numpy(), host["x"])
+    s.close()
+
+
+def test_unsupported_structure_is_reported_per_problem():
+    from vboc_amd import lib
+    from vboc_amd.ics import heldout_ics
+    b = heldout_ics(3, np.arange(8))
+    b["ubx"] = b["ubx"].copy()
+    b["ubx"][3, 6] = 2e-2           # free time: dt not pinned
+    b["ubx0"] = b["ubx0"].copy()
+    b["ubx0"][5, 1] += 0.1          # stage-0 position not fixed
+    g = _gpu(3, b, nlp_solver_max_iter=100)
+    assert g["status"][3] == 5 and g["status"][5] == 5
+    assert np.all(np.isin(g["status"][[0, 1, 2, 4, 6, 7]], [0, 2]))
+
+
+def test_error_codes():
+    import ctypes
+    from vboc_amd import lib
+    so = lib.load()
+    h = ctypes.c_void_p()
+    assert so.vboc_create(3, 100, 256, 0, ctypes.byref(h)) == 0
+    assert so.vboc_set_option(h, b"no_such_option", ctypes.c_double(1.0)) == -1
+    assert b"no_such_option" in so.vboc_last_error()
+    assert so.vboc_solve_batch(h, None, None) == -1
+    so.vboc_destroy(h)
+
+
+def test_dropin_ocp_class_matches_oracle():
+    """OCPtriplependulumINIT.OCP_solve with the reference driver's first-solve arrays."""
+    from vboc_amd.ics import data_generation_ics
+    from vboc_amd.ocp import OCPtriplependulumINIT
+    b = data_generation_ics(3, np.arange(3))
+    ocp = OCPtriplependulumINIT()
+    xo, uo, r = _oracle(3, b)
+    for i in range(3):
+        N = ocp.N
+        st = ocp.OCP_solve(b["x_guess"][i, :N], b["u_guess"][i, :N], b["p"][i], b["lbx"][i], b["ubx"][i],
+                           b["lbu"][i], b["ubu"][i], b["lbx0"][i], b["ubx0"][i], b["lbxe"][i], b["ubxe"][i])
+        assert st == r["status"][i]
+        if st == 0:
+            assert abs(ocp.ocp_solver.get_cost() - r["cost"][i]) < 2e-3
+            np.testing.assert_allclose(ocp.ocp_solver.get(0, "x"), xo[i, 0], atol=2e-3)
+
+
+def test_full_batch_properties():
+    """Size-independent properties on a 16k-problem batch (beyond what the oracle can check in
+    seconds): every converged solution is dynamically feasible (re-simulated with the GPU twin
+    RK4), inside the boxes, ends at rest, starts along the cost direction, and the cost is the
+    boundary velocity along -p."""
+    from vboc_amd import lib
+    from vboc_amd.ics import data_generation_ics
+    nq, B = 3, 16384
+    b = data_generation_ics(nq, np.arange(10**6, 10**6 + B))
+    g = _gpu(nq, b, nlp_solver_max_iter=60)
+    ok = g["status"] == 0
+    assert ok.mean() > 0.5
+    X = g["x"][ok, :, :2 * nq]
+    U = g["u"][ok]
+    N = 100
+    x1 = lib.rk4_host(nq, 1e-2, X[:, :N].reshape(-1, 2 * nq), U[:, :N].reshape(-1, nq)).reshape(-1, N, 2 * nq)
+    assert np.abs(x1 - X[:, 1:N + 1]).max() < 1e-6
+    assert np.abs(X[:, N, nq:]).max() < 1e-6
+    assert np.all(np.abs(U) <= 10 + 1e-6) and np.all(np.abs(X[:, 1:N, nq:]) <= 10 + 1e-6)
+    assert np.all(X[:, 1:N, :nq] >= b["lbx"][0, 0] - 1e-6) and np.all(X[:, 1:N, :nq] <= b["ubx"][0, 0] + 1e-6)
+    d = b["p"][ok, :nq] / np.linalg.norm(b["p"][ok, :nq], axis=1, keepdims=True)
+    v0 = X[:, 0, nq:]
+    assert np.abs(v0 - d * np.sum(d * v0, 1, keepdims=True)).max() < 1e-9
+    np.testing.assert_allclose(g["cost"][ok], np.sum(b["p"][ok, :nq] * v0, 1), atol=1e-9)

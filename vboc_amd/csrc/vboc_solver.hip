@@ -22,10 +22,13 @@
 // reference line of every option and reformulation.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/vboc.h"
 #include "model.h"
@@ -183,6 +186,25 @@ struct Lane {
   // ---------------------------------------------------------------------------------------------
   // problem setup / output (per lane, divergent - once per problem)
   // ---------------------------------------------------------------------------------------------
+  // Reads problem `pid` into this slot.  Returns false (nothing loaded) if its structure is
+  // outside what the boundary-OCP solver implements: dt not pinned by the bounds, stage-0
+  // positions not fixed, terminal velocities not fixed, horizon out of range.
+  __device__ bool supported(const Inputs& in, int pid) const {
+    constexpr int NXR = NX + 1;
+    const int n = in.N[pid];
+    if (n < 1 || n > in.nmax) return false;
+    const double* lbx = in.lbx + (long long)pid * NXR;
+    const double* ubx = in.ubx + (long long)pid * NXR;
+    const double* lbx0 = in.lbx0 + (long long)pid * NXR;
+    const double* ubx0 = in.ubx0 + (long long)pid * NXR;
+    const double* lbxe = in.lbxe + (long long)pid * NXR;
+    const double* ubxe = in.ubxe + (long long)pid * NXR;
+    bool ok = lbx[NX] == ubx[NX] && lbx0[NX] == lbx[NX] && ubx0[NX] == lbx[NX] && lbxe[NX] == lbx[NX] &&
+              ubxe[NX] == lbx[NX] && lbx[NX] > 0.0;
+    UNR for (int j = 0; j < NQ; ++j) ok = ok && lbx0[j] == ubx0[j] && lbxe[NQ + j] == ubxe[NQ + j];
+    return ok;
+  }
+
   __device__ void load(const Inputs& in, int pid) {
     constexpr int NXR = NX + 1, NP = NQ + 1;
     N = in.N[pid];
@@ -1035,6 +1057,7 @@ struct SlotState {
   int* ist;          // [IS_COUNT][S]
   unsigned* done;    // problems finished
   unsigned* qp_active;  // lanes whose QP is still iterating
+  unsigned long long* work;  // [0] lane-stages swept by k_qp_factor (roofline accounting)
   long long S;
   __device__ __forceinline__ int& operator()(int f, unsigned slot) const { return ist[(long long)f * S + slot]; }
 };
@@ -1067,6 +1090,15 @@ __global__ __launch_bounds__(256) void k_refill(Work w, Opts o, Inputs in, SlotS
     return;
   }
   Lane<NQ> L(w, o, slot);
+  if (!L.supported(in, (int)cand)) {
+    in.status[cand] = 5;
+    in.cost[cand] = NAN;
+    in.sqp_iter[cand] = 0;
+    in.qp_iter[cand] = 0;
+    atomicAdd(ss.done, 1u);
+    ss(IS_PID, slot) = -1;   // pull another problem next round
+    return;
+  }
   L.load(in, (int)cand);
   ss(IS_PID, slot) = (int)cand;
   ss(IS_IT, slot) = 0;
@@ -1128,9 +1160,17 @@ __global__ __launch_bounds__(256) VBOC_WPE void k_qp_init(Work w, Opts o, Inputs
 template <int NQ>
 __global__ __launch_bounds__(256) VBOC_WPE void k_qp_factor(Work w, Opts o, Inputs in, SlotState ss) {
   Lane<NQ> L(w, o, blockIdx.x * blockDim.x + threadIdx.x);
-  if (!qp_prologue(L, ss)) return;
-  int st = L.qp_check();
-  if (st == 1 && ss(IS_QCUR, L.slot) >= o.qp_max_iter) st = 2;
+  const bool act = qp_prologue(L, ss);
+  int st = 0;
+  if (act) {
+    st = L.qp_check();
+    if (st == 1 && ss(IS_QCUR, L.slot) >= o.qp_max_iter) st = 2;
+  }
+  // roofline accounting: lane-stages factorised by this launch (all lanes still present here)
+  unsigned long long n = (act && st == 1) ? (unsigned long long)(L.N - 1) : 0ull;  // middle stages
+  UNR for (int off = 32; off >= 1; off >>= 1) n += __shfl_xor(n, off);
+  if ((threadIdx.x & 63) == 0 && n) atomicAdd(ss.work, n);
+  if (!act) return;
   if (st == 1 && !L.qp_factor()) st = -1;
   if (st != 1) {
     ss(IS_QST, L.slot) = st;
@@ -1252,6 +1292,13 @@ struct vboc_solver {
   unsigned int* host_done = nullptr;  // pinned mirror of head[1]
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int launches = 0;
+  // optional per-launch timing of the dominant kernel (k_qp_factor) - HIP events on the launch stream
+  bool profile = false;
+  std::vector<hipEvent_t> pev;   // pairs
+  int npev = 0;
+  double fact_ms = 0.0;
+  long long fact_calls = 0;
+  unsigned long long fact_stages = 0;
   // host staging for vboc_solve_batch_host
   void* stage = nullptr;
   size_t stage_bytes = 0;
@@ -1280,6 +1327,21 @@ static size_t work_doubles_per_slot(int nq, int nmax) {
   return per_stage * (size_t)(nmax + 1) + per_slot;
 }
 
+static hipError_t prof_flush(vboc_solver* h, hipStream_t st) {
+  if (!h->npev) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return e;
+  for (int i = 0; i < h->npev; ++i) {
+    float f = 0.f;
+    e = hipEventElapsedTime(&f, h->pev[2 * i], h->pev[2 * i + 1]);
+    if (e != hipSuccess) return e;
+    h->fact_ms += f;
+  }
+  h->fact_calls += h->npev;
+  h->npev = 0;
+  return hipSuccess;
+}
+
 // One SQP iteration of every resident problem: refill, linearise, QP (host-driven interior-point
 // loop, one kernel per sweep, exits once no lane is iterating), line search + update.
 template <int NQ>
@@ -1293,7 +1355,20 @@ static hipError_t launch_round(vboc_solver* h, dim3 grid, dim3 block, hipStream_
   hipLaunchKernelGGL(k_qp_init<NQ>, grid, block, 0, st, w, o, in, ss);
   h->launches += 5;
   for (int it = 0; it <= o.qp_max_iter; ++it) {
+    if (h->profile) {
+      if ((size_t)(2 * h->npev + 2) > h->pev.size()) {
+        e = prof_flush(h, st);
+        if (e != hipSuccess) return e;
+      }
+      e = hipEventRecord(h->pev[2 * h->npev], st);
+      if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_qp_factor<NQ>, grid, block, 0, st, w, o, in, ss);
+    if (h->profile) {
+      e = hipEventRecord(h->pev[2 * h->npev + 1], st);
+      if (e != hipSuccess) return e;
+      ++h->npev;
+    }
     ++h->launches;
     // poll the active-lane counter (one host sync) from the 6th iteration on, every other one
     if (it >= 6 && (it & 1) == 0) {
@@ -1381,6 +1456,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->stage) (void)hipFree(h->stage);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
+  for (auto ev : h->pev) (void)hipEventDestroy(ev);
   delete h;
   return VBOC_OK;
 }
@@ -1404,7 +1480,14 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "ipm_mu0") o.mu0 = v;
   else if (s == "ipm_push") o.push = v;
   else if (s == "ipm_tau") o.tau = v;
-  else return fail(VBOC_ERR_ARG, "vboc_set_option: unknown field '" + s + "'");
+  else if (s == "profile_kernels") {
+    h->profile = v != 0.0;
+    if (h->profile && h->pev.empty()) {
+      h->pev.resize(2 * 4096);
+      for (auto& ev : h->pev)
+        if (hipEventCreate(&ev) != hipSuccess) return fail(VBOC_ERR_HIP, "vboc_set_option: hipEventCreate");
+    }
+  } else return fail(VBOC_ERR_ARG, "vboc_set_option: unknown field '" + s + "'");
   return VBOC_OK;
 }
 
@@ -1452,11 +1535,15 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   in.status = b->status; in.xo = b->x_out; in.uo = b->u_out; in.cost = b->cost; in.sqp_iter = b->sqp_iter;
   in.qp_iter = b->qp_iter; in.head = h->head;
   HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
+  h->fact_ms = 0.0;
+  h->fact_calls = 0;
+  h->fact_stages = 0;
+  h->npev = 0;
   // lanes: never more than the problems (rounded to whole workgroups), never more than the slots
   long long lanes = ((long long)b->B + 255) / 256 * 256;
   if (lanes > h->slots) lanes = h->slots;
   Work w = h->w;  // same carve, S = full slot stride
-  SlotState ss{h->ist, h->head + 1, h->head + 2, h->slots};
+  SlotState ss{h->ist, h->head + 1, h->head + 2, (unsigned long long*)(h->head + 4), h->slots};
   const dim3 grid((unsigned)(lanes / 256)), block(256);
   HIPCHK(hipEventRecord(h->ev0, st));
   hipLaunchKernelGGL(k_slots_init, dim3((unsigned)((h->slots + 255) / 256)), block, 0, st, h->ist, h->slots);
@@ -1465,6 +1552,9 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   const int chunk = 4;
   long long rounds = 0;
   h->launches = 1;
+  const bool progress = getenv("VBOC_PROGRESS") != nullptr;
+  auto t_start = std::chrono::steady_clock::now();
+  unsigned last_print = 0;
   for (;;) {
     for (int r = 0; r < chunk; ++r) {
       hipError_t le;
@@ -1479,12 +1569,21 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(h->host_done, h->head + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (progress && (*h->host_done - last_print >= (unsigned)b->B / 20 || *h->host_done >= (unsigned)b->B ||
+                     rounds % 64 == 0)) {
+      const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+      fprintf(stderr, "[vboc] %.1f ms rounds %lld done %u / %d\n", ms, rounds, *h->host_done, b->B);
+      last_print = *h->host_done;
+    }
     if (*h->host_done >= (unsigned)b->B) break;
     if (rounds > 4LL * (h->o.max_iter + 2) * ((b->B + lanes - 1) / lanes + 1))
       return fail(VBOC_ERR_HIP, "vboc_solve_batch: solver did not drain (internal error)");
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(h->ev1, st));
+  if (h->profile) HIPCHK(prof_flush(h, st));
+  HIPCHK(hipMemcpyAsync(&h->fact_stages, h->head + 4, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
   return VBOC_OK;
 }
 
@@ -1495,6 +1594,19 @@ int vboc_last_kernel_ms(vboc_handle h, double* ms, int* launches) {
   HIPCHK(hipEventElapsedTime(&f, h->ev0, h->ev1));
   *ms = f;
   if (launches) *launches = h->launches;
+  return VBOC_OK;
+}
+
+int vboc_kernel_stats(vboc_handle h, double* factor_ms, long long* factor_launches, double* factor_bytes) {
+  if (!h || !factor_ms || !factor_launches || !factor_bytes) return fail(VBOC_ERR_ARG, "vboc_kernel_stats: NULL argument");
+  const int nq = h->nq, NX = 2 * nq, NU = nq, NZ = 3 * nq;
+  // algorithmic bytes of one middle stage of the factorisation sweep (k_qp_factor):
+  //   reads  A, B, e, (dz, lambda_l, lambda_u), (x, u)   writes K, chol(Ru), M, Y, P e, k
+  const double loads = NX * NX + NX * NU + NX + 3 * NZ + NZ;
+  const double stores = NU * NX + NU * NU + 2 * NU * nq + NX + NU;
+  *factor_ms = h->fact_ms;
+  *factor_launches = h->fact_calls;
+  *factor_bytes = (loads + stores) * 8.0 * (double)h->fact_stages;
   return VBOC_OK;
 }
 

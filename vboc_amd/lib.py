@@ -17,9 +17,9 @@ SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
            "vboc_solve_batch_host", "vboc_rk4_batch", "vboc_rk4_batch_host", "vboc_last_kernel_ms",
-           "vboc_last_error")
+           "vboc_kernel_stats", "vboc_last_error")
 
-STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure"}
+STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
 
 
 class VbocError(RuntimeError):
@@ -72,6 +72,8 @@ def load():
                                         ctypes.c_void_p, ctypes.c_void_p]
     lib.vboc_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int)]
+    lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
     return lib
 
@@ -163,6 +165,12 @@ class Solver:
         st = stream if stream is not None else torch.cuda.current_stream()
         _check(self.lib.vboc_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
         return out
+
+    def kernel_stats(self):
+        """(factor_ms_total, factor_launches, factor_algorithmic_bytes) of the last solve."""
+        ms, n, by = ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+        _check(self.lib.vboc_kernel_stats(self.h, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(by)))
+        return ms.value, n.value, by.value
 
     def last_kernel_ms(self):
         ms = ctypes.c_double()
