@@ -25,7 +25,7 @@ def _oracle(nq, b, **opts):
 
 def _gpu(nq, b, **opts):
     from vboc_amd import lib
-    s = lib.Solver(nq, int(np.max(b["N"])), slots=1024)
+    s = lib.Solver(nq, int(np.max(b["N"])), slots=opts.pop("slots", 1024))
     for k, v in opts.items():
         s.set_option(k, v)
     try:
@@ -34,8 +34,8 @@ def _gpu(nq, b, **opts):
         s.close()
 
 
-def _compare(nq, b, max_iter):
-    g = _gpu(nq, b, nlp_solver_max_iter=max_iter)
+def _compare(nq, b, max_iter, coop=8192):
+    g = _gpu(nq, b, nlp_solver_max_iter=max_iter, coop_threshold=coop)
     xo, uo, r = _oracle(nq, b, max_iter=max_iter)
     assert np.mean(g["status"] == r["status"]) >= 0.98, (g["status"], r["status"])
     assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= 0.95
@@ -52,11 +52,30 @@ def _compare(nq, b, max_iter):
     return g, r
 
 
+# mode "lane": every SQP iteration in the lane-per-problem kernels (coop_threshold 0);
+# mode "coop": 4 lane-mode rounds, then the cooperative LDS-resident tail solver (coop.h) finishes
+# every problem (the queue of these small batches is drained at once).
+@pytest.mark.parametrize("mode", ["lane", "coop"])
 @pytest.mark.parametrize("nq,law,B", [(1, "heldout", 256), (2, "dg", 128), (3, "heldout", 96), (3, "dg", 96)])
-def test_parity_with_oracle(nq, law, B):
+def test_parity_with_oracle(nq, law, B, mode):
     from vboc_amd.ics import data_generation_ics, heldout_ics
     b = (data_generation_ics if law == "dg" else heldout_ics)(nq, np.arange(B))
-    _compare(nq, b, max_iter=200 if nq == 3 else 1000)
+    _compare(nq, b, max_iter=200 if nq == 3 else 1000, coop=0 if mode == "lane" else 1e9)
+
+
+def test_coop_tail_is_used():
+    from vboc_amd import lib
+    from vboc_amd.ics import heldout_ics
+    b = heldout_ics(3, np.arange(64))
+    s = lib.Solver(3, 100, slots=256)
+    assert s.get_option("coop_available") == 1.0
+    s.set_option("coop_threshold", 1e9)
+    s.solve_host(b)
+    assert s.get_option("coop_problems") > 0
+    s.set_option("coop_threshold", 0)
+    s.solve_host(b)
+    assert s.get_option("coop_problems") == 0
+    s.close()
 
 
 def test_parity_ragged_horizons():
@@ -79,7 +98,8 @@ def test_parity_ragged_horizons():
                 a = np.concatenate([a, np.zeros((a.shape[0], Nmax - a.shape[1], a.shape[2]))], 1)
             arrs.append(a)
         b[k] = np.concatenate(arrs)
-    _compare(3, b, max_iter=150)
+    _compare(3, b, max_iter=150, coop=0)
+    _compare(3, b, max_iter=150, coop=1e9)
 
 
 def test_twin_integrator_matches_golden():

@@ -15,9 +15,12 @@ sizes = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [4096
 slots = int(sys.argv[3]) if len(sys.argv) > 3 else 0
 law = sys.argv[4] if len(sys.argv) > 4 else "dg"
 max_iter = int(sys.argv[5]) if len(sys.argv) > 5 else 0
-for B in sizes:
+coops = [float(x) for x in sys.argv[6].split(",")] if len(sys.argv) > 6 else [None]
+for B, coop in [(B, c) for B in sizes for c in coops]:
     b = (data_generation_ics if law == "dg" else heldout_ics)(nq, np.arange(B))
     s = lib.Solver(nq, int(b["N"].max()), slots=slots)
+    if coop is not None:
+        s.set_option("coop_threshold", coop)
     if max_iter:
         s.set_option("nlp_solver_max_iter", max_iter)
     t = time.time()
@@ -25,7 +28,8 @@ for B in sizes:
     tw = time.time() - t
     ms, nl = s.last_kernel_ms()
     it = g["sqp_iter"]
-    print(f"nq={nq} law={law} B={B} slots={s.get_option('slots'):.0f}: wall {tw:.2f}s device {ms:.1f} ms "
+    print(f"nq={nq} law={law} B={B} coop={coop} ({s.get_option('coop_problems'):.0f}) "
+          f"slots={s.get_option('slots'):.0f}: wall {tw:.2f}s device {ms:.1f} ms "
           f"launches {nl} -> {B / (ms / 1e3):.0f} solves/s | ok {np.mean(g['status'] == 0):.4f} "
           f"sqp mean {it.mean():.1f} p99 {np.percentile(it, 99):.0f} max {it.max()} | qp/sqp "
           f"{g['qp_iter'].sum() / max(1, it.sum()):.1f}", flush=True)

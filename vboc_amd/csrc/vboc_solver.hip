@@ -1265,6 +1265,8 @@ __global__ __launch_bounds__(256) void rk4_kernel(int B, double T, const double*
 
 }  // namespace vboc
 
+#include "coop.h"
+
 // =================================================================================================
 // C ABI
 // =================================================================================================
@@ -1302,6 +1304,13 @@ struct vboc_solver {
   // host staging for vboc_solve_batch_host
   void* stage = nullptr;
   size_t stage_bytes = 0;
+  // cooperative tail (coop.h): once the queue is drained and at most coop_threshold problems are
+  // still iterating, each of them moves to one LDS-resident wave
+  int* list = nullptr;
+  double coop_threshold = 8192;
+  size_t coop_lds = 0;
+  bool coop_ok = false;
+  long long coop_count = 0;
 };
 
 static void default_opts(Opts& o) {
@@ -1416,6 +1425,7 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   }
   e = hipMalloc((void**)&h->head, 256);
   if (e == hipSuccess) e = hipMalloc((void**)&h->ist, sizeof(int) * IS_COUNT * (size_t)slots);
+  if (e == hipSuccess) e = hipMalloc((void**)&h->list, sizeof(int) * (size_t)slots);
   if (e == hipSuccess) e = hipHostMalloc((void**)&h->host_done, 64);
   if (e != hipSuccess) {
     vboc_destroy(h);
@@ -1423,6 +1433,15 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   }
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);
+  // cooperative tail: the whole problem must fit one workgroup's LDS (160 KiB on gfx950)
+  h->coop_lds = nq == 1 ? CoopLayout<1>::lds_bytes(nmax) : (nq == 2 ? CoopLayout<2>::lds_bytes(nmax)
+                                                                      : CoopLayout<3>::lds_bytes(nmax));
+  h->coop_ok = h->coop_lds <= 160 * 1024;
+  if (h->coop_ok) {
+    const void* fn = nq == 1 ? (const void*)k_coop<1> : (nq == 2 ? (const void*)k_coop<2> : (const void*)k_coop<3>);
+    h->coop_ok = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->coop_lds) == hipSuccess;
+    (void)hipGetLastError();
+  }
   // carve the workspace
   const int NX = 2 * nq, NU = nq, NZ = 3 * nq, M0 = nq + 1;
   const size_t st = (size_t)(nmax + 1) * slots;
@@ -1452,6 +1471,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->pool) (void)hipFree(h->pool);
   if (h->head) (void)hipFree(h->head);
   if (h->ist) (void)hipFree(h->ist);
+  if (h->list) (void)hipFree(h->list);
   if (h->host_done) (void)hipHostFree(h->host_done);
   if (h->stage) (void)hipFree(h->stage);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -1480,6 +1500,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "ipm_mu0") o.mu0 = v;
   else if (s == "ipm_push") o.push = v;
   else if (s == "ipm_tau") o.tau = v;
+  else if (s == "coop_threshold") h->coop_threshold = v;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
     if (h->profile && h->pev.empty()) {
@@ -1510,6 +1531,9 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "ipm_mu0") *v = o.mu0;
   else if (s == "ipm_push") *v = o.push;
   else if (s == "ipm_tau") *v = o.tau;
+  else if (s == "coop_threshold") *v = h->coop_threshold;
+  else if (s == "coop_available") *v = h->coop_ok ? 1.0 : 0.0;
+  else if (s == "coop_problems") *v = (double)h->coop_count;
   else if (s == "slots") *v = (double)h->slots;
   else if (s == "workspace_bytes") *v = (double)h->pool_bytes;
   else return fail(VBOC_ERR_ARG, "vboc_get_option: unknown field '" + s + "'");
@@ -1539,6 +1563,7 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   h->fact_calls = 0;
   h->fact_stages = 0;
   h->npev = 0;
+  h->coop_count = 0;
   // lanes: never more than the problems (rounded to whole workgroups), never more than the slots
   long long lanes = ((long long)b->B + 255) / 256 * 256;
   if (lanes > h->slots) lanes = h->slots;
@@ -1567,8 +1592,36 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
     }
     rounds += chunk;
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(h->host_done, h->head + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h->host_done + 4, h->head, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    h->host_done[0] = h->host_done[5];
+    const unsigned pulled = h->host_done[4] < (unsigned)b->B ? h->host_done[4] : (unsigned)b->B;
+    if (h->coop_ok && h->coop_threshold > 0 && h->host_done[4] >= (unsigned)b->B &&
+        (double)(pulled - h->host_done[0]) <= h->coop_threshold && h->host_done[0] < (unsigned)b->B) {
+      // queue drained, few problems left: finish each of them on one LDS-resident wave
+      HIPCHK(hipMemsetAsync(h->head + 3, 0, sizeof(unsigned), st));
+      hipLaunchKernelGGL(k_list, grid, block, 0, st, ss, h->list, h->head + 3);
+      HIPCHK(hipMemcpyAsync(h->host_done + 2, h->head + 3, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      const unsigned n = h->host_done[2];
+      h->coop_count = n;
+      if (n) {
+        switch (h->nq) {
+          case 1: hipLaunchKernelGGL(k_coop<1>, dim3(n), dim3(64), h->coop_lds, st, w, h->o, in, ss, h->list, h->nmax); break;
+          case 2: hipLaunchKernelGGL(k_coop<2>, dim3(n), dim3(64), h->coop_lds, st, w, h->o, in, ss, h->list, h->nmax); break;
+          default: hipLaunchKernelGGL(k_coop<3>, dim3(n), dim3(64), h->coop_lds, st, w, h->o, in, ss, h->list, h->nmax); break;
+        }
+        h->launches += 2;
+        HIPCHK(hipGetLastError());
+      }
+      HIPCHK(hipMemcpyAsync(h->host_done, h->head + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (progress) {
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+        fprintf(stderr, "[vboc] %.1f ms cooperative tail: %u problems, done %u / %d\n", ms, n, *h->host_done, b->B);
+      }
+      if (*h->host_done < (unsigned)b->B) return fail(VBOC_ERR_HIP, "vboc_solve_batch: cooperative tail did not finish");
+    }
     if (progress && (*h->host_done - last_print >= (unsigned)b->B / 20 || *h->host_done >= (unsigned)b->B ||
                      rounds % 64 == 0)) {
       const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();

@@ -12,7 +12,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libvboc_amd.so")
+# VBOC_LIB selects another in-tree build of the same sources (e.g. the phase-profiling build
+# libvboc_amd_prof.so made with -DVBOC_COOP_PROF); default: the product library.
+LIB_PATH = os.environ.get("VBOC_LIB") or os.path.join(HERE, "libvboc_amd.so")
 SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
