@@ -25,6 +25,23 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak
+# SURVEY.md 8(d) algorithmic FLOP convention (triple n=7, m=3; double n=5, m=2; pendulum n=3, m=1)
+F_DYN = {3: 6382, 2: 2146, 1: 4 * 14 + 8 * 9 * 4 + 8 * 3 * 4 + 6}
+F_IPM = {3: 3513, 2: 1346, 1: int(2 * 9 * 4 + 2 * 3 * 16 + 64 / 3 + 8 * 16)}
+C_F = {3: 183, 2: 52, 1: 8}
+
+
+def pmc_traffic(kernel):
+    """HBM traffic per launch of `kernel` from the newest committed rocprofv3 PMC summary
+    (profiles/*_pmc_<kernel>.json, made by tools/pmc_summary.py from FETCH_SIZE / WRITE_SIZE passes of
+    this bench command, gfx950-corrected).  None if there is none."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{kernel}.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d["traffic_bytes_per_launch"] / 1e9, os.path.relpath(files[-1], ROOT)
 
 
 def make_batch(nq, ids, device):
@@ -128,6 +145,15 @@ def main():
 
     status = torch.cat([o["status"] for o in outs]).cpu().numpy()
     sqp = torch.cat([o["sqp_iter"] for o in outs]).cpu().numpy()
+    qpi = torch.cat([o["qp_iter"] for o in outs]).cpu().numpy()
+    # whole-path FP64 work by the SURVEY 8(d) convention, with the solver's reported K_sqp and K_ipm;
+    # K_ls counted as 2 merit evaluations per SQP iteration (phi(0) + one trial: a lower bound)
+    Nh = 100
+    flops = float(np.sum(Nh * (F_DYN[nq] * sqp + F_IPM[nq] * qpi + 2 * 4 * C_F[nq] * sqp)))
+    if world > 1:
+        ft = torch.tensor([flops], device=device, dtype=torch.float64)
+        dist.all_reduce(ft)
+        flops = float(ft.item())
     total = world * args.steps * B
     value = total / elapsed
     avg_launch_ms = fact_ms / max(1, fact_launch)
@@ -141,6 +167,7 @@ def main():
         cpu = {"value": round(v, 2), "unit": "solves/s", "cores": threads, "kind": "port",
                "sample": f"first {n} problems of the same workload (oracle/vboc_oracle.c, OpenMP, {t:.1f} s)"}
 
+    traffic_gb, traffic_src = pmc_traffic("k_qp_factor")
     if rank == 0:
         line = {
             "metric": "VBOC boundary OCP solves/sec, triple pendulum, 1/2/4/8 MI355X",
@@ -162,8 +189,14 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1) if achieved_gbs else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved_gbs / HBM_PEAK_GBS, 4) if achieved_gbs else None,
-                         "traffic": None, "kernel": "k_qp_factor<3>",
+                         "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
+                         "traffic_source": traffic_src,
+                         "algorithmic_gb_per_launch": round(fact_bytes / max(1, fact_launch) / 1e9, 4),
+                         "kernel": "k_qp_factor<3>",
                          "avg_launch_ms": round(avg_launch_ms, 4), "launches": fact_launch},
+            "path_fp64": {"achieved": round(flops / elapsed / 1e12, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": round(flops / elapsed / 1e12 / FP64_PEAK_TFLOPS, 5),
+                          "convention": "SURVEY.md 8(d): N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp)"},
             "cpu_baseline": cpu,
             "solver": {"status_ok_frac": round(float(np.mean(status == 0)), 4),
                        "sqp_iter_mean": round(float(sqp.mean()), 1), "sqp_iter_max": int(sqp.max())},

@@ -1,0 +1,40 @@
+"""Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+Usage: python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv>
+       <bench_line.json> [kernel-substring] > profiles/<round>_pmc_<kernel>.json
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE (KB) reports half the bytes of wide
+coalesced streaming reads, so it is doubled; WRITE_SIZE (KB) is taken as is.  The algorithmic bytes
+per launch come from the bench line of the same (warmup 0) run: roofline.achieved x avg_launch_ms.
+"""
+import csv
+import json
+import sys
+
+
+def total(path, counter, kernel):
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if r["Counter_Name"] == counter and kernel in r["Kernel_Name"]]
+    return sum(vals), len(vals)
+
+
+def main():
+    fetch_csv, write_csv, bench_json = sys.argv[1:4]
+    kernel = sys.argv[4] if len(sys.argv) > 4 else "k_qp_factor"
+    fs, nf = total(fetch_csv, "FETCH_SIZE", kernel)
+    ws, nw = total(write_csv, "WRITE_SIZE", kernel)
+    line = json.loads(open(bench_json).read().strip().splitlines()[-1])
+    rf = line["roofline"]
+    alg = rf["achieved"] * 1e9 * rf["avg_launch_ms"] * 1e-3
+    fetch_b = 2.0 * fs * 1024 / nf
+    write_b = ws * 1024 / nw
+    out = {"kernel": kernel, "launches_fetch_pass": nf, "launches_write_pass": nw,
+           "fetch_bytes_per_launch_corrected": fetch_b, "write_bytes_per_launch": write_b,
+           "traffic_bytes_per_launch": fetch_b + write_b,
+           "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (fetch_b + write_b) / alg,
+           "correction": "FETCH_SIZE x2 (gfx950), KB -> bytes x1024"}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
