@@ -120,6 +120,12 @@ int vboc_last_kernel_ms(vboc_handle h, double* ms, int* launches);
  * to move (lane-stages factorised x bytes per stage; DESIGN.md "Roofline"). */
 int vboc_kernel_stats(vboc_handle h, double* factor_ms, long long* factor_launches, double* factor_bytes);
 
+/* Diagnostics: per-phase shader-clock cycles of the wave solver summed over all jobs since the last
+ * call (then reset): [0] linearise [1] IPM init [2] H/g preparation [3] factorisation [4] vector
+ * passes [5] forward sweeps [6] update [7] costate [8] line search + step, [9] SQP iterations,
+ * [10] IPM iterations.  All zero unless the library was built with -DVBOC_COOP_PROF. */
+int vboc_debug_counters(unsigned long long* out16);
+
 const char* vboc_last_error(void);
 
 #ifdef __cplusplus

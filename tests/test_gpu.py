@@ -34,8 +34,8 @@ def _gpu(nq, b, **opts):
         s.close()
 
 
-def _compare(nq, b, max_iter, coop=8192):
-    g = _gpu(nq, b, nlp_solver_max_iter=max_iter, coop_threshold=coop)
+def _compare(nq, b, max_iter, coop=8192, wave=0):
+    g = _gpu(nq, b, nlp_solver_max_iter=max_iter, coop_threshold=coop, wave_all=wave)
     xo, uo, r = _oracle(nq, b, max_iter=max_iter)
     assert np.mean(g["status"] == r["status"]) >= 0.98, (g["status"], r["status"])
     assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= 0.95
@@ -53,14 +53,16 @@ def _compare(nq, b, max_iter, coop=8192):
 
 
 # mode "lane": every SQP iteration in the lane-per-problem kernels (coop_threshold 0);
-# mode "coop": 4 lane-mode rounds, then the cooperative LDS-resident tail solver (coop.h) finishes
-# every problem (the queue of these small batches is drained at once).
-@pytest.mark.parametrize("mode", ["lane", "coop"])
+# mode "coop": 4 lane-mode rounds, then the wave solver (coop.h) takes over every problem still
+# iterating (the queue of these small batches is drained at once);
+# mode "wave": every problem solved start-to-end by the wave solver (wave_all).
+@pytest.mark.parametrize("mode", ["lane", "coop", "wave"])
 @pytest.mark.parametrize("nq,law,B", [(1, "heldout", 256), (2, "dg", 128), (3, "heldout", 96), (3, "dg", 96)])
 def test_parity_with_oracle(nq, law, B, mode):
     from vboc_amd.ics import data_generation_ics, heldout_ics
     b = (data_generation_ics if law == "dg" else heldout_ics)(nq, np.arange(B))
-    _compare(nq, b, max_iter=200 if nq == 3 else 1000, coop=0 if mode == "lane" else 1e9)
+    _compare(nq, b, max_iter=200 if nq == 3 else 1000, coop=0 if mode == "lane" else 1e9,
+             wave=1 if mode == "wave" else 0)
 
 
 def test_coop_tail_is_used():
@@ -69,12 +71,17 @@ def test_coop_tail_is_used():
     b = heldout_ics(3, np.arange(64))
     s = lib.Solver(3, 100, slots=256)
     assert s.get_option("coop_available") == 1.0
+    assert s.get_option("wave_all") == 1.0          # default: every problem on the wave solver
+    s.set_option("wave_all", 0)
     s.set_option("coop_threshold", 1e9)
     s.solve_host(b)
     assert s.get_option("coop_problems") > 0
     s.set_option("coop_threshold", 0)
     s.solve_host(b)
     assert s.get_option("coop_problems") == 0
+    s.set_option("wave_all", 1)
+    s.solve_host(b)
+    assert s.get_option("coop_problems") == 64
     s.close()
 
 
@@ -100,6 +107,7 @@ def test_parity_ragged_horizons():
         b[k] = np.concatenate(arrs)
     _compare(3, b, max_iter=150, coop=0)
     _compare(3, b, max_iter=150, coop=1e9)
+    _compare(3, b, max_iter=150, wave=1)
 
 
 def test_twin_integrator_matches_golden():

@@ -1,49 +1,71 @@
-// coop.h - cooperative tail solver: ONE boundary OCP per wave, every stage array resident in LDS.
+// coop.h - wave solver: ONE boundary OCP per wave (64 lanes cooperate on one problem).
 //
-// Why: the lane-per-problem kernels (vboc_solver.hip) are bandwidth-efficient while tens of
-// thousands of problems are resident, but the SQP iteration count has a long tail (a few percent of
-// the problems take 300-1000 iterations).  Once only those remain, a lane-mode sweep is a serial
-// chain of ~100 stage bodies of ~4k instructions each on an almost empty GPU, so one SQP iteration
-// costs ~100 ms.  Here the 64 lanes of a wave cooperate on one problem instead:
+// Why: the lane-per-problem kernels (vboc_solver.hip) stream stage data at full HBM rate while every
+// lane of a wave is iterating, but SQP/IPM iteration counts differ wildly between problems (SQP
+// median ~20, a few percent at 300-1000; IPM 5-50 per SQP iteration), so lane-mode waves turn sparse
+// (a masked wave still fetches whole lines and waits for its slowest lane).  Here a problem owns a
+// wave and runs its own SQP/IPM loop to termination inside one persistent kernel:
 //   * stage-parallel passes (linearisation + sensitivities, residuals, IPM initial point,
 //     Hessian/gradient preparation, step-length tests, iterate update, merit re-simulation,
 //     weights, step application): lane j owns stages j, j+64, ...;
 //   * the Riccati factorisation recursion: per stage three "dot-product steps" in which every lane
 //     computes one entry of P A, P B, A'PA, B'PB, B'PA, B'Pi, A'Pi+K'Y, ... from operands in LDS
 //     (per-lane descriptor tables, so the 64 lanes run ONE instruction stream - no divergence),
-//     plus one step where all lanes factorise Ru redundantly and lanes solve one column each;
+//     plus one step where all lanes factorise Ru redundantly (rsq + Newton, no division) and lanes
+//     solve one column each;
 //   * the vector, forward and costate recursions in closed-loop form, A_cl = A + B K, one short
 //     dependent step per stage on NX lanes.
+// Storage: each problem's stage records live in a problem-major region in HBM (L2/MALL-resident
+// while it is being solved); LDS holds only the recursion state, parameters, scratch and a 3-slot
+// ring of stage windows that the recursions prefetch two stages ahead (16-B loads) and write back.
+// LDS per problem is ~8 KB, so several problems share a CU (occupancy is set by registers).
 // The arithmetic is the algorithm of Lane<NQ> / oracle/vboc_oracle.c (same formulas, same
 // decisions); only summation orders differ (rounding-level).
-//
-// LDS layout (doubles): stage record k at [k * REC, (k + 1) * REC), then a fixed region.
 #pragma once
 
 namespace vboc {
 
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) dbl2 gdbl2;
+
+__host__ __device__ constexpr int even_up(int v) { return (v + 1) & ~1; }
+
 template <int NQ>
-struct CoopLayout {
+struct WaveLayout {
   static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1;
-  // stage record: A, B, z (current iterate), dz, lambda_l, lambda_u, e (defect -> initial residual),
-  // K, k_f, chol(Ru), M, Y, P e, D (H / g_corr / corrector direction), DA (g_pred / affine
-  // direction / costate), V (v = P e + p of the vector pass)
+  // global stage record: A, B, z (current iterate), dz, lambda_l, lambda_u, e (defect -> initial
+  // residual), K, k_f, chol(Ru), M, Y, P e, D (H / g_corr / corrector direction), DA (g_pred /
+  // affine direction / costate), V (v = P e + p), then the SQP state x, u, pi, lam_l, lam_u, w_pi
   static constexpr int OA = 0, OB = OA + NX * NX, OZ = OB + NX * NU, ODZ = OZ + NZ, OQL = ODZ + NZ, OQU = OQL + NZ,
-                       OE = OQU + NZ, OK = OE + NX, OKF = OK + NU * NX, OLR = OKF + NU, OM = OLR + NU * NU,
-                       OY = OM + NU * NQ, OPE = OY + NU * NQ, OD = OPE + NX, ODA = OD + NZ, OV = ODA + NZ,
-                       REC = (OV + NX) | 1;
-  // fixed region: stage-0 blocks, recursion scratch, constants, parameters
-  static constexpr int F0 = 0, LR0 = F0 + NX * M0, MM0 = LR0 + M0 * M0, Y0 = MM0 + M0 * NQ, PE0 = Y0 + M0 * NQ,
-                       P = PE0 + NX, PA = P + NX * NX, PB = PA + NX * NX, APA = PB + NX * NU, RU = APA + NX * NX,
-                       S = RU + NU * NU, PI = S + NU * NX, PV = PI + NX * NQ, SC = PV + 2 * NX, LINE = SC + NQ * NQ,
-                       ZERO = LINE + NQ, TRASH = ZERO + 16, PAR = TRASH + 64, FIXN = PAR + Par<NQ>::COUNT;
+                       OE = OQU + NZ, OD = OE + NX, ODA = OD + NZ, OK = ODA + NZ, OKF = OK + NU * NX,
+                       OLR = OKF + NU, OM = OLR + NU * NU, OY = OM + NU * NQ, OPE = OY + NU * NQ, OC = OPE + NX,
+                       OACL = OC + NX, OX = OACL + NX * NX, OU = OX + NX, OPI = OU + NU, OLL = OPI + NX,
+                       OLU = OLL + NZ, OWPI = OLU + NZ, REC = even_up(OWPI + NX);
+  // OC: per-pass constant of the vector / forward recursion; OACL: closed-loop A + B K (row-major)
+  // ring windows [lo, lo + W): factor [0, OC) (writes back [OK, OC)); vector pass [OPE, OX);
+  // forward sweep [OC, OX); costate [0, OE)
+  static constexpr int W_FAC = OC, LO_VEC = OPE, W_VEC = OX - OPE, LO_FWD = OC, W_FWD = OX - OC, W_COS = even_up(OE);
+  static constexpr int RS = even_up(W_FAC > W_COS ? W_FAC : W_COS);
+  static_assert(OB % 2 == 0 && OZ % 2 == 0 && OD % 2 == 0 && OK % 2 == 0 && OPE % 2 == 0 && OC % 2 == 0 &&
+                    OACL % 2 == 0 && OX % 2 == 0,
+                "16-byte aligned field ranges");
+  static_assert(RS <= 256 && W_VEC <= RS && W_FWD <= RS, "ring window: two 16-B chunks per lane");
+  // LDS (doubles): ring, then the fixed region
+  static constexpr int RING = 0, F0 = RING + 3 * RS, LR0 = F0 + NX * M0, MM0 = LR0 + M0 * M0, Y0 = MM0 + M0 * NQ,
+                       PE0 = Y0 + M0 * NQ, P = PE0 + NX, PA = P + NX * NX, PB = PA + NX * NX, APA = PB + NX * NU,
+                       RU = APA + NX * NX, S = RU + NU * NU, PI = S + NU * NX, PV = PI + NX * NQ, DXV = PV + 2 * NX,
+                       SC = DXV + 2 * NX, LINE = SC + NQ * NQ, ZERO = LINE + NQ, TRASH = ZERO + 16, PAR = TRASH + 64,
+                       XS = even_up(PAR + Par<NQ>::COUNT);
+  // XS: per-stage staging rows [nmax + 1][NX] (v of the vector pass, dx of the forward sweep, the
+  // costate) so that the recursions issue no global stores
   static_assert(M0 * NX <= NX * NX, "stage-0 B'P reuses the PA scratch");
-  static constexpr size_t lds_bytes(int nmax) { return ((size_t)REC * (nmax + 1) + FIXN) * sizeof(double); }
+  static constexpr size_t lds_bytes(int nmax) { return ((size_t)XS + (size_t)(nmax + 1) * NX) * sizeof(double); }
+  static constexpr size_t region_doubles(int nmax) { return (size_t)REC * (nmax + 1); }
 };
 
 // one output of a recursion step:  out = s[ini] + sg * sum_q s[x1+q*sx1] s[y1+q*sy1]
 //                                               +      sum_q s[x2+q*sx2] s[y2+q*sy2];  s[d1] = s[d2] = out
-// `rel` marks operands inside the current stage record (offset by k * REC at run time).
+// `rel` marks operands inside the current stage window (offset by the ring slot base at run time).
 struct Dsc {
   int x1, sx1, y1, sy1, x2, sx2, y2, sy2, ini, d1, d2;
   unsigned rel;
@@ -69,6 +91,18 @@ __device__ __forceinline__ double wmind(double v) {
   UNR for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off));
   return uni(v);
 }
+
+// Ordering point inside a recursion.  A k_wave workgroup is ONE wave and the LDS executes a wave's DS
+// instructions in issue order, so lanes exchanging values through LDS only need the compiler not to
+// move memory operations across this point.  Unlike __syncthreads() (a workgroup-scope fence, i.e.
+// s_waitcnt vmcnt(0) lgkmcnt(0)) it leaves the ring prefetch loads and the per-stage global stores in
+// flight.  Passes that exchange data through GLOBAL memory end with __syncthreads().
+__device__ __forceinline__ void lsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Cholesky for the recursion's critical path: pivots from rsq + two Newton steps give both
 // d = sqrt(s) and 1/d without a division; solves multiply by the inverse diagonal.  Same
 // factorisation and failure test (s > 0) as chol<n> (model.h), rounding-level different.
@@ -116,38 +150,71 @@ __device__ __forceinline__ void tri(int u, int& i, int& j) {
   j = u - i * (i + 1) / 2;
 }
 
+// Optional phase accounting (build with -DVBOC_COOP_PROF): shader-clock cycles per phase, summed over
+// all jobs into g_wave_prof[0..9] ([9] = SQP iterations, [10] = IPM iterations), read with
+// vboc_debug_counters().  Scalar counters (no arrays, no printf) keep the instrumented build's
+// register allocation and schedule close to the product build.
+__device__ unsigned long long g_wave_prof[16];
 #ifdef VBOC_COOP_PROF
-#define CPROF_DECL unsigned long long cp_[12] = {0}; unsigned long long cp_t = clock64();
-#define CPROF(i) { __syncthreads(); const unsigned long long n_ = clock64(); cp_[i] += n_ - cp_t; cp_t = n_; }
+#define CPROF_DECL unsigned long long cp0 = 0, cp1 = 0, cp2 = 0, cp3 = 0, cp4 = 0, cp5 = 0, cp6 = 0, cp7 = 0, cp8 = 0; \
+  unsigned long long cp_t = __builtin_amdgcn_s_memtime();
+#define CPROF(i) { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); cp##i += n_ - cp_t; cp_t = n_; }
+#define CPROF_FLUSH(sq, ip) if (t == 0) { atomicAdd(&g_wave_prof[0], cp0); atomicAdd(&g_wave_prof[1], cp1); \
+  atomicAdd(&g_wave_prof[2], cp2); atomicAdd(&g_wave_prof[3], cp3); atomicAdd(&g_wave_prof[4], cp4); \
+  atomicAdd(&g_wave_prof[5], cp5); atomicAdd(&g_wave_prof[6], cp6); atomicAdd(&g_wave_prof[7], cp7); \
+  atomicAdd(&g_wave_prof[8], cp8); atomicAdd(&g_wave_prof[9], (unsigned long long)(sq)); \
+  atomicAdd(&g_wave_prof[10], (unsigned long long)(ip)); }
 #else
 #define CPROF_DECL
 #define CPROF(i)
+#define CPROF_FLUSH(sq, ip)
 #endif
 
 template <int NQ>
 struct Coop {
-  using CL = CoopLayout<NQ>;
+  using L = WaveLayout<NQ>;
   using PF = Par<NQ>;
-  static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1, REC = CL::REC;
-  static constexpr int OA = CL::OA, OB = CL::OB, OZ = CL::OZ, ODZ = CL::ODZ, OQL = CL::OQL, OQU = CL::OQU,
-                       OE = CL::OE, OK = CL::OK, OKF = CL::OKF, OLR = CL::OLR, OM = CL::OM, OY = CL::OY,
-                       OPE = CL::OPE, OD = CL::OD, ODA = CL::ODA, OV = CL::OV;
+  static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1, REC = L::REC, RS = L::RS;
+  static constexpr int OA = L::OA, OB = L::OB, OZ = L::OZ, ODZ = L::ODZ, OQL = L::OQL, OQU = L::OQU,
+                       OE = L::OE, OK = L::OK, OKF = L::OKF, OLR = L::OLR, OM = L::OM, OY = L::OY,
+                       OPE = L::OPE, OD = L::OD, ODA = L::ODA, OC = L::OC, OACL = L::OACL, OX = L::OX, OU = L::OU,
+                       OPI = L::OPI,
+                       OLL = L::OLL, OLU = L::OLU, OWPI = L::OWPI;
 
-  double* s;      // LDS
-  const int fx;   // fixed-region base
+  double* s;        // LDS (ring + fixed region)
+  gdouble* g;       // this workgroup's stage records in HBM
   const Work& w;
   const Opts& o;
-  Lane<NQ> G;     // this problem's slot in the tiled global arrays (X, U, PI, LL, LU, WPI, PAR)
-  const int t;    // lane
+  const int t;      // lane
   int N;
   double rs, rd0, e00, mu, nbox;   // interior-point scalars (wave-uniform)
 
-  __device__ Coop(double* s_, int fx_, const Work& w_, const Opts& o_, unsigned slot, int t_)
-      : s(s_), fx(fx_), w(w_), o(o_), G(w_, o_, slot), t(t_), N(0) {}
+  __device__ Coop(double* s_, gdouble* g_, const Work& w_, const Opts& o_, int t_)
+      : s(s_), g(g_), w(w_), o(o_), t(t_), N(0) {}
 
-  __device__ __forceinline__ double& st(int k, int off) const { return s[k * REC + off]; }
-  __device__ __forceinline__ double& fv(int off) const { return s[fx + off]; }
-  __device__ __forceinline__ double& par(int f) const { return s[fx + CL::PAR + f]; }
+  __device__ __forceinline__ gdouble& st(int k, int off) const { return g[(long long)k * REC + off]; }
+  __device__ __forceinline__ double& par(int f) const { return s[L::PAR + f]; }
+  __device__ __forceinline__ static constexpr int slot_base(int slot) { return L::RING + slot * RS; }
+
+  // ---- ring of stage windows: lane t moves 16-B chunks t and t + 64 ---------------------------------
+  __device__ __forceinline__ void ring_issue(int k, int lo, int W, dbl2 (&b)[2]) const {
+    // unconditional (clamped) loads: no exec-masked blocks around VMEM, so the waitcnt pass can keep
+    // the prefetch in flight across iterations
+    const gdbl2* src = (const gdbl2*)(g + (long long)k * REC + lo);
+    const int nc = W / 2;
+    b[0] = src[t < nc ? t : nc - 1];
+    b[1] = src[t + 64 < nc ? t + 64 : nc - 1];
+  }
+  __device__ __forceinline__ void ring_put(int slot, int W, const dbl2 (&b)[2]) const {
+    dbl2* dst = (dbl2*)(s + slot_base(slot));
+    if (2 * t < W) dst[t] = b[0];
+    if (2 * (t + 64) < W) dst[t + 64] = b[1];
+  }
+  __device__ __forceinline__ void ring_wb(int slot, int k, int lo, int hi) const {
+    const dbl2* src = (const dbl2*)(s + slot_base(slot));
+    gdbl2* dst = (gdbl2*)(g + (long long)k * REC);
+    for (int c = lo / 2 + t; c < hi / 2; c += 64) dst[c] = src[c];
+  }
 
   // box of component i of stage k (the Lane::stage_box pattern)
   __device__ __forceinline__ bool box(int k, int i, double& lb, double& ub) const {
@@ -166,12 +233,39 @@ struct Coop {
     return true;
   }
   __device__ __forceinline__ double dz_init(double lb, double ub, double z) const {
-    const double L = lb - z, U = ub - z, del = o.push * (U - L);
-    return fmin(fmax(0.0, L + del), U - del);
+    const double Lo = lb - z, U = ub - z, del = o.push * (U - Lo);
+    return fmin(fmax(0.0, Lo + del), U - del);
   }
   __device__ __forceinline__ double cgrad(int k, int i) const { return (k == 0 && i == 0) ? par(PF::CS) : 0.0; }
 
+  // contiguous field range [LO, LO + 2*C) of stage k into registers (16-B loads, all issued at once)
+  template <int LO, int C>
+  __device__ __forceinline__ void ldr(int k, double (&d)[2 * C]) const {
+    static_assert(LO % 2 == 0, "16-byte aligned range");
+    const gdbl2* src = (const gdbl2*)(g + (long long)k * REC + LO);
+    UNR for (int c = 0; c < C; ++c) {
+      const dbl2 v = src[c];
+      d[2 * c] = v.x;
+      d[2 * c + 1] = v.y;
+    }
+  }
+  // z, dz, lambda_l, lambda_u of a stage: the contiguous range [OZ, OE)
+  static constexpr int NIP = (4 * NZ + 1) / 2;
+  struct IP { double v[2 * NIP]; };
+  __device__ __forceinline__ void ld_ip(int k, IP& r) const { ldr<OZ, NIP>(k, r.v); }
+
   struct CS { double tl, tu, itl, itu, ql, qu, dz; bool bx; };
+  __device__ __forceinline__ CS comp_r(const IP& r, int k, int i) const {
+    CS c;
+    double lb, ub;
+    c.bx = box(k, i, lb, ub);
+    const double z = r.v[i];
+    c.dz = r.v[NZ + i]; c.ql = r.v[2 * NZ + i]; c.qu = r.v[3 * NZ + i];
+    c.tl = c.dz - (lb - z); c.tu = (ub - z) - c.dz;
+    c.itl = c.bx ? 1.0 / c.tl : 0.0;
+    c.itu = c.bx ? 1.0 / c.tu : 0.0;
+    return c;
+  }
   __device__ __forceinline__ CS comp(int k, int i) const {
     CS c;
     double lb, ub;
@@ -190,12 +284,12 @@ struct Coop {
   }
 
   // ---------------------------------------------------------------------------------------------
-  // recursion-step machinery
+  // recursion-step machinery (all operands in LDS)
   // ---------------------------------------------------------------------------------------------
   __device__ __forceinline__ void dnull(Dsc& d) const {
-    d.x1 = d.y1 = d.x2 = d.y2 = d.ini = fx + CL::ZERO;
+    d.x1 = d.y1 = d.x2 = d.y2 = d.ini = L::ZERO;
     d.sx1 = d.sy1 = d.sx2 = d.sy2 = 0;
-    d.d1 = d.d2 = fx + CL::TRASH + t;
+    d.d1 = d.d2 = L::TRASH + t;
     d.rel = 0;
     d.sg = 1.0;
   }
@@ -213,32 +307,32 @@ struct Coop {
     UNR for (int q = 0; q < L1; ++q) s1 += a1[q] * b1[q];
     UNR for (int q = 0; q < L2; ++q) s2 += a2[q] * b2[q];
     const double r = r0 + d.sg * s1 + s2;
-    __syncthreads();
+    lsync();
     s[ad(d.d1, RD1)] = r;
     s[ad(d.d2, RD2)] = r;
-    __syncthreads();
+    lsync();
   }
   // all lanes: L = chol(s[ru..]); lane-specific column solve rhs -> sgn * Ru^-1 rhs; lane 0 stores L
   template <int n>
   __device__ __forceinline__ bool sstep(int ru, int ldst, int rb, int rstr, int db, int dstr, double sgn) const {
-    double L[n * n], id[n], b[n];
+    double Lm[n * n], id[n], b[n];
     UNR for (int a = 0; a < n; ++a) b[a] = s[rb + a * rstr];
-    UNR for (int e = 0; e < n * n; ++e) L[e] = s[ru + e];
-    const bool ok = chol_inv<n>(L, id);
-    solve_inv<n>(L, id, b);
-    __syncthreads();
+    UNR for (int e = 0; e < n * n; ++e) Lm[e] = s[ru + e];
+    const bool ok = chol_inv<n>(Lm, id);
+    solve_inv<n>(Lm, id, b);
+    lsync();
     UNR for (int a = 0; a < n; ++a) s[db + a * dstr] = sgn * b[a];
     if (t == 0) {
-      UNR for (int e = 0; e < n * n; ++e) s[ldst + e] = L[e];
+      UNR for (int e = 0; e < n * n; ++e) s[ldst + e] = Lm[e];
     }
-    __syncthreads();
+    lsync();
     return ok;
   }
 
   // descriptors of the middle-stage factorisation steps (rs enters through sg)
   __device__ void desc_mid(Dsc& d1, Dsc& d2, Dsc& d4) const {
-    const int P = fx + CL::P, PA = fx + CL::PA, PB = fx + CL::PB, APA = fx + CL::APA, RU = fx + CL::RU,
-              S = fx + CL::S, PI = fx + CL::PI, SC = fx + CL::SC, LINE = fx + CL::LINE;
+    constexpr int P = L::P, PA = L::PA, PB = L::PB, APA = L::APA, RU = L::RU, S = L::S, PI = L::PI, SC = L::SC,
+                  LINE = L::LINE;
     constexpr int TX = NX * (NX + 1) / 2, TU = NU * (NU + 1) / 2;
     dnull(d1); dnull(d2); dnull(d4);
     // step 1: PA = P A, PB = P B, P e (-> stage PE), lin_e += Pi' e
@@ -294,10 +388,10 @@ struct Coop {
       d4.ini = d4.d1 = d4.d2 = SC + u;
     }
   }
-  // stage 0 (controls s, u_0; F0 = [A0 g, B0]); the stage-0 record starts at 0, so all absolute
+  // stage 0 (controls s, u_0; F0 = [A0 g, B0]): e and H of stage 0 come from its ring slot
   __device__ void desc_s0(Dsc& z1, Dsc& z2, Dsc& z4) const {
-    const int P = fx + CL::P, BP = fx + CL::PA, PI = fx + CL::PI, F0 = fx + CL::F0, Y0 = fx + CL::Y0,
-              PE0 = fx + CL::PE0, LINE = fx + CL::LINE, LR0 = fx + CL::LR0, MM0 = fx + CL::MM0, SC = fx + CL::SC;
+    constexpr int P = L::P, BP = L::PA, PI = L::PI, F0 = L::F0, Y0 = L::Y0, PE0 = L::PE0, LINE = L::LINE,
+                  LR0 = L::LR0, MM0 = L::MM0, SC = L::SC;
     constexpr int TM = M0 * (M0 + 1) / 2;
     dnull(z1); dnull(z2); dnull(z4);
     int u = t;
@@ -308,16 +402,16 @@ struct Coop {
       const int a = u / NQ, j = u % NQ;
       z1.x1 = F0 + a; z1.sx1 = M0; z1.y1 = PI + j; z1.sy1 = NQ; z1.d1 = z1.d2 = Y0 + u;
     } else if ((u -= M0 * NQ) < NX) {
-      z1.x1 = P + u * NX; z1.sx1 = 1; z1.y1 = OE; z1.sy1 = 1; z1.sg = rs; z1.d1 = z1.d2 = PE0 + u;
+      z1.x1 = P + u * NX; z1.sx1 = 1; z1.y1 = OE; z1.sy1 = 1; z1.sg = rs; z1.d1 = z1.d2 = PE0 + u; z1.rel = RY1;
     } else if ((u -= NX) < NQ) {
-      z1.x1 = PI + u; z1.sx1 = NQ; z1.y1 = OE; z1.sy1 = 1; z1.sg = rs; z1.ini = z1.d1 = z1.d2 = LINE + u;
+      z1.x1 = PI + u; z1.sx1 = NQ; z1.y1 = OE; z1.sy1 = 1; z1.sg = rs; z1.ini = z1.d1 = z1.d2 = LINE + u; z1.rel = RY1;
     }
     u = t;
     if (u < TM) {
       int a, c;
       tri(u, a, c);
       z2.x1 = BP + a * NX; z2.sx1 = 1; z2.y1 = F0 + c; z2.sy1 = M0;
-      if (a == c) z2.ini = OD + a;
+      if (a == c) { z2.ini = OD + a; z2.rel = RINI; }
       z2.d1 = LR0 + a * M0 + c; z2.d2 = LR0 + c * M0 + a;
     }
     u = t;
@@ -328,27 +422,98 @@ struct Coop {
   }
 
   // ---------------------------------------------------------------------------------------------
+  // problem set-up: from the inputs (wave mode) or from a lane-mode slot (hand-off)
+  // ---------------------------------------------------------------------------------------------
+  __device__ void from_inputs(const Inputs& in, int pid) {
+    constexpr int NXR = NX + 1, NP = NQ + 1;
+    N = in.N[pid];
+    const double* p = in.p + (long long)pid * NP;
+    const double* lbx = in.lbx + (long long)pid * NXR;
+    const double* ubx = in.ubx + (long long)pid * NXR;
+    const double* lbx0 = in.lbx0 + (long long)pid * NXR;
+    const double* ubx0 = in.ubx0 + (long long)pid * NXR;
+    const double* lbxe = in.lbxe + (long long)pid * NXR;
+    const double* ubxe = in.ubxe + (long long)pid * NXR;
+    const double* xg = in.xg + (long long)pid * (in.nmax + 1) * NXR;
+    const double* ug = in.ug + (long long)pid * in.nmax * NU;
+    if (t == 0) {   // parameters: the Lane::load formulas
+      const double h = lbx[NX];
+      par(PF::H) = h;
+      double nrm = 0.0;
+      UNR for (int j = 0; j < NQ; ++j) nrm += p[j] * p[j];
+      nrm = sqrt(nrm);
+      double slb = -INFINITY, sub = INFINITY, cs = 0.0, sv = 0.0;
+      UNR for (int j = 0; j < NQ; ++j) {
+        const double dj = (NQ == 1) ? 1.0 : p[j] / nrm;
+        par(PF::DIR + j) = dj;
+        par(PF::Q0 + j) = lbx0[j];
+        cs += p[j] * dj;
+        const double lo = lbx0[NQ + j], hi = ubx0[NQ + j];
+        if (dj > 0) { slb = fmax(slb, lo / dj); sub = fmin(sub, hi / dj); }
+        else if (dj < 0) { slb = fmax(slb, hi / dj); sub = fmin(sub, lo / dj); }
+        sv += dj * xg[NQ + j];
+      }
+      par(PF::SLB) = slb; par(PF::SUB) = sub; par(PF::CS) = cs;
+      par(PF::CCONST) = p[NQ] * h * (double)N;
+      UNR for (int i = 0; i < NX; ++i) { par(PF::XLB + i) = lbx[i]; par(PF::XUB + i) = ubx[i]; }
+      UNR for (int a = 0; a < NU; ++a) {
+        par(PF::ULB + a) = in.lbu[(long long)pid * NU + a];
+        par(PF::UUB + a) = in.ubu[(long long)pid * NU + a];
+      }
+      UNR for (int j = 0; j < NQ; ++j) {
+        par(PF::QNLB + j) = lbxe[j]; par(PF::QNUB + j) = ubxe[j]; par(PF::VFIN + j) = lbxe[NQ + j];
+        par(PF::NU_ + j) = 0.0; par(PF::WNU + j) = 0.0;
+      }
+      par(PF::WBND) = 0.0;
+      par(PF::S) = sv;
+    }
+    for (int k = t; k <= N; k += 64) {
+      UNR for (int i = 0; i < NX; ++i) st(k, OX + i) = xg[(long long)k * NXR + i];
+      UNR for (int i = 0; i < NZ; ++i) { st(k, OLL + i) = 0.0; st(k, OLU + i) = 0.0; }
+      if (k < N) {
+        UNR for (int a = 0; a < NU; ++a) st(k, OU + a) = ug[(long long)k * NU + a];
+        UNR for (int i = 0; i < NX; ++i) { st(k, OPI + i) = 0.0; st(k, OWPI + i) = 0.0; }
+      }
+    }
+    __syncthreads();
+  }
+  __device__ void from_slot(const SlotState& ss, unsigned slot) {
+    Lane<NQ> G(w, o, slot);
+    N = ss(IS_N, slot);
+    for (int f = t; f < PF::COUNT; f += 64) par(f) = G.par(f);
+    for (int k = t; k <= N; k += 64) {
+      UNR for (int i = 0; i < NX; ++i) st(k, OX + i) = G.atv(w.X, NX, k, i);
+      UNR for (int i = 0; i < NZ; ++i) { st(k, OLL + i) = G.atv(w.LL, NZ, k, i); st(k, OLU + i) = G.atv(w.LU, NZ, k, i); }
+      if (k < N) {
+        UNR for (int a = 0; a < NU; ++a) st(k, OU + a) = G.atv(w.U, NU, k, a);
+        UNR for (int i = 0; i < NX; ++i) { st(k, OPI + i) = G.atv(w.PI, NX, k, i); st(k, OWPI + i) = G.atv(w.WPI, NX, k, i); }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------------------------------------
   // linearisation (stage-parallel): ERK4 + sensitivities, defects, current z, NLP residuals
   // ---------------------------------------------------------------------------------------------
   __device__ void linearize(double& rstat, double& req, double& rineq, double& rcomp) {
     const double h = par(PF::H), sv = par(PF::S);
     double stt = 0.0, eq = 0.0, inq = 0.0, cp = 0.0;
     for (int k = t; k <= N; k += 64) {
-      double* rec = &s[k * REC];
+      gdouble* rec = &g[(long long)k * REC];
       if (k < N) {
         double xk[NX], uk[NU], x1[NX];
         if (k == 0) {
           UNR for (int j = 0; j < NQ; ++j) { xk[j] = par(PF::Q0 + j); xk[NQ + j] = sv * par(PF::DIR + j); }
         } else {
-          UNR for (int i = 0; i < NX; ++i) xk[i] = G.atv(w.X, NX, k, i);
+          UNR for (int i = 0; i < NX; ++i) xk[i] = rec[OX + i];
         }
-        UNR for (int a = 0; a < NU; ++a) uk[a] = G.atv(w.U, NU, k, a);
+        UNR for (int a = 0; a < NU; ++a) uk[a] = rec[OU + a];
         rk4_sens<NQ>(h, xk, uk, x1, [&](int i, int c, double v) {
           if (c < NX) rec[OA + i * NX + c] = v;
           else rec[OB + i * NU + (c - NX)] = v;
         });
         UNR for (int i = 0; i < NX; ++i) {
-          const double b = x1[i] - G.atv(w.X, NX, k + 1, i);
+          const double b = x1[i] - st(k + 1, OX + i);
           rec[OE + i] = b;
           eq = fmax(eq, fabs(b));
         }
@@ -361,7 +526,7 @@ struct Coop {
           UNR for (int a = 0; a < NU; ++a) rec[OZ + NX + a] = uk[a];
         }
         double pik[NX];
-        UNR for (int i = 0; i < NX; ++i) pik[i] = G.atv(w.PI, NX, k, i);
+        UNR for (int i = 0; i < NX; ++i) pik[i] = rec[OPI + i];
         if (k == 0) {
           double F[NX * M0];
           UNR for (int i = 0; i < NX; ++i) {
@@ -370,17 +535,17 @@ struct Coop {
             F[i * M0] = tt;
             UNR for (int a = 0; a < NU; ++a) F[i * M0 + 1 + a] = rec[OB + i * NU + a];
           }
-          UNR for (int e = 0; e < NX * M0; ++e) fv(CL::F0 + e) = F[e];
+          UNR for (int e = 0; e < NX * M0; ++e) s[L::F0 + e] = F[e];
           UNR for (int c = 0; c < M0; ++c) {
-            double gr = (c == 0 ? par(PF::CS) : 0.0) - G.atv(w.LL, NZ, 0, c) + G.atv(w.LU, NZ, 0, c);
+            double gr = (c == 0 ? par(PF::CS) : 0.0) - rec[OLL + c] + rec[OLU + c];
             UNR for (int r = 0; r < NX; ++r) gr += F[r * M0 + c] * pik[r];
             stt = fmax(stt, fabs(gr));
           }
         } else {
           double pprev[NX];
-          UNR for (int i = 0; i < NX; ++i) pprev[i] = G.atv(w.PI, NX, k - 1, i);
+          UNR for (int i = 0; i < NX; ++i) pprev[i] = st(k - 1, OPI + i);
           UNR for (int c = 0; c < NZ; ++c) {
-            double gr = -G.atv(w.LL, NZ, k, c) + G.atv(w.LU, NZ, k, c);
+            double gr = -rec[OLL + c] + rec[OLU + c];
             if (c < NX) {
               UNR for (int r = 0; r < NX; ++r) gr += rec[OA + r * NX + c] * pik[r];
               gr -= pprev[c];
@@ -393,16 +558,16 @@ struct Coop {
         UNR for (int c = 0; c < NZ; ++c) {
           double lb, ub;
           if (!box(k, c, lb, ub)) continue;
-          const double z = rec[OZ + c], ll = G.atv(w.LL, NZ, k, c), lu = G.atv(w.LU, NZ, k, c);
+          const double z = rec[OZ + c], ll = rec[OLL + c], lu = rec[OLU + c];
           inq = fmax(inq, fmax(lb - z, z - ub));
           cp = fmax(cp, fmax(fabs(ll * (z - lb)), fabs(lu * (ub - z))));
         }
       } else {
-        UNR for (int i = 0; i < NX; ++i) rec[OZ + i] = G.atv(w.X, NX, N, i);
+        UNR for (int i = 0; i < NX; ++i) rec[OZ + i] = rec[OX + i];
         UNR for (int i = NX; i < NZ; ++i) rec[OZ + i] = 0.0;
         UNR for (int c = 0; c < NX; ++c) {
-          const double z = rec[OZ + c];
-          double gr = -G.atv(w.LL, NZ, N, c) + G.atv(w.LU, NZ, N, c) - G.atv(w.PI, NX, N - 1, c);
+          const double z = rec[OX + c];
+          double gr = -rec[OLL + c] + rec[OLU + c] - st(N - 1, OPI + c);
           if (c >= NQ) {
             gr += par(PF::NU_ + c - NQ);
             eq = fmax(eq, fabs(z - par(PF::VFIN + c - NQ)));
@@ -410,7 +575,7 @@ struct Coop {
           stt = fmax(stt, fabs(gr));
           if (c < NQ) {
             const double lb = par(PF::QNLB + c), ub = par(PF::QNUB + c);
-            const double ll = G.atv(w.LL, NZ, N, c), lu = G.atv(w.LU, NZ, N, c);
+            const double ll = rec[OLL + c], lu = rec[OLU + c];
             inq = fmax(inq, fmax(lb - z, z - ub));
             cp = fmax(cp, fmax(fabs(ll * (z - lb)), fabs(lu * (ub - z))));
           }
@@ -427,14 +592,14 @@ struct Coop {
   __device__ void qp_init() {
     double musum = 0.0, nb = 0.0, rd = 0.0, e0 = 0.0;
     for (int k = t; k <= N; k += 64) {
-      double* rec = &s[k * REC];
+      gdouble* rec = &g[(long long)k * REC];
       double dz[NZ];
       UNR for (int i = 0; i < NZ; ++i) {
         double lb, ub, ql = 0.0, qu = 0.0, d0 = 0.0;
         if (box(k, i, lb, ub)) {
-          const double z = rec[OZ + i], L = lb - z, U = ub - z;
+          const double z = rec[OZ + i], Lo = lb - z, U = ub - z;
           d0 = dz_init(lb, ub, z);
-          ql = o.mu0 / (d0 - L);
+          ql = o.mu0 / (d0 - Lo);
           qu = o.mu0 / (U - d0);
           musum += o.mu0 + o.mu0;
           nb += 2.0;
@@ -444,13 +609,13 @@ struct Coop {
         rd = fmax(rd, fabs(o.lm * d0 + cgrad(k, i) - ql + qu));
       }
       if (k < N) {
-        const double* rn = &s[(k + 1) * REC];
+        const gdouble* rn = &g[(long long)(k + 1) * REC];
         UNR for (int i = 0; i < NX; ++i) {
           double lb, ub, dn = 0.0;
           if (box(k + 1, i, lb, ub)) dn = dz_init(lb, ub, rn[OZ + i]);
           double tt = rec[OE + i] - dn;
           if (k == 0) {
-            UNR for (int a = 0; a < M0; ++a) tt += fv(CL::F0 + i * M0 + a) * dz[a];
+            UNR for (int a = 0; a < M0; ++a) tt += s[L::F0 + i * M0 + a] * dz[a];
           } else {
             UNR for (int q = 0; q < NX; ++q) tt += rec[OA + i * NX + q] * dz[q];
             UNR for (int a = 0; a < NU; ++a) tt += rec[OB + i * NU + a] * dz[NX + a];
@@ -484,10 +649,14 @@ struct Coop {
   // H -> D slot, predictor gradient -> DA slot
   __device__ void prep_pred() {
     for (int k = t; k <= N; k += 64) {
+      IP r;
+      ld_ip(k, r);
+      __builtin_amdgcn_sched_barrier(0);
+      gdouble* rec = &g[(long long)k * REC];
       UNR for (int i = 0; i < NZ; ++i) {
-        const CS c = comp(k, i);
-        st(k, OD + i) = o.lm + (c.bx ? c.ql * c.itl + c.qu * c.itu : 0.0);
-        st(k, ODA + i) = o.lm * c.dz + cgrad(k, i);
+        const CS c = comp_r(r, k, i);
+        rec[OD + i] = o.lm + (c.bx ? c.ql * c.itl + c.qu * c.itu : 0.0);
+        rec[ODA + i] = o.lm * c.dz + cgrad(k, i);
       }
     }
     __syncthreads();
@@ -495,165 +664,237 @@ struct Coop {
   // corrector gradient (uses the affine direction in DA) -> D slot
   __device__ void prep_corr(double smu) {
     for (int k = t; k <= N; k += 64) {
+      IP r;
+      double da[2 * ((2 * NZ + 1) / 2)];
+      ld_ip(k, r);
+      ldr<OD, (2 * NZ + 1) / 2>(k, da);
+      __builtin_amdgcn_sched_barrier(0);
+      gdouble* rec = &g[(long long)k * REC];
       UNR for (int i = 0; i < NZ; ++i) {
-        const CS c = comp(k, i);
-        double g = o.lm * c.dz + cgrad(k, i);
+        const CS c = comp_r(r, k, i);
+        double gg = o.lm * c.dz + cgrad(k, i);
         if (c.bx) {
           double rl, ru;
-          corr_rhs(c, st(k, ODA + i), smu, rl, ru);
-          g += -c.ql - rl * c.itl + c.qu + ru * c.itu;
+          corr_rhs(c, da[NZ + i], smu, rl, ru);
+          gg += -c.ql - rl * c.itl + c.qu + ru * c.itu;
         }
-        st(k, OD + i) = g;
+        rec[OD + i] = gg;
       }
     }
     __syncthreads();
   }
 
-  // Riccati factorisation (matrix part) of stages N-1..0; the vector part is vec()
+  // Riccati factorisation (matrix part) of stages N-1..0 through the LDS ring; the vector part is vec()
   __device__ bool factor() {
     for (int e = t; e < NX * NX; e += 64) {
       const int i = e / NX, j = e % NX;
-      fv(CL::P + e) = (i == j) ? st(N, OD + i) : 0.0;
+      s[L::P + e] = (i == j) ? (double)st(N, OD + i) : 0.0;
     }
     for (int e = t; e < NX * NQ; e += 64) {
       const int i = e / NQ, j = e % NQ;
-      fv(CL::PI + e) = (i == NQ + j) ? 1.0 : 0.0;
+      s[L::PI + e] = (i == NQ + j) ? 1.0 : 0.0;
     }
-    for (int e = t; e < NQ * NQ; e += 64) fv(CL::SC + e) = 0.0;
-    if (t < NQ) fv(CL::LINE + t) = 0.0;
+    for (int e = t; e < NQ * NQ; e += 64) s[L::SC + e] = 0.0;
+    if (t < NQ) s[L::LINE + t] = 0.0;
+    dbl2 b[2];
+    ring_issue(N - 1, 0, L::W_FAC, b);
+    ring_put(0, L::W_FAC, b);
+    if (N >= 2) {
+      ring_issue(N - 2, 0, L::W_FAC, b);
+      ring_put(1, L::W_FAC, b);
+    }
     __syncthreads();
     bool ok = true;
-    {
-      Dsc d1, d2, d4;
-      desc_mid(d1, d2, d4);
-      const int Z = fx + CL::ZERO, TR = fx + CL::TRASH + t;
-      for (int k = N - 1; k >= 1; --k) {
-        const int kb = k * REC;
+    Dsc d1, d2, d4;
+    desc_mid(d1, d2, d4);
+    for (int j = 0; j < N; ++j) {
+      const int k = N - 1 - j, slot = j % 3, kb = slot_base(slot);
+      const bool pf = k >= 2;
+      // outputs of the previous stage (k + 1) go out first, so their stores complete under this
+      // stage's arithmetic instead of stalling the ring put at its end
+      if (j >= 1) ring_wb((j - 1) % 3, k + 1, OK, OC);
+      if (pf) ring_issue(k - 2, 0, L::W_FAC, b);
+      if (k >= 1) {
         dstep<NX, 0>(d1, kb);
         dstep<NX, 0>(d2, kb);
-        int rb = Z, rstr = 0, db = TR, dstr = 0;
+        int rb = L::ZERO, rstr = 0, db = L::TRASH + t, dstr = 0;
         double sgn = 1.0;
-        if (t < NX) { rb = fx + CL::S + t; rstr = NX; db = kb + OK + t; dstr = NX; sgn = -1.0; }
+        if (t < NX) { rb = L::S + t; rstr = NX; db = kb + OK + t; dstr = NX; sgn = -1.0; }
         else if (t < NX + NQ) { rb = kb + OY + (t - NX); rstr = NQ; db = kb + OM + (t - NX); dstr = NQ; }
-        const bool okk = sstep<NU>(fx + CL::RU, kb + OLR, rb, rstr, db, dstr, sgn);
+        const bool okk = sstep<NU>(L::RU, kb + OLR, rb, rstr, db, dstr, sgn);
         ok = ok && okk;
         dstep<NX, NU>(d4, kb);
+      } else {
+        Dsc z1, z2, z4;
+        desc_s0(z1, z2, z4);
+        dstep<NX, 0>(z1, kb);
+        dstep<NX, 0>(z2, kb);
+        int rb = L::ZERO, rstr = 0, db = L::TRASH + t, dstr = 0;
+        if (t < NQ) { rb = L::Y0 + t; rstr = NQ; db = L::MM0 + t; dstr = NQ; }
+        const bool ok0 = sstep<M0>(L::LR0, L::LR0, rb, rstr, db, dstr, 1.0);
+        ok = ok && ok0;
+        dstep<0, M0>(z4, kb);
+      }
+      if (pf) ring_put((j + 2) % 3, L::W_FAC, b);
+      lsync();
+    }
+    __syncthreads();   // write-back visible to the next sweep's ring loads
+    return ok;
+  }
+
+  // closed-loop matrices A_cl = A + B K of stages 1..N-1 (row-major, OACL): formed once per
+  // factorisation, stage-parallel, and shared by both vector passes (columns) and both forward
+  // sweeps (rows) of the interior-point iteration
+  __device__ void acl_pass() {
+    constexpr int NAB = (NX * NX + NX * NU) / 2, NKK = (NU * NX) / 2;
+    for (int k = 1 + t; k < N; k += 64) {
+      double ab[2 * NAB], kk[2 * NKK];
+      ldr<OA, NAB>(k, ab);
+      ldr<OK, NKK>(k, kk);
+      __builtin_amdgcn_sched_barrier(0);
+      gdbl2* dst = (gdbl2*)(g + (long long)k * REC + OACL);
+      UNR for (int e = 0; e < NX * NX; e += 2) {
+        double v[2];
+        UNR for (int h2 = 0; h2 < 2; ++h2) {
+          const int q = (e + h2) / NX, i = (e + h2) % NX;
+          double a = ab[q * NX + i];
+          UNR for (int c = 0; c < NU; ++c) a += ab[NX * NX + q * NU + c] * kk[c * NX + i];
+          v[h2] = a;
+        }
+        dbl2 vv;
+        vv.x = v[0];
+        vv.y = v[1];
+        dst[e / 2] = vv;
       }
     }
-    {
-      Dsc z1, z2, z4;
-      desc_s0(z1, z2, z4);
-      dstep<NX, 0>(z1, 0);
-      dstep<NX, 0>(z2, 0);
-      int rb = fx + CL::ZERO, rstr = 0, db = fx + CL::TRASH + t, dstr = 0;
-      if (t < NQ) { rb = fx + CL::Y0 + t; rstr = NQ; db = fx + CL::MM0 + t; dstr = NQ; }
-      const bool ok0 = sstep<M0>(fx + CL::LR0, fx + CL::LR0, rb, rstr, db, dstr, 1.0);
-      ok = ok && ok0;
-      dstep<0, M0>(z4, 0);
-    }
-    return ok;
+    __syncthreads();
   }
 
   // vector pass with the gradient in slot OG; leaves the stage-0 open-loop step w0 and the
   // terminal multiplier nu (wave-uniform).  False if S = sum Y'M is not positive definite.
   __device__ bool vec(int OG, double (&w0)[M0], double (&nun)[NQ]) {
-    // p_k = c_k + A_cl,k' (PE_k + p_{k+1}),  c_k = g_x + K'g_u,  A_cl = A + B K  (lane i: row i of p).
-    // Software-pipelined: the stage-only terms of stage k-1 (closed-loop column, c + A_cl' PE) are
-    // loaded and formed while stage k waits on p_{k+1}; PV is double-buffered (one barrier/stage).
-    double pcur = 0.0;
-    if (t < NX) {
-      pcur = st(N, OG + t);
-      fv(CL::PV + t) = pcur;
-    }
-    // raw stage operands of the closed-loop column (loaded as one block), then the arithmetic
-    struct VT { double a[NX], b[NX * NU], k[NU], g, gu[NU], pe[NX], pei; };
-    auto vload = [&](int k, VT& r) {
-      const int i = t;
-      UNR for (int q = 0; q < NX; ++q) r.a[q] = st(k, OA + q * NX + i);
-      UNR for (int e = 0; e < NX * NU; ++e) r.b[e] = st(k, OB + e);
-      UNR for (int b = 0; b < NU; ++b) { r.k[b] = st(k, OK + b * NX + i); r.gu[b] = st(k, OG + NX + b); }
-      r.g = st(k, OG + i);
-      UNR for (int q = 0; q < NX; ++q) r.pe[q] = st(k, OPE + q);
-      r.pei = st(k, OPE + i);
-    };
-    auto vterms = [&](const VT& r, double (&acl)[NX], double& cc, double& pe) {
-      double c = r.g;
-      UNR for (int b = 0; b < NU; ++b) c += r.k[b] * r.gu[b];
-      UNR for (int q = 0; q < NX; ++q) {
-        double a = r.a[q];
-        UNR for (int b = 0; b < NU; ++b) a += r.b[q * NU + b] * r.k[b];
-        acl[q] = a;
-      }
-      UNR for (int q = 0; q < NX; ++q) c += acl[q] * r.pe[q];
-      cc = c;
-      pe = r.pei;
-    };
-    double acl[NX], cc = 0.0, pe = 0.0;
-    if (t < NX) {
-      VT r;
-      vload(N - 1 >= 1 ? N - 1 : 1, r);
-      vterms(r, acl, cc, pe);
-    }
-    __syncthreads();
-    for (int k = N - 1; k >= 1; --k) {
-      const int rb = fx + CL::PV + ((N - 1 - k) & 1) * NX, wb = fx + CL::PV + ((N - k) & 1) * NX;
-      if (t < NX) {
-        double pv[NX];
-        UNR for (int q = 0; q < NX; ++q) pv[q] = s[rb + q];
-        VT r;
-        vload(k - 1 >= 1 ? k - 1 : 1, r);
+    // p_k = c'_k + A_cl,k' p_{k+1},  c'_k = g_x + K'g_u + A_cl' PE_k  (lane i: row i of p);
+    // v_k = PE_k + p_{k+1} is kept for k_f.  c' is formed stage-parallel first (-> OC).
+    {
+      constexpr int NZH = (2 * NZ + 1) / 2, NKK = (NU * NX) / 2;
+      for (int k = 1 + t; k < N; k += 64) {
+        double gg[2 * NZH], kk[2 * NKK], ac[NX * NX], pe[NX];
+        ldr<OD, NZH>(k, gg);
+        ldr<OK, NKK>(k, kk);
+        ldr<OACL, NX * NX / 2>(k, ac);
+        ldr<OPE, NX / 2>(k, pe);
         __builtin_amdgcn_sched_barrier(0);
-        double p0 = cc, p1 = 0.0;
-        UNR for (int q = 0; q < NX; q += 2) p0 += acl[q] * pv[q];
-        UNR for (int q = 1; q < NX; q += 2) p1 += acl[q] * pv[q];
-        st(k, OV + t) = pe + pcur;
-        pcur = p0 + p1;
-        s[wb + t] = pcur;
-        vterms(r, acl, cc, pe);
+        const int go = OG - OD;
+        gdbl2* dst = (gdbl2*)(g + (long long)k * REC + OC);
+        double cv[NX];
+        UNR for (int i = 0; i < NX; ++i) {
+          double c = gg[go + i];
+          UNR for (int q = 0; q < NU; ++q) c += kk[q * NX + i] * gg[go + NX + q];
+          UNR for (int q = 0; q < NX; ++q) c += ac[q * NX + i] * pe[q];
+          cv[i] = c;
+        }
+        UNR for (int i = 0; i < NX; i += 2) {
+          dbl2 vv;
+          vv.x = cv[i];
+          vv.y = cv[i + 1];
+          dst[i / 2] = vv;
+        }
       }
       __syncthreads();
     }
-    if (t < NX) fv(CL::PV + t) = pcur;
+    double pcur = st(N, OG + (t < NX ? t : NX - 1));
+    if (t < NX) s[L::PV + t] = pcur;
+    const int cnt = N - 1;   // stages N-1 .. 1
+    dbl2 b[2];
+    if (cnt >= 1) { ring_issue(N - 1, L::LO_VEC, L::W_VEC, b); ring_put(0, L::W_VEC, b); }
+    if (cnt >= 2) { ring_issue(N - 2, L::LO_VEC, L::W_VEC, b); ring_put(1, L::W_VEC, b); }
     __syncthreads();
-    // k_f = -Ru^-1 (g_u + B'v) per stage, lin = sum Y'k_f
+    // ring slot of the vector pass: [PE | C | ACL]
+    auto vld = [&](int kb, double (&acl)[NX], double& cc, double& pe) {
+      const int i = t < NX ? t : NX - 1;
+      UNR for (int q = 0; q < NX; ++q) acl[q] = s[kb + (OACL - OPE) + q * NX + i];
+      cc = s[kb + (OC - OPE) + i];
+      pe = s[kb + i];
+    };
+    double acl[NX], cc = 0.0, pe = 0.0;
+    if (cnt >= 1) vld(slot_base(0), acl, cc, pe);
+    // prefetch distance 2: stage S[j+3] is loaded into one register buffer while the other (S[j+2],
+    // loaded one iteration earlier) goes to its ring slot; the loop is unrolled x2 to alternate them
+    dbl2 bA[2], bB[2];
+    if (cnt >= 3) ring_issue(N - 3, L::LO_VEC, L::W_VEC, bB);
+    auto vbody = [&](int j, dbl2 (&bl)[2], dbl2 (&bp)[2]) {
+      const int k = N - 1 - j;
+      const int rb = L::PV + (j & 1) * NX, wb = L::PV + ((j + 1) & 1) * NX;
+      ring_issue(k - 3 >= 0 ? k - 3 : 0, L::LO_VEC, L::W_VEC, bl);
+      double pv[NX], an[NX], cn, pn;
+      UNR for (int q = 0; q < NX; ++q) pv[q] = s[rb + q];
+      vld(slot_base((j + 1 < cnt ? j + 1 : j) % 3), an, cn, pn);
+      __builtin_amdgcn_sched_barrier(0);
+      double p0 = cc, p1 = 0.0;
+      UNR for (int q = 0; q < NX; q += 2) p0 += acl[q] * pv[q];
+      UNR for (int q = 1; q < NX; q += 2) p1 += acl[q] * pv[q];
+      if (t < NX) s[L::XS + k * NX + t] = pe + pcur;
+      pcur = p0 + p1;
+      if (t < NX) s[wb + t] = pcur;
+      UNR for (int q = 0; q < NX; ++q) acl[q] = an[q];
+      cc = cn;
+      pe = pn;
+      if (j + 2 < cnt) ring_put((j + 2) % 3, L::W_VEC, bp);
+      lsync();
+    };
+    for (int j = 0; j < cnt; j += 2) {
+      vbody(j, bA, bB);
+      if (j + 1 < cnt) vbody(j + 1, bB, bA);
+    }
+    if (t < NX) s[L::PV + t] = pcur;
+    __syncthreads();
+    // k_f = -Ru^-1 (g_u + B'v) per stage, lin = sum Y'k_f  (stage-parallel)
     double lin[NQ];
     UNR for (int j = 0; j < NQ; ++j) lin[j] = 0.0;
+    constexpr int NBB = (NX * NU + 1) / 2, NLY = (OPE - (OLR & ~1) + 1) / 2;   // B; chol(Ru), M, Y
     for (int k = 1 + t; k < N; k += 64) {
-      double r[NU], L[NU * NU];
+      double bb[2 * NBB], ly[2 * NLY], gg[2 * ((2 * NZ + 1) / 2)];
+      ldr<OB, NBB>(k, bb);
+      ldr<(OLR & ~1), NLY>(k, ly);
+      ldr<OD, (2 * NZ + 1) / 2>(k, gg);
+      __builtin_amdgcn_sched_barrier(0);
+      constexpr int LR_ = OLR - (OLR & ~1), Y_ = OY - (OLR & ~1);
+      const int go = OG - OD;
+      double r[NU], Lm[NU * NU];
       UNR for (int a = 0; a < NU; ++a) {
-        double x = st(k, OG + NX + a);
-        UNR for (int i = 0; i < NX; ++i) x += st(k, OB + i * NU + a) * st(k, OV + i);
+        double x = (go == 0) ? gg[NX + a] : gg[NZ + NX + a];
+        UNR for (int i = 0; i < NX; ++i) x += bb[i * NU + a] * s[L::XS + k * NX + i];
         r[a] = x;
       }
-      UNR for (int e = 0; e < NU * NU; ++e) L[e] = st(k, OLR + e);
-      chol_solve<NU>(L, r);
+      UNR for (int e = 0; e < NU * NU; ++e) Lm[e] = ly[LR_ + e];
+      chol_solve<NU>(Lm, r);
       UNR for (int a = 0; a < NU; ++a) {
         r[a] = -r[a];
         st(k, OKF + a) = r[a];
       }
       UNR for (int j = 0; j < NQ; ++j)
-        UNR for (int a = 0; a < NU; ++a) lin[j] += st(k, OY + a * NQ + j) * r[a];
+        UNR for (int a = 0; a < NU; ++a) lin[j] += ly[Y_ + a * NQ + j] * r[a];
     }
     UNR for (int j = 0; j < NQ; ++j) lin[j] = wsum(lin[j]);
     // stage 0 (every lane, identical)
     {
-      double v[NX], L[M0 * M0];
-      UNR for (int i = 0; i < NX; ++i) v[i] = fv(CL::PE0 + i) + fv(CL::PV + i);
+      double v[NX], Lm[M0 * M0];
+      UNR for (int i = 0; i < NX; ++i) v[i] = s[L::PE0 + i] + s[L::PV + i];
       UNR for (int a = 0; a < M0; ++a) {
         double x = st(0, OG + a);
-        UNR for (int i = 0; i < NX; ++i) x += fv(CL::F0 + i * M0 + a) * v[i];
+        UNR for (int i = 0; i < NX; ++i) x += s[L::F0 + i * M0 + a] * v[i];
         w0[a] = x;
       }
-      UNR for (int e = 0; e < M0 * M0; ++e) L[e] = fv(CL::LR0 + e);
-      chol_solve<M0>(L, w0);
+      UNR for (int e = 0; e < M0 * M0; ++e) Lm[e] = s[L::LR0 + e];
+      chol_solve<M0>(Lm, w0);
       UNR for (int a = 0; a < M0; ++a) w0[a] = -w0[a];
       UNR for (int j = 0; j < NQ; ++j)
-        UNR for (int a = 0; a < M0; ++a) lin[j] += fv(CL::Y0 + a * NQ + j) * w0[a];
+        UNR for (int a = 0; a < M0; ++a) lin[j] += s[L::Y0 + a * NQ + j] * w0[a];
     }
     double Sl[NQ * NQ];
-    UNR for (int e = 0; e < NQ * NQ; ++e) Sl[e] = fv(CL::SC + e);
+    UNR for (int e = 0; e < NQ * NQ; ++e) Sl[e] = s[L::SC + e];
     const bool ok = chol<NQ>(Sl);
-    UNR for (int j = 0; j < NQ; ++j) nun[j] = lin[j] + fv(CL::LINE + j) - rs * par(PF::E0N + j);
+    UNR for (int j = 0; j < NQ; ++j) nun[j] = lin[j] + s[L::LINE + j] - rs * par(PF::E0N + j);
     chol_solve<NQ>(Sl, nun);
     __syncthreads();
     return ok;
@@ -669,7 +910,7 @@ struct Coop {
       double w0[M0];
       UNR for (int a = 0; a < M0; ++a) {
         double x = w0in[a];
-        UNR for (int j = 0; j < NQ; ++j) x -= fv(CL::MM0 + a * NQ + j) * nun[j];
+        UNR for (int j = 0; j < NQ; ++j) x -= s[L::MM0 + a * NQ + j] * nun[j];
         w0[a] = x;
       }
       if (t == 0) {
@@ -677,93 +918,133 @@ struct Coop {
       }
       if (t < NX) {
         double x = rs * st(0, OE + t);
-        UNR for (int a = 0; a < M0; ++a) x += fv(CL::F0 + t * M0 + a) * w0[a];
-        st(1, OT + t) = x;
+        UNR for (int a = 0; a < M0; ++a) x += s[L::F0 + t * M0 + a] * w0[a];
+        s[L::XS + NX + t] = x;
+        s[L::DXV + t] = x;
       }
     }
+    // dx_{k+1} = c_k + A_cl,k dx_k,  c_k = rs e_k + B_k (k_f - M_k nu)  (lane i: row i); c is formed
+    // stage-parallel first (-> OC)
+    {
+      constexpr int NBB = (NX * NU + 1) / 2, NFM = (OY - OKF + 1) / 2;   // B; k_f, chol(Ru), M
+      for (int k = 1 + t; k < N; k += 64) {
+        double e[NX], bb[2 * NBB], fm[2 * NFM];
+        ldr<OE, NX / 2>(k, e);
+        ldr<OB, NBB>(k, bb);
+        ldr<OKF, NFM>(k, fm);
+        __builtin_amdgcn_sched_barrier(0);
+        double kfm[NU];
+        UNR for (int a = 0; a < NU; ++a) {
+          double x = fm[a];
+          UNR for (int j = 0; j < NQ; ++j) x -= fm[(OM - OKF) + a * NQ + j] * nun[j];
+          kfm[a] = x;
+        }
+        gdbl2* dst = (gdbl2*)(g + (long long)k * REC + OC);
+        UNR for (int i = 0; i < NX; i += 2) {
+          double v[2];
+          UNR for (int h2 = 0; h2 < 2; ++h2) {
+            double c = rs * e[i + h2];
+            UNR for (int a = 0; a < NU; ++a) c += bb[(i + h2) * NU + a] * kfm[a];
+            v[h2] = c;
+          }
+          dbl2 vv;
+          vv.x = v[0];
+          vv.y = v[1];
+          dst[i / 2] = vv;
+        }
+      }
+      __syncthreads();
+    }
+    const int cnt = N - 1;   // stages 1 .. N-1
+    dbl2 b[2];
+    if (cnt >= 1) { ring_issue(1, L::LO_FWD, L::W_FWD, b); ring_put(0, L::W_FWD, b); }
+    if (cnt >= 2) { ring_issue(2, L::LO_FWD, L::W_FWD, b); ring_put(1, L::W_FWD, b); }
     __syncthreads();
-    // dx_{k+1} = c_k + A_cl,k dx_k, c_k = rs e_k + B_k (k_f - M nu); lane i: row i.  The stage-only
-    // terms of stage k+1 are formed while stage k waits on dx_k.
-    struct FT { double e, kf[NU], m[NU * NQ], b[NU], a[NX], k[NU * NX]; };
-    auto fload = [&](int k, FT& r) {
-      const int i = t;
-      r.e = st(k, OE + i);
-      UNR for (int a = 0; a < NU; ++a) { r.kf[a] = st(k, OKF + a); r.b[a] = st(k, OB + i * NU + a); }
-      UNR for (int e = 0; e < NU * NQ; ++e) r.m[e] = st(k, OM + e);
-      UNR for (int q = 0; q < NX; ++q) r.a[q] = st(k, OA + i * NX + q);
-      UNR for (int e = 0; e < NU * NX; ++e) r.k[e] = st(k, OK + e);
-    };
-    auto fterms = [&](const FT& r, double (&acl)[NX], double& cc) {
-      double c = rs * r.e;
-      UNR for (int a = 0; a < NU; ++a) {
-        double kfm = r.kf[a];
-        UNR for (int j = 0; j < NQ; ++j) kfm -= r.m[a * NQ + j] * nun[j];
-        c += r.b[a] * kfm;
-      }
-      UNR for (int q = 0; q < NX; ++q) {
-        double a = r.a[q];
-        UNR for (int b = 0; b < NU; ++b) a += r.b[b] * r.k[b * NX + q];
-        acl[q] = a;
-      }
-      cc = c;
+    // ring slot of the forward sweep: [C | ACL]
+    auto fld = [&](int kb, double (&acl)[NX], double& cc) {
+      const int i = t < NX ? t : NX - 1;
+      UNR for (int q = 0; q < NX; ++q) acl[q] = s[kb + (OACL - OC) + i * NX + q];
+      cc = s[kb + i];
     };
     {
       double acl[NX], cc = 0.0;
-      if (t < NX) {
-        FT r;
-        fload(1 < N ? 1 : N - 1 > 0 ? N - 1 : 1, r);
-        fterms(r, acl, cc);
-      }
-      for (int k = 1; k < N; ++k) {
+      if (cnt >= 1) fld(slot_base(0), acl, cc);
+      dbl2 bA[2], bB[2];
+      if (cnt >= 3) ring_issue(3, L::LO_FWD, L::W_FWD, bB);
+      auto fbody = [&](int j, dbl2 (&bl)[2], dbl2 (&bp)[2]) {
+        const int k = 1 + j;
+        const int rb = L::DXV + (j & 1) * NX, wb = L::DXV + ((j + 1) & 1) * NX;
+        ring_issue(k + 3 < N ? k + 3 : N - 1, L::LO_FWD, L::W_FWD, bl);
+        double dx[NX], an[NX], cn;
+        UNR for (int q = 0; q < NX; ++q) dx[q] = s[rb + q];
+        fld(slot_base((j + 1 < cnt ? j + 1 : j) % 3), an, cn);
+        __builtin_amdgcn_sched_barrier(0);
+        double p0 = cc, p1 = 0.0;
+        UNR for (int q = 0; q < NX; q += 2) p0 += acl[q] * dx[q];
+        UNR for (int q = 1; q < NX; q += 2) p1 += acl[q] * dx[q];
+        const double dn = p0 + p1;
         if (t < NX) {
-          double dx[NX];
-          UNR for (int q = 0; q < NX; ++q) dx[q] = st(k, OT + q);
-          FT r;
-          fload(k + 1 < N ? k + 1 : k, r);
-          __builtin_amdgcn_sched_barrier(0);
-          double p0 = cc, p1 = 0.0;
-          UNR for (int q = 0; q < NX; q += 2) p0 += acl[q] * dx[q];
-          UNR for (int q = 1; q < NX; q += 2) p1 += acl[q] * dx[q];
-          st(k + 1, OT + t) = p0 + p1;
-          fterms(r, acl, cc);
+          s[wb + t] = dn;
+          s[L::XS + (k + 1) * NX + t] = dn;
         }
-        __syncthreads();
+        UNR for (int q = 0; q < NX; ++q) acl[q] = an[q];
+        cc = cn;
+        if (j + 2 < cnt) ring_put((j + 2) % 3, L::W_FWD, bp);
+        lsync();
+      };
+      for (int j = 0; j < cnt; j += 2) {
+        fbody(j, bA, bB);
+        if (j + 1 < cnt) fbody(j + 1, bB, bA);
       }
     }
+    __syncthreads();   // dx rows (global) visible to the stage-parallel pass
     // controls of the middle stages, then the step-length tests (stage-parallel)
     typename Lane<NQ>::MinRatio mr{1.0, CORR ? o.tau : 1.0};
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    constexpr int NKM = (OY - OK + 1) / 2;   // K, k_f, chol(Ru), M: the range [OK, OY)
     for (int k = t; k <= N; k += 64) {
-      if (k > 0) {
+      IP r;
+      double km[2 * NKM], da[2 * ((2 * NZ + 1) / 2)];
+      const int kk = (k > 0 && k < N) ? k : 1 < N ? 1 : 0;
+      ld_ip(k, r);
+      ldr<OK, NKM>(kk, km);
+      if (CORR) ldr<OD, (2 * NZ + 1) / 2>(k, da);
+      __builtin_amdgcn_sched_barrier(0);
+      gdouble* rec = &g[(long long)k * REC];
+      double d[NZ];
+      if (k == 0) {
+        UNR for (int i = 0; i < NZ; ++i) d[i] = rec[OT + i];   // written by lane 0 before the sweep
+      } else {
+        UNR for (int i = 0; i < NX; ++i) d[i] = s[L::XS + k * NX + i];
         UNR for (int a = 0; a < NU; ++a) {
           double x = 0.0;
           if (k < N) {
-            x = st(k, OKF + a);
-            UNR for (int j = 0; j < NQ; ++j) x -= st(k, OM + a * NQ + j) * nun[j];
-            UNR for (int i = 0; i < NX; ++i) x += st(k, OK + a * NX + i) * st(k, OT + i);
+            x = km[OKF - OK + a];
+            UNR for (int j = 0; j < NQ; ++j) x -= km[OM - OK + a * NQ + j] * nun[j];
+            UNR for (int i = 0; i < NX; ++i) x += km[a * NX + i] * d[i];
           }
-          st(k, OT + NX + a) = x;
+          d[NX + a] = x;
         }
+        UNR for (int i = 0; i < NZ; ++i) rec[OT + i] = d[i];
       }
       UNR for (int i = 0; i < NZ; ++i) {
-        const CS c = comp(k, i);
+        const CS c = comp_r(r, k, i);
         if (!c.bx) continue;
-        const double d = st(k, OT + i);
         double dll, dlu;
         if (!CORR) {
-          dll = -c.ql - c.ql * d * c.itl;
-          dlu = -c.qu + c.qu * d * c.itu;
+          dll = -c.ql - c.ql * d[i] * c.itl;
+          dlu = -c.qu + c.qu * d[i] * c.itu;
           a0 += c.tl * c.ql + c.tu * c.qu;
-          a1 += c.tl * dll + d * c.ql + c.tu * dlu - d * c.qu;
-          a2 += d * dll - d * dlu;
+          a1 += c.tl * dll + d[i] * c.ql + c.tu * dlu - d[i] * c.qu;
+          a2 += d[i] * dll - d[i] * dlu;
         } else {
           double rl, ru;
-          corr_rhs(c, st(k, ODA + i), smu, rl, ru);
-          dll = (rl - c.ql * d) * c.itl;
-          dlu = (ru + c.qu * d) * c.itu;
+          corr_rhs(c, da[NZ + i], smu, rl, ru);
+          dll = (rl - c.ql * d[i]) * c.itl;
+          dlu = (ru + c.qu * d[i]) * c.itu;
         }
-        mr.add(c.tl, d);
-        mr.add(c.tu, -d);
+        mr.add(c.tl, d[i]);
+        mr.add(c.tu, -d[i]);
         mr.add(c.ql, dll);
         mr.add(c.qu, dlu);
       }
@@ -776,17 +1057,23 @@ struct Coop {
   __device__ void update(double alpha, double smu) {
     double musum = 0.0;
     for (int k = t; k <= N; k += 64) {
+      IP r;
+      double dd[2 * ((2 * NZ + 1) / 2)];   // D then DA
+      ld_ip(k, r);
+      ldr<OD, (2 * NZ + 1) / 2>(k, dd);
+      __builtin_amdgcn_sched_barrier(0);
+      gdouble* rec = &g[(long long)k * REC];
       UNR for (int i = 0; i < NZ; ++i) {
-        const CS c = comp(k, i);
-        const double d = st(k, OD + i);
-        st(k, ODZ + i) = c.dz + alpha * d;
+        const CS c = comp_r(r, k, i);
+        const double d = dd[i];
+        rec[ODZ + i] = c.dz + alpha * d;
         if (!c.bx) continue;
         double rl, ru;
-        corr_rhs(c, st(k, ODA + i), smu, rl, ru);
+        corr_rhs(c, dd[NZ + i], smu, rl, ru);
         const double dll = (rl - c.ql * d) * c.itl, dlu = (ru + c.qu * d) * c.itu;
         const double qln = c.ql + alpha * dll, qun = c.qu + alpha * dlu;
-        st(k, OQL + i) = qln;
-        st(k, OQU + i) = qun;
+        rec[OQL + i] = qln;
+        rec[OQU + i] = qun;
         musum += (c.tl + alpha * d) * qln + (c.tu - alpha * d) * qun;
       }
     }
@@ -800,36 +1087,56 @@ struct Coop {
     if (t < NX) {
       const int i = t;
       const double dz = st(N, ODZ + i);
-      st(N - 1, ODA + i) = o.lm * dz - st(N, OQL + i) + st(N, OQU + i) +
-                           (i >= NQ ? par(PF::QNU + (i >= NQ ? i - NQ : 0)) : 0.0);
+      const double lam = o.lm * dz - st(N, OQL + i) + st(N, OQU + i) +
+                         (i >= NQ ? par(PF::QNU + (i >= NQ ? i - NQ : 0)) : 0.0);
+      s[L::XS + (N - 1) * NX + i] = lam;
+      s[L::DXV + i] = lam;
       fin = isfinite(dz);
     }
     fin = __ballot(!fin) == 0ull;
+    const int cnt = N - 1;   // stages N-1 .. 1
+    dbl2 b[2];
+    if (cnt >= 1) { ring_issue(N - 1, 0, L::W_COS, b); ring_put(0, L::W_COS, b); }
+    if (cnt >= 2) { ring_issue(N - 2, 0, L::W_COS, b); ring_put(1, L::W_COS, b); }
     __syncthreads();
-    {
-      auto cterms = [&](int k, double (&ac)[NX], double& cc) {
-        const int i = t;
-        cc = o.lm * st(k, ODZ + i) - st(k, OQL + i) + st(k, OQU + i);
-        UNR for (int q = 0; q < NX; ++q) ac[q] = st(k, OA + q * NX + i);
-      };
-      double ac[NX], cc = 0.0;
-      if (t < NX) cterms(N - 1 >= 1 ? N - 1 : 1, ac, cc);
-      for (int k = N - 1; k >= 1; --k) {
-        if (t < NX) {
-          double lam[NX], an[NX], cn;
-          UNR for (int q = 0; q < NX; ++q) lam[q] = st(k, ODA + q);
-          cterms(k - 1 >= 1 ? k - 1 : 1, an, cn);
-          __builtin_amdgcn_sched_barrier(0);
-          double p0 = cc, p1 = 0.0;
-          UNR for (int q = 0; q < NX; q += 2) p0 += ac[q] * lam[q];
-          UNR for (int q = 1; q < NX; q += 2) p1 += ac[q] * lam[q];
-          st(k - 1, ODA + t) = p0 + p1;
-          UNR for (int q = 0; q < NX; ++q) ac[q] = an[q];
-          cc = cn;
-        }
-        __syncthreads();
+    auto cterms = [&](int kb, double (&ac)[NX], double& cc) {
+      const int i = t < NX ? t : NX - 1;
+      cc = o.lm * s[kb + ODZ + i] - s[kb + OQL + i] + s[kb + OQU + i];
+      UNR for (int q = 0; q < NX; ++q) ac[q] = s[kb + OA + q * NX + i];
+    };
+    double ac[NX], cc = 0.0;
+    if (cnt >= 1) cterms(slot_base(0), ac, cc);
+    dbl2 bA[2], bB[2];
+    if (cnt >= 3) ring_issue(N - 3, 0, L::W_COS, bB);
+    auto cbody = [&](int j, dbl2 (&bl)[2], dbl2 (&bp)[2]) {
+      const int k = N - 1 - j;
+      const int rb = L::DXV + (j & 1) * NX, wb = L::DXV + ((j + 1) & 1) * NX;
+      ring_issue(k - 3 >= 0 ? k - 3 : 0, 0, L::W_COS, bl);
+      double lam[NX], an[NX], cn;
+      UNR for (int q = 0; q < NX; ++q) lam[q] = s[rb + q];
+      cterms(slot_base((j + 1 < cnt ? j + 1 : j) % 3), an, cn);
+      __builtin_amdgcn_sched_barrier(0);
+      double p0 = cc, p1 = 0.0;
+      UNR for (int q = 0; q < NX; q += 2) p0 += ac[q] * lam[q];
+      UNR for (int q = 1; q < NX; q += 2) p1 += ac[q] * lam[q];
+      const double x = p0 + p1;
+      if (t < NX) {
+        s[wb + t] = x;
+        s[L::XS + (k - 1) * NX + t] = x;
       }
+      UNR for (int q = 0; q < NX; ++q) ac[q] = an[q];
+      cc = cn;
+      if (j + 2 < cnt) ring_put((j + 2) % 3, L::W_COS, bp);
+      lsync();
+    };
+    for (int j = 0; j < cnt; j += 2) {
+      cbody(j, bA, bB);
+      if (j + 1 < cnt) cbody(j + 1, bB, bA);
     }
+    for (int k = t; k < N; k += 64) {
+      UNR for (int i = 0; i < NX; ++i) st(k, ODA + i) = s[L::XS + k * NX + i];
+    }
+    __syncthreads();
     return fin;
   }
 
@@ -840,12 +1147,9 @@ struct Coop {
     double lmax = 0.0;
     for (int k = t; k <= N; k += 64) {
       if (k < N) {
-        UNR for (int i = 0; i < NX; ++i) {
-          gdouble& wp = G.atv(w.WPI, NX, k, i);
-          wp = Lane<NQ>::wupd(wp, st(k, ODA + i));
-        }
+        UNR for (int i = 0; i < NX; ++i) st(k, OWPI + i) = Lane<NQ>::wupd(st(k, OWPI + i), st(k, ODA + i));
       }
-      UNR for (int i = 0; i < NZ; ++i) lmax = fmax(lmax, fmax(st(k, OQL + i), st(k, OQU + i)));
+      UNR for (int i = 0; i < NZ; ++i) lmax = fmax(lmax, fmax((double)st(k, OQL + i), (double)st(k, OQU + i)));
     }
     lmax = wmaxd(lmax);
     if (t == 0) {
@@ -860,7 +1164,7 @@ struct Coop {
     const double sv = par(PF::S) + alpha * st(0, ODZ);
     double val = 0.0, viol = 0.0;
     for (int k = t; k <= N; k += 64) {
-      const double* rec = &s[k * REC];
+      const gdouble* rec = &g[(long long)k * REC];
       UNR for (int i = 0; i < NZ; ++i) {
         double lb, ub;
         if (!box(k, i, lb, ub)) continue;
@@ -868,7 +1172,7 @@ struct Coop {
         viol += fmax(0.0, lb - v) + fmax(0.0, v - ub);
       }
       if (k > 0) {
-        const double* rp = &s[(k - 1) * REC];
+        const gdouble* rp = &g[(long long)(k - 1) * REC];
         double xp[NX], up[NU], phi[NX];
         if (k == 1) {
           UNR for (int j = 0; j < NQ; ++j) { xp[j] = par(PF::Q0 + j); xp[NQ + j] = sv * par(PF::DIR + j); }
@@ -880,7 +1184,7 @@ struct Coop {
         rk4<NQ>(h, xp, up, phi);
         UNR for (int i = 0; i < NX; ++i) {
           const double xn = rec[OZ + i] + alpha * rec[ODZ + i];
-          val += G.atv(w.WPI, NX, k - 1, i) * fabs(phi[i] - xn);
+          val += rp[OWPI + i] * fabs(phi[i] - xn);
         }
         if (k == N) {
           UNR for (int j = 0; j < NQ; ++j)
@@ -893,25 +1197,21 @@ struct Coop {
 
   __device__ void apply(double alpha) {
     for (int k = t; k <= N; k += 64) {
+      gdouble* rec = &g[(long long)k * REC];
       if (k == 0) {
-        UNR for (int a = 0; a < NU; ++a) G.atv(w.U, NU, 0, a) += alpha * st(0, ODZ + 1 + a);
+        UNR for (int a = 0; a < NU; ++a) rec[OU + a] += alpha * rec[ODZ + 1 + a];
       } else {
-        UNR for (int i = 0; i < NX; ++i) G.atv(w.X, NX, k, i) += alpha * st(k, ODZ + i);
+        UNR for (int i = 0; i < NX; ++i) rec[OX + i] += alpha * rec[ODZ + i];
         if (k < N) {
-          UNR for (int a = 0; a < NU; ++a) G.atv(w.U, NU, k, a) += alpha * st(k, ODZ + NX + a);
+          UNR for (int a = 0; a < NU; ++a) rec[OU + a] += alpha * rec[ODZ + NX + a];
         }
       }
       UNR for (int i = 0; i < NZ; ++i) {
-        gdouble& ll = G.atv(w.LL, NZ, k, i);
-        gdouble& lu = G.atv(w.LU, NZ, k, i);
-        ll += alpha * (st(k, OQL + i) - ll);
-        lu += alpha * (st(k, OQU + i) - lu);
+        rec[OLL + i] += alpha * (rec[OQL + i] - rec[OLL + i]);
+        rec[OLU + i] += alpha * (rec[OQU + i] - rec[OLU + i]);
       }
       if (k < N) {
-        UNR for (int i = 0; i < NX; ++i) {
-          gdouble& pi = G.atv(w.PI, NX, k, i);
-          pi += alpha * (st(k, ODA + i) - pi);
-        }
+        UNR for (int i = 0; i < NX; ++i) rec[OPI + i] += alpha * (rec[ODA + i] - rec[OPI + i]);
       }
     }
     __syncthreads();
@@ -930,12 +1230,12 @@ struct Coop {
     for (int k = t; k <= N; k += 64) {
       UNR for (int i = 0; i < NX; ++i) {
         const double v = (k == 0) ? (i < NQ ? par(PF::Q0 + i) : sv * par(PF::DIR + (i - NQ + (i < NQ ? NQ : 0))))
-                                  : (double)G.atv(w.X, NX, k, i);
+                                  : (double)st(k, OX + i);
         xo[(long long)k * NXR + i] = v;
       }
       xo[(long long)k * NXR + NX] = h;
       if (k < N) {
-        UNR for (int a = 0; a < NU; ++a) uo[(long long)k * NU + a] = G.atv(w.U, NU, k, a);
+        UNR for (int a = 0; a < NU; ++a) uo[(long long)k * NU + a] = st(k, OU + a);
       }
     }
     if (t == 0) {
@@ -946,17 +1246,14 @@ struct Coop {
     }
   }
 
-  // the remaining SQP of this slot's problem, to termination
-  __device__ void run(const Inputs& in, const SlotState& ss) {
-    const unsigned sl = G.slot;
-    const int pid = ss(IS_PID, sl);
-    N = ss(IS_N, sl);
-    int it = ss(IS_IT, sl), qit = ss(IS_QIT, sl);
-    for (int f = t; f < PF::COUNT; f += 64) par(f) = G.par(f);
-    for (int e = t; e < 16; e += 64) fv(CL::ZERO + e) = 0.0;
+  // the remaining SQP of the loaded problem, to termination; returns the ACADOS status
+  __device__ int run(int& it, int& qit) {
+    for (int e = t; e < 16; e += 64) s[L::ZERO + e] = 0.0;
     __syncthreads();
     int status = -1;
     CPROF_DECL
+    const int it0 = it;
+    int qtot = 0;
     for (;;) {
       double rstat, req, rineq, rcomp;
       linearize(rstat, req, rineq, rcomp);
@@ -976,6 +1273,7 @@ struct Coop {
         prep_pred();
         CPROF(2)
         const bool okf = factor();
+        acl_pass();
         CPROF(3)
         const bool okv = vec(ODA, w0, nun);
         CPROF(4)
@@ -1005,6 +1303,7 @@ struct Coop {
         CPROF(6)
       }
       qit += qcur;
+      qtot += qcur;
       if (qst < 0 || !costate()) { status = 4; break; }
       CPROF(7)
       update_weights();
@@ -1021,28 +1320,74 @@ struct Coop {
       ++it;
       if (!isfinite(par(PF::S))) { status = 1; break; }
     }
-#ifdef VBOC_COOP_PROF
-    if (t == 0 && it - ss(IS_IT, sl) >= 300)
-      printf("[coop] pid %d N %d sqp %d qp %d | cyc lin %llu qpinit %llu prep %llu factor %llu vec %llu fwd %llu upd %llu costate %llu ls %llu\n",
-             pid, N, it, qit, cp_[0], cp_[1], cp_[2], cp_[3], cp_[4], cp_[5], cp_[6], cp_[7], cp_[8]);
-#endif
-    store(in, pid, status, it, qit);
-    __syncthreads();
-    if (t == 0) {
-      ss(IS_PID, sl) = -1;
-      ss(IS_PH, sl) = 0;
-      atomicAdd(ss.done, 1u);
-    }
+    CPROF_FLUSH(it - it0, qtot)
+    (void)it0;
+    return status;
   }
 };
 
-// one workgroup = one wave = one problem; list[] holds the slots still iterating
+// Jobs of the persistent wave kernel: either the slots still iterating in lane mode (hand-off,
+// list != nullptr) or problems [0, count) straight from the inputs.
+struct WaveJobs {
+  const int* list;
+  int count;
+  unsigned* next;          // job counter
+  double* regions;         // one stage-record region per workgroup
+  long long region_doubles;
+};
+
+// Register budget of the wave kernel.  Default: unrestricted (~470 VGPR+AGPR, 1 wave per SIMD, 4
+// problems per CU).  Forcing 2 waves per SIMD (-DVBOC_WAVE_WPE='__attribute__((amdgpu_waves_per_eu(2,2)))')
+// spills inside the recursions and measured 1.6x slower on the 100k bench (profiles/r01_*wave*).
+#ifndef VBOC_WAVE_WPE
+#define VBOC_WAVE_WPE
+#endif
+
+// one workgroup = one wave = one problem at a time; workgroups pull jobs until none are left
 template <int NQ>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_coop(Work w, Opts o, Inputs in, SlotState ss, const int* list, int nmax) {
+__global__ __launch_bounds__(64) VBOC_WAVE_WPE void k_wave(Work w, Opts o, Inputs in, SlotState ss, WaveJobs jb) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  const unsigned slot = (unsigned)__builtin_amdgcn_readfirstlane(list[blockIdx.x]);
-  Coop<NQ> C(smem, CoopLayout<NQ>::REC * (nmax + 1), w, o, slot, (int)threadIdx.x);
-  C.run(in, ss);
+  const int t = (int)threadIdx.x;
+  Coop<NQ> C(smem, gptr(jb.regions) + (long long)blockIdx.x * jb.region_doubles, w, o, t);
+  for (;;) {
+    unsigned idx = 0;
+    if (t == 0) idx = atomicAdd(jb.next, 1u);
+    idx = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl((int)idx, 0));
+    if (idx >= (unsigned)jb.count) break;
+    int pid, it = 0, qit = 0;
+    unsigned slot = 0;
+    if (jb.list) {
+      slot = (unsigned)__builtin_amdgcn_readfirstlane(jb.list[idx]);
+      pid = ss(IS_PID, slot);
+      it = ss(IS_IT, slot);
+      qit = ss(IS_QIT, slot);
+      C.from_slot(ss, slot);
+    } else {
+      pid = (int)idx;
+      Lane<NQ> chk(w, o, 0u);
+      if (!chk.supported(in, pid)) {
+        if (t == 0) {
+          in.status[pid] = 5;
+          in.cost[pid] = NAN;
+          in.sqp_iter[pid] = 0;
+          in.qp_iter[pid] = 0;
+          atomicAdd(ss.done, 1u);
+        }
+        continue;
+      }
+      C.from_inputs(in, pid);
+    }
+    const int status = C.run(it, qit);
+    C.store(in, pid, status, it, qit);
+    __syncthreads();
+    if (t == 0) {
+      if (jb.list) {
+        ss(IS_PID, slot) = -1;
+        ss(IS_PH, slot) = 0;
+      }
+      atomicAdd(ss.done, 1u);
+    }
+  }
 }
 
 // compact the slots still iterating (phase 1 at a round boundary) into list[]

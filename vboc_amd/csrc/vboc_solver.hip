@@ -1304,11 +1304,15 @@ struct vboc_solver {
   // host staging for vboc_solve_batch_host
   void* stage = nullptr;
   size_t stage_bytes = 0;
-  // cooperative tail (coop.h): once the queue is drained and at most coop_threshold problems are
-  // still iterating, each of them moves to one LDS-resident wave
+  // wave solver (coop.h): one problem per wave, stage records in per-workgroup HBM regions.
+  // Used for the tail (queue drained and at most coop_threshold problems still iterating) or, with
+  // wave_all, for every problem.
   int* list = nullptr;
   double coop_threshold = 8192;
-  size_t coop_lds = 0;
+  bool wave_all = true;
+  double* regions = nullptr;
+  long long n_regions = 0, region_doubles = 0, group_cap = 0;
+  size_t wave_lds = 0;
   bool coop_ok = false;
   long long coop_count = 0;
 };
@@ -1399,6 +1403,20 @@ static hipError_t launch_round(vboc_solver* h, dim3 grid, dim3 block, hipStream_
   return hipGetLastError();
 }
 
+static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs, hipStream_t st, const Work& w,
+                              const Inputs& in, const SlotState& ss) {
+  long long groups = jobs < h->n_regions ? jobs : h->n_regions;
+  if (h->group_cap > 0 && groups > h->group_cap) groups = h->group_cap;
+  if (groups < 1) return hipSuccess;
+  const dim3 grid((unsigned)groups), block(64);
+  switch (h->nq) {
+    case 1: hipLaunchKernelGGL(k_wave<1>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
+    case 2: hipLaunchKernelGGL(k_wave<2>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
+    default: hipLaunchKernelGGL(k_wave<3>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
+  }
+  return hipGetLastError();
+}
+
 extern "C" {
 
 const char* vboc_last_error(void) { return g_err.c_str(); }
@@ -1433,13 +1451,29 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   }
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);
-  // cooperative tail: the whole problem must fit one workgroup's LDS (160 KiB on gfx950)
-  h->coop_lds = nq == 1 ? CoopLayout<1>::lds_bytes(nmax) : (nq == 2 ? CoopLayout<2>::lds_bytes(nmax)
-                                                                      : CoopLayout<3>::lds_bytes(nmax));
-  h->coop_ok = h->coop_lds <= 160 * 1024;
-  if (h->coop_ok) {
-    const void* fn = nq == 1 ? (const void*)k_coop<1> : (nq == 2 ? (const void*)k_coop<2> : (const void*)k_coop<3>);
-    h->coop_ok = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->coop_lds) == hipSuccess;
+  // wave solver: one region of stage records per resident workgroup (occupancy x CUs)
+  {
+    const void* fn = nq == 1 ? (const void*)k_wave<1> : (nq == 2 ? (const void*)k_wave<2> : (const void*)k_wave<3>);
+    h->wave_lds = nq == 1 ? WaveLayout<1>::lds_bytes(nmax)
+                          : (nq == 2 ? WaveLayout<2>::lds_bytes(nmax) : WaveLayout<3>::lds_bytes(nmax));
+    h->region_doubles = (long long)(nq == 1 ? WaveLayout<1>::region_doubles(nmax)
+                                            : (nq == 2 ? WaveLayout<2>::region_doubles(nmax) : WaveLayout<3>::region_doubles(nmax)));
+    int per_cu = 0, cus = 0;
+    hipDeviceProp_t prop;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, h->wave_lds) == hipSuccess &&
+        hipGetDeviceProperties(&prop, device) == hipSuccess) {
+      cus = prop.multiProcessorCount;
+    }
+    (void)hipGetLastError();
+    if (per_cu < 1) per_cu = 1;
+    if (cus < 1) cus = 256;
+    h->n_regions = (long long)per_cu * cus;
+    if (h->n_regions > 16384) h->n_regions = 16384;
+    if (h->wave_lds > 160 * 1024) h->n_regions = 0;
+    h->coop_ok = h->n_regions > 0 &&
+                 hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wave_lds) == hipSuccess &&
+                 hipMalloc((void**)&h->regions, sizeof(double) * (size_t)h->region_doubles * (size_t)h->n_regions) ==
+                     hipSuccess;
     (void)hipGetLastError();
   }
   // carve the workspace
@@ -1472,6 +1506,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->head) (void)hipFree(h->head);
   if (h->ist) (void)hipFree(h->ist);
   if (h->list) (void)hipFree(h->list);
+  if (h->regions) (void)hipFree(h->regions);
   if (h->host_done) (void)hipHostFree(h->host_done);
   if (h->stage) (void)hipFree(h->stage);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
@@ -1501,6 +1536,8 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "ipm_push") o.push = v;
   else if (s == "ipm_tau") o.tau = v;
   else if (s == "coop_threshold") h->coop_threshold = v;
+  else if (s == "wave_all") h->wave_all = v != 0.0;
+  else if (s == "wave_groups") h->group_cap = (long long)v;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
     if (h->profile && h->pev.empty()) {
@@ -1533,6 +1570,8 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "ipm_tau") *v = o.tau;
   else if (s == "coop_threshold") *v = h->coop_threshold;
   else if (s == "coop_available") *v = h->coop_ok ? 1.0 : 0.0;
+  else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
+  else if (s == "wave_groups") *v = (double)h->n_regions;
   else if (s == "coop_problems") *v = (double)h->coop_count;
   else if (s == "slots") *v = (double)h->slots;
   else if (s == "workspace_bytes") *v = (double)h->pool_bytes;
@@ -1571,6 +1610,18 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   SlotState ss{h->ist, h->head + 1, h->head + 2, (unsigned long long*)(h->head + 4), h->slots};
   const dim3 grid((unsigned)(lanes / 256)), block(256);
   HIPCHK(hipEventRecord(h->ev0, st));
+  if (h->wave_all && h->coop_ok) {
+    // every problem on its own wave, pulled from the input queue (head[0])
+    WaveJobs jb{nullptr, b->B, h->head, h->regions, h->region_doubles};
+    h->launches = 1;
+    h->coop_count = b->B;
+    HIPCHK(launch_wave(h, jb, (long long)b->B, st, w, in, ss));
+    HIPCHK(hipEventRecord(h->ev1, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipMemcpy(h->host_done, h->head + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+    if (*h->host_done != (unsigned)b->B) return fail(VBOC_ERR_HIP, "vboc_solve_batch: wave solver did not finish");
+    return VBOC_OK;
+  }
   hipLaunchKernelGGL(k_slots_init, dim3((unsigned)((h->slots + 255) / 256)), block, 0, st, h->ist, h->slots);
   // One SQP iteration of every resident problem per round; finished slots refill from the queue.
   // The finished-problem counter is read back every `chunk` rounds (one host sync per chunk).
@@ -1606,13 +1657,10 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
       const unsigned n = h->host_done[2];
       h->coop_count = n;
       if (n) {
-        switch (h->nq) {
-          case 1: hipLaunchKernelGGL(k_coop<1>, dim3(n), dim3(64), h->coop_lds, st, w, h->o, in, ss, h->list, h->nmax); break;
-          case 2: hipLaunchKernelGGL(k_coop<2>, dim3(n), dim3(64), h->coop_lds, st, w, h->o, in, ss, h->list, h->nmax); break;
-          default: hipLaunchKernelGGL(k_coop<3>, dim3(n), dim3(64), h->coop_lds, st, w, h->o, in, ss, h->list, h->nmax); break;
-        }
+        HIPCHK(hipMemsetAsync(h->head + 5, 0, sizeof(unsigned), st));
+        WaveJobs jb{h->list, (int)n, h->head + 5, h->regions, h->region_doubles};
+        HIPCHK(launch_wave(h, jb, (long long)n, st, w, in, ss));
         h->launches += 2;
-        HIPCHK(hipGetLastError());
       }
       HIPCHK(hipMemcpyAsync(h->host_done, h->head + 1, sizeof(unsigned), hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -1637,6 +1685,14 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   if (h->profile) HIPCHK(prof_flush(h, st));
   HIPCHK(hipMemcpyAsync(&h->fact_stages, h->head + 4, sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  return VBOC_OK;
+}
+
+int vboc_debug_counters(unsigned long long* out16) {
+  if (!out16) return fail(VBOC_ERR_ARG, "vboc_debug_counters: NULL argument");
+  HIPCHK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_wave_prof), 16 * sizeof(unsigned long long)));
+  static const unsigned long long zero[16] = {0};
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), zero, sizeof(zero)));
   return VBOC_OK;
 }
 

@@ -19,7 +19,7 @@ SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
            "vboc_solve_batch_host", "vboc_rk4_batch", "vboc_rk4_batch_host", "vboc_last_kernel_ms",
-           "vboc_kernel_stats", "vboc_last_error")
+           "vboc_kernel_stats", "vboc_debug_counters", "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
 
@@ -74,6 +74,7 @@ def load():
                                         ctypes.c_void_p, ctypes.c_void_p]
     lib.vboc_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int)]
+    lib.vboc_debug_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
     lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
@@ -179,6 +180,15 @@ class Solver:
         n = ctypes.c_int()
         _check(self.lib.vboc_last_kernel_ms(self.h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+
+def debug_counters():
+    """Wave-solver phase cycles since the last call (zeros unless built with -DVBOC_COOP_PROF)."""
+    buf = (ctypes.c_ulonglong * 16)()
+    _check(load().vboc_debug_counters(buf))
+    names = ("linearize", "qp_init", "prep", "factor", "vec", "fwd", "update", "costate", "linesearch",
+             "sqp_iters", "ipm_iters")
+    return {n: int(buf[i]) for i, n in enumerate(names)}
 
 
 def rk4_host(nq, T, x, u):
