@@ -7,9 +7,13 @@ feeds the NN fit (configs[3]).  Problem ids are a global counter (Philox per id)
 ids [(step * world + r) * B, ... + B): per-GPU work is fixed as N grows (weak scaling).
 
 Output: ONE JSON line on rank 0 (contract in the task statement), with
-  roofline     dominant kernel k_qp_factor (Riccati factorisation sweep): algorithmic bytes per
-               launch / average launch duration, both measured live over the timed region with HIP
-               events on the solve stream (vboc_kernel_stats); bound "hbm", peak 8 TB/s.
+  roofline     the dominant kernel.  Default (wave mode) k_wave, the whole solve in one launch per
+               step: algorithmic FP64 work of the launch by the SURVEY 8(d) convention / its duration
+               (HIP events on the solve stream, vboc_last_kernel_ms); bound "mfma" = the FP64 dense
+               peak (78.6 TFLOP/s; vector and matrix are equal on MI355X).  --mode lane: the lane-mode
+               dominant kernel k_qp_factor, algorithmic bytes / duration (vboc_kernel_stats), bound "hbm".
+               traffic: HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
+               WRITE_SIZE, profiles/*_pmc_<kernel>.json).
   cpu_baseline the oracle's C restatement (oracle/, test infrastructure) on a bounded sample of the
                same workload on the host's cores, rank 0, N = 1 only.
 """
@@ -81,6 +85,8 @@ def main():
     ap.add_argument("--slots", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", choices=("wave", "lane"), default="wave",
+                    help="wave: one problem per wave (default); lane: lane-per-problem kernels + wave tail")
     args = ap.parse_args()
 
     import torch
@@ -99,12 +105,14 @@ def main():
     from vboc_amd import lib
     nq, B = args.nq, args.batch
     solver = lib.Solver(nq, 100, slots=args.slots, device=local)
-    solver.set_option("profile_kernels", 1)
+    solver.set_option("wave_all", 1 if args.mode == "wave" else 0)
+    solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
     stream = torch.cuda.current_stream(device)
 
+    from vboc_amd.dist import gather_boundary_states, shard_ids
+
     def ids_for(step):
-        base = (step * world + rank) * B
-        return np.arange(base, base + B, dtype=np.int64)
+        return shard_ids(step, world, rank, B)
 
     # inputs for every step generated and copied to HBM before any timing
     batches = [make_batch(nq, ids_for(s), device)[0] for s in range(args.warmup + args.steps)]
@@ -113,10 +121,7 @@ def main():
     def run_step(tb):
         out = solver.solve_device(tb, stream=stream)
         if world > 1:
-            x0 = out["x"][:, 0, :].contiguous()
-            gathered = torch.empty((world,) + tuple(x0.shape), dtype=x0.dtype, device=device)
-            dist.all_gather_into_tensor(gathered, x0)
-            out["gathered"] = gathered
+            out["gathered"] = gather_boundary_states(out["x"][:, 0, :])
         return out
 
     for s in range(args.warmup):
@@ -124,16 +129,22 @@ def main():
     torch.cuda.synchronize(device)
 
     fact_ms, fact_launch, fact_bytes = 0.0, 0, 0.0
+    wave_ms, wave_launch = 0.0, 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for s in range(args.steps):
         outs.append(run_step(batches[args.warmup + s]))
-        ms, nl, by = solver.kernel_stats()
-        fact_ms += ms
-        fact_launch += nl
-        fact_bytes += by
+        if args.mode == "lane":
+            ms, nl, by = solver.kernel_stats()
+            fact_ms += ms
+            fact_launch += nl
+            fact_bytes += by
+        else:
+            ms, _ = solver.last_kernel_ms()
+            wave_ms += ms
+            wave_launch += 1
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
@@ -150,6 +161,7 @@ def main():
     # K_ls counted as 2 merit evaluations per SQP iteration (phi(0) + one trial: a lower bound)
     Nh = 100
     flops = float(np.sum(Nh * (F_DYN[nq] * sqp + F_IPM[nq] * qpi + 2 * 4 * C_F[nq] * sqp)))
+    local_flops = flops
     if world > 1:
         ft = torch.tensor([flops], device=device, dtype=torch.float64)
         dist.all_reduce(ft)
@@ -167,7 +179,29 @@ def main():
         cpu = {"value": round(v, 2), "unit": "solves/s", "cores": threads, "kind": "port",
                "sample": f"first {n} problems of the same workload (oracle/vboc_oracle.c, OpenMP, {t:.1f} s)"}
 
-    traffic_gb, traffic_src = pmc_traffic("k_qp_factor")
+    if args.mode == "lane":
+        traffic_gb, traffic_src = pmc_traffic("k_qp_factor")
+        roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1) if achieved_gbs else None,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved_gbs / HBM_PEAK_GBS, 4) if achieved_gbs else None,
+                    "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
+                    "traffic_source": traffic_src,
+                    "algorithmic_gb_per_launch": round(fact_bytes / max(1, fact_launch) / 1e9, 4),
+                    "kernel": f"k_qp_factor<{nq}>", "avg_launch_ms": round(avg_launch_ms, 4),
+                    "launches": fact_launch}
+    else:
+        traffic_gb, traffic_src = pmc_traffic("k_wave")
+        avg_ms = wave_ms / max(1, wave_launch)
+        per_launch = local_flops / max(1, args.steps)
+        wave_tf = per_launch / (avg_ms * 1e-3) / 1e12 if wave_ms else None
+        roofline = {"bound": "mfma", "achieved": round(wave_tf, 4) if wave_tf else None,
+                    "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(wave_tf / FP64_PEAK_TFLOPS, 5) if wave_tf else None,
+                    "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
+                    "traffic_source": traffic_src,
+                    "algorithmic": "FP64 flops per launch, SURVEY.md 8(d): N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp)",
+                    "flops_per_launch": round(per_launch), "kernel": f"k_wave<{nq}>",
+                    "avg_launch_ms": round(avg_ms, 3), "launches": wave_launch}
     if rank == 0:
         line = {
             "metric": "VBOC boundary OCP solves/sec, triple pendulum, 1/2/4/8 MI355X",
@@ -184,16 +218,9 @@ def main():
             "data": "synthetic (Philox-seeded ICs by the reference's data_generation law)",
             "config": {"workload": f"{'triple' if nq == 3 else nq}-pendulum data_generation first OCP solve, "
                                    f"N=100, {B} ICs per GPU per step (configs[2]; configs[3] at 8 GPUs)",
-                       "problems_per_gpu": B, "horizon": 100, "parallelism": f"dp{world}",
+                       "problems_per_gpu": B, "horizon": 100, "parallelism": f"dp{world}", "mode": args.mode,
                        "allgather": world > 1},
-            "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 1) if achieved_gbs else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved_gbs / HBM_PEAK_GBS, 4) if achieved_gbs else None,
-                         "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
-                         "traffic_source": traffic_src,
-                         "algorithmic_gb_per_launch": round(fact_bytes / max(1, fact_launch) / 1e9, 4),
-                         "kernel": "k_qp_factor<3>",
-                         "avg_launch_ms": round(avg_launch_ms, 4), "launches": fact_launch},
+            "roofline": roofline,
             "path_fp64": {"achieved": round(flops / elapsed / 1e12, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                           "frac": round(flops / elapsed / 1e12 / FP64_PEAK_TFLOPS, 5),
                           "convention": "SURVEY.md 8(d): N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp)"},

@@ -25,14 +25,19 @@ def main():
     ws, nw = total(write_csv, "WRITE_SIZE", kernel)
     line = json.loads(open(bench_json).read().strip().splitlines()[-1])
     rf = line["roofline"]
-    alg = rf["achieved"] * 1e9 * rf["avg_launch_ms"] * 1e-3
     fetch_b = 2.0 * fs * 1024 / nf
     write_b = ws * 1024 / nw
     out = {"kernel": kernel, "launches_fetch_pass": nf, "launches_write_pass": nw,
            "fetch_bytes_per_launch_corrected": fetch_b, "write_bytes_per_launch": write_b,
            "traffic_bytes_per_launch": fetch_b + write_b,
-           "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (fetch_b + write_b) / alg,
            "correction": "FETCH_SIZE x2 (gfx950), KB -> bytes x1024"}
+    if rf["unit"] == "GB/s":   # bandwidth roofline: compare with the algorithmic bytes
+        alg = rf["achieved"] * 1e9 * rf["avg_launch_ms"] * 1e-3
+        out.update(algorithmic_bytes_per_launch=alg, traffic_over_algorithmic=(fetch_b + write_b) / alg)
+    else:                      # FP64 roofline: arithmetic intensity against HBM traffic
+        out.update(flops_per_launch=rf["flops_per_launch"],
+                   flop_per_hbm_byte=rf["flops_per_launch"] / (fetch_b + write_b),
+                   hbm_gbs_during_launch=(fetch_b + write_b) / (rf["avg_launch_ms"] * 1e-3) / 1e9)
     print(json.dumps(out, indent=1))
 
 

@@ -294,7 +294,9 @@ __device__ __forceinline__ void rk4_sens_g(double h, const double* x, const doub
         Ts[i][c] = 0.0;
       }
     }
-#pragma unroll
+    // stages not unrolled: one ModelPoint live at a time (bounds register pressure; the
+    // linearisation is ~1% of the solve)
+#pragma unroll 1
     for (int st = 0; st < 4; ++st) {
       const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
       const double cnext = (st < 2) ? 0.5 * h : h;
