@@ -1,0 +1,163 @@
+"""Golden outputs of the reference's data_generation state machine (run HERE only, needs /root/reference).
+
+`data_generation` is taken from the reference driver files by AST (the function alone, parsed from the
+text of VBOC/triplependulum_vboc.py and VBOC/doublependulum_vboc.py) and executed with injected globals:
+  * `random`: serves the problem's Philox draws (vboc_amd.ics.uniforms stream 0 for the IC sampling,
+    vboc_amd.drivers.ProblemRNG stream 2 afterwards) in the order the function asks for them;
+  * `ocp`: an object with the OCP<sys>INIT surface the driver uses (N, OCP_solve, ocp_solver.get /
+    get_cost / set_new_time_steps / update_qp_solver_cond_N, and the double's g, l1, l2, m1, m2)
+    whose OCP_solve follows VBOC/triplependulum_class_vboc.py:155-191 (stages i < N from the guess
+    rows, stage N from the last row) and solves with the CPU oracle (oracle/, test infrastructure);
+  * `sim`: the twin integrator (set x/u/T, solve, get) as one oracle RK4 step.
+The fixture records each problem's return value.  tests/test_drivers.py runs vboc_amd.drivers with the
+same oracle backend and must reproduce it exactly: the pair pins the batched driver's restatement to
+the reference's own state machine (given identical solver results).
+
+Usage: python tests/golden/make_driver_golden.py  ->  tests/golden/driver_{2,3}.json
+"""
+import ast
+import json
+import math
+import os
+import sys
+
+import numpy as np
+from numpy.linalg import norm
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+REF = "/root/reference/VBOC"
+
+from vboc_amd.drivers import IC_DRAWS, ProblemRNG  # noqa: E402
+from vboc_amd.ics import SEED, uniforms  # noqa: E402
+from vboc_amd.systems import system  # noqa: E402
+
+IDS = {3: list(range(0, 12)), 2: list(range(100, 124))}
+N_START = 100
+
+
+def extract(path, name="data_generation"):
+    tree = ast.parse(open(path).read())
+    fn = [n for n in tree.body if isinstance(n, ast.FunctionDef) and n.name == name][0]
+    return compile(ast.Module(body=[fn], type_ignores=[]), path, "exec")
+
+
+class FakeRandom:
+    def __init__(self, first, rng):
+        self.first, self.rng = [float(v) for v in first], rng
+
+    def random(self):
+        return self.first.pop(0) if self.first else self.rng.random()
+
+    def choice(self, seq):
+        u = self.random()
+        return seq[min(int(u * len(seq)), len(seq) - 1)]
+
+
+def oracle_solve(nq, N, x_sol_guess, u_sol_guess, p, q_lb, q_ub, u_lb, u_ub, q_init_lb, q_init_ub, q_fin_lb,
+                 q_fin_ub):
+    import oracle
+    nx = 2 * nq + 1
+    xg = np.zeros((1, N + 1, nx))
+    ug = np.zeros((1, N, nq))
+    for i in range(N):
+        xg[0, i] = x_sol_guess[i]
+        ug[0, i] = u_sol_guess[i]
+    xg[0, N] = x_sol_guess[-1]
+    a = lambda v: np.asarray(v, dtype=np.float64)[None]
+    xo, uo, r = oracle.solve_batch(nq, np.array([N], np.int32), xg, ug, a(p), a(q_lb), a(q_ub), a(u_lb), a(u_ub),
+                                   a(q_init_lb), a(q_init_ub), a(q_fin_lb), a(q_fin_ub), nthreads=1)
+    return int(r["status"][0]), xo[0], uo[0], float(r["cost"][0])
+
+
+class FakeSolver:
+    def __init__(self):
+        self.x = self.u = None
+        self.cost = None
+
+    def set_new_time_steps(self, steps):
+        pass
+
+    def update_qp_solver_cond_N(self, N):
+        pass
+
+    def get(self, i, field):
+        return np.copy(self.x[i] if field == "x" else self.u[i])
+
+    def get_cost(self):
+        return self.cost
+
+
+class FakeOCP:
+    def __init__(self, nq):
+        s = system(nq)
+        self.nq, self.N = nq, N_START
+        self.ocp_solver = FakeSolver()
+        self.g, self.l1, self.m1 = s.g, s.l[0], s.m[0]
+        if nq == 2:
+            self.l2, self.m2 = s.l[1], s.m[1]
+
+    def OCP_solve(self, *args):
+        st, x, u, c = oracle_solve(self.nq, self.N, *args)
+        self.ocp_solver.x, self.ocp_solver.u, self.ocp_solver.cost = x, u, c
+        return st
+
+
+class FakeIntegrator:
+    def __init__(self, nq):
+        self.nq, self.T, self.xv, self.uv, self.out = nq, 1e-2, None, None, None
+
+    def set(self, field, v):
+        setattr(self, {"x": "xv", "u": "uv", "T": "T"}[field], np.array(v, dtype=np.float64))
+
+    def solve(self):
+        import oracle
+        self.out = oracle.rk4(self.nq, float(self.T), self.xv, self.uv)
+        return 0
+
+    def get(self, field):
+        return np.copy(self.out)
+
+
+class FakeSim:
+    def __init__(self, nq):
+        self.acados_integrator = FakeIntegrator(nq)
+
+
+def tolist(v):
+    if v is None:
+        return None
+    if isinstance(v, tuple):
+        return [tolist(e) for e in v]
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    if isinstance(v, list):
+        return [tolist(e) for e in v]
+    return float(v) if isinstance(v, (float, np.floating)) else v
+
+
+def main():
+    for nq, fname in ((3, "triplependulum_vboc.py"), (2, "doublependulum_vboc.py")):
+        code = extract(os.path.join(REF, fname))
+        s = system(nq)
+        ocp = FakeOCP(nq)
+        g = dict(np=np, norm=norm, math=math, ocp=ocp, sim=FakeSim(nq), q_min=s.q_min, q_max=s.q_max,
+                 v_min=-s.v_max, v_max=s.v_max, tau_max=s.u_max, dt_sym=s.dt, tol=s.tol, eps=s.eps)
+        exec(code, g)
+        ids = IDS[nq]
+        U = uniforms(np.array(ids), 3 * nq + 1, SEED)
+        out = []
+        for b, pid in enumerate(ids):
+            g["random"] = FakeRandom(U[b, :IC_DRAWS[nq]], ProblemRNG(pid, SEED))
+            ocp.N = N_START                       # N_start per problem
+            out.append(tolist(g["data_generation"](pid)))
+            print(nq, pid, "None" if out[-1] is None or out[-1][0] is None else len(out[-1] if nq == 3 else out[-1][0]),
+                  flush=True)
+        with open(os.path.join(HERE, f"driver_{nq}.json"), "w") as f:
+            json.dump({"nq": nq, "ids": ids, "N_start": N_START, "seed": SEED, "results": out}, f)
+
+
+if __name__ == "__main__":
+    main()

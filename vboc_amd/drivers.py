@@ -1,0 +1,440 @@
+"""Batched VBOC data-generation driver.
+
+The reference runs `data_generation(v)` once per problem in a process pool
+(VBOC/triplependulum_vboc.py:19-370 with the fan-out at :399-405; VBOC/doublependulum_vboc.py:19-403).
+Each call is a state machine that issues OCP solves and twin-integrator steps one at a time:
+  1. IC sampling (:32-83), Philox-keyed by problem id;
+  2. horizon extension: solve, and while the cost still drops by more than tol, re-solve with N+1
+     from the previous solution (<= 10 solves); on a failed solve perturb the cost direction and the
+     free initial positions by <= 0.01 and restart (:105-174);
+  3. the sweep f = 1..N-1 along the optimal trajectory (:205-365): while a state is on dV the
+     "unviable twin" is advanced with one RK4 step (:341-360); when the trajectory leaves dX a
+     verification OCP from x_sol[f] decides between V and dV (<= 5 solves, :232-339);
+  4. the save filter (:362-365).
+Here every problem's state machine is a Python generator that yields its next request - `Solve`
+(one OCP_solve) or `Rk4` (one twin step) - and a scheduler gathers the requests of ALL problems into
+one batched solve on the GPU (`vboc_solve_batch`) and one batched twin step (`vboc_rk4_batch`) per
+round.  The per-problem logic is a restatement of the reference's; quirk A.3 (the duplicated
+x_sol[f] sample on the unresolved branch, :333-337) is reproduced, quirk A.1 (a horizon inherited
+from the previous problem of the same worker, :23) is fixed to N_start per problem
+(VBOC/vboc.py:28 does the same).
+
+Randomness: the IC sampling draws from the problem's Philox block (ics.uniforms stream 0, the
+block `ics.data_generation_ics` uses), the perturbations of step 2 from a second per-problem stream
+(stream 2), both in the reference's call order (`random.random()` before `random.choice`).  Parity:
+tests/test_drivers.py runs the reference's own `data_generation` (AST-extracted, oracle-backed) on the
+same draws and requires identical results.
+"""
+from dataclasses import dataclass
+
+import numpy as np
+from numpy.linalg import norm
+
+from .ics import SEED, uniforms
+from .systems import system
+
+
+@dataclass
+class Solve:
+    """One OCP_solve: guesses have N rows (stage-N guess = last row) or N+1 rows."""
+    N: int
+    x_guess: np.ndarray
+    u_guess: np.ndarray
+    p: np.ndarray
+    q_lb: np.ndarray
+    q_ub: np.ndarray
+    u_lb: np.ndarray
+    u_ub: np.ndarray
+    q_init_lb: np.ndarray
+    q_init_ub: np.ndarray
+    q_fin_lb: np.ndarray
+    q_fin_ub: np.ndarray
+
+
+@dataclass
+class Rk4:
+    """One step of the twin integrator (SYM<sys>INIT.acados_integrator, T = dt)."""
+    x: np.ndarray
+    u: np.ndarray
+    T: float
+
+
+@dataclass
+class Solution:
+    status: int
+    x: np.ndarray      # [N+1, nx]
+    u: np.ndarray      # [N, nu]
+    cost: float
+
+
+class ProblemRNG:
+    """`random.random()` / `random.choice(seq)` drawn from one problem's Philox stream."""
+
+    def __init__(self, pid, seed=SEED, stream=2, block=32):
+        self.pid, self.seed, self.stream, self.block = int(pid), seed, stream, block
+        self.buf, self.pos, self.blocks = np.empty(0), 0, 0
+
+    def random(self):
+        if self.pos >= self.buf.shape[0]:
+            n = self.block * (self.blocks + 1)
+            self.buf = uniforms(np.array([self.pid]), n, self.seed, self.stream)[0, self.block * self.blocks:]
+            self.blocks += 1
+            self.pos = 0
+        u = float(self.buf[self.pos])
+        self.pos += 1
+        return u
+
+    def choice(self, seq):
+        u = self.random()
+        return seq[min(int(u * len(seq)), len(seq) - 1)]
+
+
+# ------------------------------------------------------------------------------------------------
+# per-problem state machine (a restatement of the reference's data_generation)
+# ------------------------------------------------------------------------------------------------
+def _gravity_u(sysd, q):
+    """Double-pendulum guess: gravity compensation (VBOC/doublependulum_vboc.py:84)."""
+    import math
+    return np.array([sysd.g * sysd.l[0] * (sysd.m[0] + sysd.m[1]) * math.sin(q[0]),
+                     sysd.g * sysd.l[1] * sysd.m[1] * math.sin(q[1])])
+
+
+# draws of the reference's IC sampling from the problem's first uniform block (stream 0):
+# triple :33-73 (choice, choice, random, choice, random, choice, random, random x3) -> 10,
+# double VBOC/doublependulum_vboc.py:35-60 (choice, choice, random, choice, random, random) -> 6
+IC_DRAWS = {3: 10, 2: 6}
+
+
+def data_generation_problem(nq, pid, U, rng, N_start):
+    """Generator for one problem.  U: the problem's first uniform block (ics.uniforms stream 0), drawn
+    in the reference's order; rng: its perturbation stream.  Yields Solve / Rk4 requests, receives
+    Solution / next state.  Returns the saved samples (list of rows) or None (triple); for the
+    double pendulum a 3-tuple (samples | None, ic | None, ic | None) like
+    VBOC/doublependulum_vboc.py:399,402."""
+    sysd = system(nq)
+    NX = 2 * nq
+    q_min, q_max, v_max = sysd.q_min, sysd.q_max, sysd.v_max
+    v_min, tau_max, dt_sym, tol, eps = -v_max, sysd.u_max, sysd.dt, sysd.tol, sysd.eps
+    grav = nq == 2
+    N = N_start
+    draw = iter(float(v) for v in U[:IC_DRAWS[nq]])
+    pick = lambda seq: seq[min(int(next(draw) * len(seq)), len(seq) - 1)]
+    # ---- IC sampling, the reference's scalar arithmetic (:33-83) ----
+    joint_sel = pick(list(range(nq)))
+    vel_sel = pick([-1, 1])
+    q_init_sel, q_fin_sel = (q_min, q_max) if vel_sel == -1 else (q_max, q_min)
+    ran1 = vel_sel * next(draw)
+    others = []
+    for _ in range(nq - 1):
+        sgn = pick([-1, 1])
+        others.append(sgn * next(draw))
+    norm_weights = norm(np.array([ran1] + others))
+    w = [r / norm_weights for r in [ran1] + others]
+    pw = [0.0] * nq
+    pw[joint_sel] = w[0]
+    for c, v in zip([c for c in range(nq) if c != joint_sel], w[1:]):
+        pw[c] = v
+    p = np.array(pw + [0.])
+
+    def clamp_eps(v):
+        if v > q_max - eps:
+            v = v - eps
+        if v < q_min + eps:
+            v = v + eps
+        return v
+
+    if grav:
+        joint_oth = 1 - joint_sel
+        ran = [ran1, others[0]]
+        q_init_oth = clamp_eps(q_min + next(draw) * (q_max - q_min))
+        store_ic = [vel_sel + 1 + joint_sel, ran[0], ran[1], q_init_oth]
+        qpos = [q_init_oth] * nq
+    else:
+        qpos = [clamp_eps(q_min + next(draw) * (q_max - q_min)) for _ in range(nq)]
+    q_init_lb = np.array(qpos + [v_min] * nq + [dt_sym])
+    q_init_ub = np.array(qpos + [v_max] * nq + [dt_sym])
+    sel0 = q_min + eps if q_init_sel == q_min else q_max - eps
+    q_init_lb[joint_sel] = sel0
+    q_init_ub[joint_sel] = sel0
+    q_lb = np.array([q_min] * nq + [v_min] * nq + [dt_sym])
+    q_ub = np.array([q_max] * nq + [v_max] * nq + [dt_sym])
+    u_lb = np.array([-tau_max] * nq)
+    u_ub = np.array([tau_max] * nq)
+    q_fin_lb = np.array([q_min] * nq + [0.] * nq + [dt_sym])
+    q_fin_ub = np.array([q_max] * nq + [0.] * nq + [dt_sym])
+
+    def solve(Nc, xg, ug, pc, qi_lb, qi_ub):
+        return Solve(Nc, xg, ug, pc.copy(), q_lb, q_ub, u_lb, u_ub, qi_lb.copy(), qi_ub.copy(), q_fin_lb, q_fin_ub)
+
+    def straight_guess(Nc, qpos):
+        xg = np.empty((Nc, NX + 1))
+        ug = np.empty((Nc, nq))
+        for i, tau in enumerate(np.linspace(0, 1, Nc)):
+            x_guess = np.concatenate([qpos, np.zeros(nq), [dt_sym]])
+            x_guess[joint_sel] = (1 - tau) * q_init_sel + tau * q_fin_sel
+            x_guess[joint_sel + nq] = 2 * (1 - tau) * (q_fin_sel - q_init_sel)
+            xg[i] = x_guess
+            ug[i] = _gravity_u(sysd, x_guess) if grav else np.zeros(nq)
+        return xg, ug
+
+    x_sol_guess, u_sol_guess = straight_guess(N, np.array(qpos))
+
+    # ---- horizon extension (:105-174) ----
+    cost = 1e6
+    all_ok = False
+    sol = None
+    for _ in range(10):
+        res = yield solve(N, x_sol_guess, u_sol_guess, p, q_init_lb, q_init_ub)
+        if res.status == 0:
+            cost_new = res.cost
+            if cost_new > cost - tol:
+                all_ok = True
+                sol = res
+                break
+            cost = cost_new
+            x_sol_guess = np.empty((N + 1, NX + 1))
+            u_sol_guess = np.empty((N + 1, nq))
+            x_sol_guess[:N] = res.x[:N]
+            u_sol_guess[:N] = res.u[:N]
+            x_sol_guess[N] = res.x[N]
+            u_sol_guess[N] = _gravity_u(sysd, x_sol_guess[N]) if grav else np.zeros(nq)
+            N = N + 1
+        else:
+            if grav:
+                ran[0] = ran[0] + rng.random() * rng.choice([-1, 1]) * 0.01
+                ran[1] = ran[1] + rng.random() * rng.choice([-1, 1]) * 0.01
+                norm_weights = norm(np.array(ran))
+                p = (np.array([ran[0] / norm_weights, ran[1] / norm_weights, 0.]) if joint_sel == 0
+                     else np.array([ran[1] / norm_weights, ran[0] / norm_weights, 0.]))
+                q_init_oth = q_init_oth + rng.random() * rng.choice([-1, 1]) * 0.01
+                if q_init_oth > q_max - eps:
+                    q_init_oth = q_init_oth - eps
+                if q_init_oth < q_min + eps:
+                    q_init_oth = q_init_oth + eps
+                q_init_lb[joint_oth] = q_init_oth
+                q_init_ub[joint_oth] = q_init_oth
+                store_ic = [vel_sel + 1 + joint_sel, ran[0], ran[1], q_init_oth]
+            else:
+                rans = []
+                for k in range(nq):
+                    rans.append(p[k] + rng.random() * rng.choice([-1, 1]) * 0.01)
+                norm_weights = norm(np.array(rans))
+                p = np.array([r / norm_weights for r in rans] + [0])
+                dev = rng.random() * rng.choice([-1, 1]) * 0.01
+                for j in range(nq):
+                    if j != joint_sel:
+                        val = q_init_lb[j] + dev
+                        if val > q_max - eps:
+                            val = val - eps
+                        if val < q_min + eps:
+                            val = val + eps
+                        q_init_lb[j] = val
+                        q_init_ub[j] = val
+            x_sol_guess, u_sol_guess = straight_guess(N, q_init_lb[:nq])
+            cost = 1e6
+
+    if not all_ok:
+        return (None, None, store_ic) if grav else None
+
+    # ---- sweep along the optimal trajectory (:177-365) ----
+    x_sol = np.array(sol.x[:N + 1], dtype=float)
+    u_sol = np.array(sol.u[:N], dtype=float)
+    x_sym = [None] * (N + 1)
+    valid_data = [x_sol[0][:NX].tolist()]
+    x_out = np.copy(x_sol[0][:NX])
+    for j in range(nq):
+        x_out[nq + j] = x_out[nq + j] - eps * p[j]
+
+    def vel_out(xo):
+        return any(xo[nq + j] > v_max or xo[nq + j] < v_min for j in range(nq))
+
+    def pos_at_limit(xs):
+        return any(xs[j] > q_max - eps or xs[j] < q_min + eps for j in range(nq))
+
+    is_x_at_limit = vel_out(x_out)
+    if not is_x_at_limit:
+        x_sym[0] = x_out
+    for f in range(1, N):
+        if is_x_at_limit:
+            x_out = np.copy(x_sol[f][:NX])
+            norm_vel = norm(x_out[nq:])
+            for j in range(nq):
+                x_out[nq + j] = x_out[nq + j] + eps * x_out[nq + j] / norm_vel
+            if pos_at_limit(x_sol[f]) or vel_out(x_out):
+                is_x_at_limit = True
+            else:
+                is_x_at_limit = False
+                if pos_at_limit(x_sol[f - 1]):
+                    break
+                # verification OCP from x_sol[f] (:245-339)
+                N_test = N - f
+                norm_weights = norm(np.array([x_sol[f][nq + j] for j in range(nq)]))
+                p = np.array([-x_sol[f][nq + j] / norm_weights for j in range(nq)] + [0.])
+                q_init_lb = np.concatenate([x_sol[f][:nq], [v_min] * nq, [dt_sym]])
+                q_init_ub = np.concatenate([x_sol[f][:nq], [v_max] * nq, [dt_sym]])
+                x_sol_guess = np.empty((N_test + 1, NX + 1))
+                u_sol_guess = np.empty((N_test + 1, nq))
+                for i in range(N_test):
+                    x_sol_guess[i] = x_sol[i + f]
+                    u_sol_guess[i] = u_sol[i + f]
+                x_sol_guess[N_test] = x_sol[N]
+                u_sol_guess[N_test] = _gravity_u(sysd, x_sol[N]) if grav else np.zeros(nq)
+                norm_old = norm(np.array([x_sol[f][nq:NX]]))
+                norm_bef = 0
+                ok_v = False
+                sol_v = None
+                norm_new = None
+                for _ in range(5):
+                    res = yield solve(N_test, x_sol_guess, u_sol_guess, p, q_init_lb, q_init_ub)
+                    if res.status == 0:
+                        x0_new = res.x[0]
+                        norm_new = norm(np.array([x0_new[nq:NX]]))
+                        if norm_new < norm_bef + tol:
+                            ok_v = True
+                            sol_v = res
+                            break
+                        norm_bef = norm_new
+                        x_sol_guess = np.empty((N_test + 1, NX + 1))
+                        u_sol_guess = np.empty((N_test + 1, nq))
+                        x_sol_guess[:N_test] = res.x[:N_test]
+                        u_sol_guess[:N_test] = res.u[:N_test]
+                        x_sol_guess[N_test] = res.x[N_test]
+                        u_sol_guess[N_test] = _gravity_u(sysd, x_sol_guess[N_test]) if grav else np.zeros(nq)
+                        N_test = N_test + 1
+                    else:
+                        break
+                if ok_v:
+                    if norm_new > norm_old + tol:   # the state is inside V
+                        for i in range(N - f):
+                            x_sol[i + f] = sol_v.x[i]
+                            u_sol[i + f] = sol_v.u[i]
+                        x_out = np.copy(x_sol[f][:NX])
+                        for j in range(nq):
+                            x_out[nq + j] = x_out[nq + j] + eps * x_out[nq + j] / norm_new
+                        if vel_out(x_out):
+                            is_x_at_limit = True
+                        else:
+                            is_x_at_limit = False
+                            x_sym[f] = x_out
+                    else:                            # the state is on dV
+                        is_x_at_limit = False
+                        x_out = np.copy(x_sol[f][:NX])
+                        for j in range(nq):
+                            x_out[nq + j] = x_out[nq + j] - eps * p[j]
+                        if x_out[joint_sel + nq] > v_max:
+                            x_out[joint_sel + nq] = v_max
+                        if x_out[joint_sel + nq] < v_min:
+                            x_out[joint_sel + nq] = v_min
+                        x_sym[f] = x_out
+                else:
+                    # unresolved: the reference appends x_sol[f] once per later state at a velocity
+                    # limit (quirk A.3, :333-337), then stops the sweep
+                    for r in range(f, N):
+                        if any(abs(x_sol[r][nq + j]) > v_max - eps for j in range(nq)):
+                            valid_data.append(x_sol[f][:NX].tolist())
+                    break
+        else:
+            x_out = yield Rk4(np.array(x_sym[f - 1], dtype=float), np.copy(u_sol[f - 1]), dt_sym)
+            x_sym[f] = x_out
+            is_x_at_limit = (any(x_out[j] > q_max or x_out[j] < q_min for j in range(nq)) or vel_out(x_out))
+        if (all(q_min + eps < x_sol[f][j] < q_max - eps for j in range(nq))
+                and all(abs(x_sol[f][nq + j]) > tol for j in range(nq))):
+            valid_data.append(x_sol[f][:NX].tolist())
+    return (valid_data, store_ic, None) if grav else valid_data
+
+
+# ------------------------------------------------------------------------------------------------
+# scheduler + backends
+# ------------------------------------------------------------------------------------------------
+class GpuBackend:
+    """The product backend: batched OCP solves and twin steps on the GPU (libvboc_amd)."""
+
+    def __init__(self, nq, nmax=200, device=0, **options):
+        from . import lib
+        self.lib = lib
+        self.nq = nq
+        self.nmax = nmax
+        self.solver = lib.Solver(nq, nmax, device=device, **options)
+
+    def solve(self, batch):
+        return self.solver.solve_host(batch)
+
+    def rk4(self, x, u, T):
+        return self.lib.rk4_host(self.nq, T, x, u)
+
+
+def _pack(nq, reqs, nmax):
+    """Solve requests -> one padded batch in the ics layout (rows beyond N unused)."""
+    B = len(reqs)
+    nx = 2 * nq + 1
+    Nmax = max(r.N for r in reqs)
+    if Nmax > nmax:
+        raise ValueError(f"horizon {Nmax} exceeds the solver's nmax {nmax}")
+    xg = np.zeros((B, Nmax + 1, nx))
+    ug = np.zeros((B, Nmax, nq))
+    for b, r in enumerate(reqs):
+        xg[b, :r.N] = r.x_guess[:r.N]
+        xg[b, r.N] = r.x_guess[-1]
+        ug[b, :r.N] = r.u_guess[:r.N]
+        xg[b, r.N + 1:] = xg[b, r.N]
+    stack = lambda name: np.stack([getattr(r, name) for r in reqs]).astype(np.float64)
+    return dict(N=np.array([r.N for r in reqs], dtype=np.int32), x_guess=xg, u_guess=ug, p=stack("p"),
+                lbx=stack("q_lb"), ubx=stack("q_ub"), lbu=stack("u_lb"), ubu=stack("u_ub"),
+                lbx0=stack("q_init_lb"), ubx0=stack("q_init_ub"), lbxe=stack("q_fin_lb"),
+                ubxe=stack("q_fin_ub"))
+
+
+def run_problems(nq, gens, backend, nmax=200):
+    """Drive the generators to completion: every round, all pending OCP solves go to the backend as
+    one batch and all pending twin steps as one batched call.  Returns the generators' results."""
+    results = [None] * len(gens)
+    pending = {}
+    for i, g in enumerate(gens):
+        try:
+            pending[i] = next(g)
+        except StopIteration as e:
+            results[i] = e.value
+    stats = dict(rounds=0, solves=0, rk4=0)
+    while pending:
+        stats["rounds"] += 1
+        rk = [i for i, r in pending.items() if isinstance(r, Rk4)]
+        sv = [i for i, r in pending.items() if isinstance(r, Solve)]
+        answers = {}
+        if rk:
+            x = np.stack([pending[i].x for i in rk])
+            u = np.stack([pending[i].u for i in rk])
+            T = pending[rk[0]].T
+            x1 = backend.rk4(x, u, T)
+            for k, i in enumerate(rk):
+                answers[i] = x1[k]
+            stats["rk4"] += len(rk)
+        if sv and not rk:
+            # solves are the expensive part: batch them only once no twin steps are outstanding, so
+            # problems that are sweeping catch up and join the next solve batch
+            reqs = [pending[i] for i in sv]
+            out = backend.solve(_pack(nq, reqs, nmax))
+            for k, i in enumerate(sv):
+                Nk = reqs[k].N
+                answers[i] = Solution(int(out["status"][k]), out["x"][k, :Nk + 1], out["u"][k, :Nk],
+                                      float(out["cost"][k]))
+            stats["solves"] += len(sv)
+        for i, a in answers.items():
+            try:
+                pending[i] = gens[i].send(a)
+            except StopIteration as e:
+                results[i] = e.value
+                del pending[i]
+    return results, stats
+
+
+def data_generation_batch(nq, ids, backend, N_start=None, seed=SEED):
+    """`data_generation(v)` for every problem id in `ids`, batched.  Returns
+    (results, stats): results[i] is what the reference's call returns for problem ids[i]
+    (triple: list of samples or None; double: 3-tuple)."""
+    sysd = system(nq)
+    N_start = N_start or sysd.N
+    ids = np.asarray(ids)
+    U = uniforms(ids, 3 * nq + 1, seed)
+    gens = [data_generation_problem(nq, int(pid), U[b], ProblemRNG(int(pid), seed), N_start)
+            for b, pid in enumerate(ids)]
+    return run_problems(nq, gens, backend, nmax=getattr(backend, "nmax", 200))
