@@ -13,7 +13,16 @@ The fixture records each problem's return value.  tests/test_drivers.py runs vbo
 same oracle backend and must reproduce it exactly: the pair pins the batched driver's restatement to
 the reference's own state machine (given identical solver results).
 
-Usage: python tests/golden/make_driver_golden.py  ->  tests/golden/driver_{2,3}.json
+The held-out driver `testing` (triplependulum_testdata.py:9-125, doublependulum_testdata.py:9-121,
+pendulum_testdata.py:7-53) drives `ocp.ocp_solver` directly (reset / set / constraints_set / solve /
+get / get_cost / set_new_time_steps).  It is extracted the same way and run against the product's
+drop-in classes (vboc_amd.ocp.OCP<sys>INIT / OCPpendulum) with the oracle injected as their solver
+(vboc_amd.ocp.use_backend): the fixture then pins the batched `testing_batch` to the reference's state
+machine AND the drop-in classes' mapping of the ACADOS calls onto the solver.  `random` serves the
+problem's stream-1 block (ics.heldout_ics) and then the restart stream (drivers.TEST_STREAM).
+
+Usage: python tests/golden/make_driver_golden.py [dg|test]
+  ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json
 """
 import ast
 import json
@@ -30,11 +39,13 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 REF = "/root/reference/VBOC"
 
-from vboc_amd.drivers import IC_DRAWS, ProblemRNG  # noqa: E402
+from vboc_amd.drivers import IC_DRAWS, TEST_DRAWS, TEST_STREAM, ProblemRNG  # noqa: E402
 from vboc_amd.ics import SEED, uniforms  # noqa: E402
 from vboc_amd.systems import system  # noqa: E402
 
 IDS = {3: list(range(0, 12)), 2: list(range(100, 124))}
+TEST_IDS = {3: list(range(0, 64)), 2: list(range(0, 64)), 1: list(range(0, 128))}
+FAIL_MOD = 3   # oracle_backend.forced_failure: about a third of the solves fail -> restarts exercised
 N_START = 100
 
 
@@ -159,5 +170,35 @@ def main():
             json.dump({"nq": nq, "ids": ids, "N_start": N_START, "seed": SEED, "results": out}, f)
 
 
+def main_testing():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_backend import OracleOcpBackend
+    from vboc_amd import ocp as dropin
+    dropin.use_backend(OracleOcpBackend(FAIL_MOD))
+    for nq, fname, cls in ((3, "triplependulum_testdata.py", "OCPtriplependulumINIT"),
+                           (2, "doublependulum_testdata.py", "OCPdoublependulumINIT"),
+                           (1, "pendulum_testdata.py", "OCPpendulum")):
+        code = extract(os.path.join(os.path.dirname(REF), fname), "testing")
+        ocp = getattr(dropin, cls)()
+        s = system(nq)
+        g = dict(np=np, norm=norm, math=math, ocp=ocp, v_max=ocp.dthetamax, v_min=-ocp.dthetamax,
+                 q_max=ocp.thetamax, q_min=ocp.thetamin, tau_max=s.u_max)
+        exec(code, g)
+        ids = TEST_IDS[nq]
+        U = uniforms(np.array(ids), 3 * nq + 1, SEED, stream=1)
+        out = []
+        for b, pid in enumerate(ids):
+            g["random"] = FakeRandom(U[b, :TEST_DRAWS[nq]], ProblemRNG(pid, SEED, stream=TEST_STREAM))
+            out.append(tolist(g["testing"](pid)))
+            print(nq, pid, out[-1], flush=True)
+        with open(os.path.join(HERE, f"testing_{nq}.json"), "w") as f:
+            json.dump({"nq": nq, "ids": ids, "N_start": ocp.N, "seed": SEED, "fail_mod": FAIL_MOD,
+                       "results": out}, f)
+
+
 if __name__ == "__main__":
-    main()
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("dg", "all"):
+        main()
+    if what in ("test", "all"):
+        main_testing()

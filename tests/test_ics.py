@@ -68,4 +68,10 @@ def test_heldout_law(nq):
         np.testing.assert_allclose(np.linalg.norm(b["p"][:, :nq], axis=1), 1.0, rtol=1e-14)
     # constant guess at the initial position, at rest (:37-38)
     np.testing.assert_array_equal(b["x_guess"][:, :, :nq], np.repeat(q0[:, None, :], sysd.N + 1, 1))
-    assert np.all(b["x_guess"][:, :, nq:2 * nq] == 0) and np.all(b["u_guess"] == 0)
+    assert np.all(b["x_guess"][:, :, nq:2 * nq] == 0)
+    if nq == 2:   # gravity compensation at q0 (doublependulum_testdata.py:37)
+        np.testing.assert_allclose(b["u_guess"][:, 0, 1], sysd.g * sysd.l[1] * sysd.m[1] * np.sin(q0[:, 1]),
+                                   rtol=1e-15)
+        assert np.all(b["u_guess"] == b["u_guess"][:, :1])
+    else:
+        assert np.all(b["u_guess"] == 0)

@@ -1,4 +1,5 @@
-"""Batched VBOC data-generation driver.
+"""Batched VBOC drivers: data generation and the held-out test set
+(row a10, `testing_batch`).
 
 The reference runs `data_generation(v)` once per problem in a process pool
 (VBOC/triplependulum_vboc.py:19-370 with the fan-out at :399-405; VBOC/doublependulum_vboc.py:19-403).
@@ -344,6 +345,99 @@ def data_generation_problem(nq, pid, U, rng, N_start):
 
 
 # ------------------------------------------------------------------------------------------------
+# held-out test-set state machine (a restatement of the reference's `testing`)
+# ------------------------------------------------------------------------------------------------
+# draws of `testing` from the problem's first uniform block (ics.uniforms stream 1, the block
+# ics.heldout_ics uses): (choice, random) per joint, then one position per joint; the pendulum draws
+# choice, then its position (triplependulum_testdata.py:19-28, doublependulum_testdata.py:19-27,
+# pendulum_testdata.py:14-18)
+TEST_DRAWS = {3: 9, 2: 6, 1: 2}
+TEST_STREAM = 3          # the restart perturbations of `testing` (stream 2 is data_generation's)
+MAX_TEST_RESTARTS = 100  # the reference retries forever (`while True`, :41); a problem still failing
+                         # after this many perturbed restarts returns None
+
+
+def testing_problem(nq, pid, U, rng, N_start, max_restarts=MAX_TEST_RESTARTS):
+    """Generator for one held-out problem (triplependulum_testdata.py:9-125, the double
+    doublependulum_testdata.py:9-121; the pendulum pendulum_testdata.py:7-53 solves once).
+    U: the problem's first uniform block (stream 1), drawn in the reference's order; rng: its restart
+    stream.  Yields Solve requests and returns x_0[:2nq] of the accepted solution (None if the
+    pendulum's single solve fails or the restart cap is hit)."""
+    sysd = system(nq)
+    NX = 2 * nq
+    q_min, q_max, v_max = sysd.q_min, sysd.q_max, sysd.v_max
+    v_min, tau_max, dt_sym = -v_max, sysd.u_max, sysd.dt
+    grav = nq == 2
+    draw = iter(float(v) for v in U[:TEST_DRAWS[nq]])
+    pick = lambda seq: seq[min(int(next(draw) * len(seq)), len(seq) - 1)]
+    q_lb = np.array([q_min] * nq + [v_min] * nq + [dt_sym])
+    q_ub = np.array([q_max] * nq + [v_max] * nq + [dt_sym])
+    u_lb = np.array([-tau_max] * nq)
+    u_ub = np.array([tau_max] * nq)
+    q_fin_lb = np.array([q_min] * nq + [0.] * nq + [dt_sym])
+    q_fin_ub = np.array([q_max] * nq + [0.] * nq + [dt_sym])
+
+    if nq == 1:
+        ran = pick([-1, 1])
+        p = np.array([ran, 0.])
+        q_init = q_min + next(draw) * (q_max - q_min)
+        x0b = np.array([q_init, v_min, dt_sym]), np.array([q_init, v_max, dt_sym])
+        xg = np.full((N_start, 3), np.array([q_init, 0., dt_sym]))
+        res = yield Solve(N_start, xg, np.zeros((N_start, 1)), p, q_lb, q_ub, u_lb, u_ub, x0b[0], x0b[1],
+                          q_fin_lb, q_fin_ub)
+        return res.x[0][:2].copy() if res.status == 0 else None
+
+    rans = []
+    for _ in range(nq):
+        c = pick([-1, 1])
+        rans.append(c * next(draw))
+
+    def direction(rs):
+        nw = norm(np.array(rs))
+        return np.array([r / nw for r in rs] + [0.])
+
+    def start(qs):
+        xg = np.full((N_start, NX + 1), np.array(qs + [0.] * nq + [dt_sym]))
+        ug = np.full((N_start, nq), _gravity_u(sysd, qs) if grav else np.zeros(nq))
+        return (np.array(qs + [v_min] * nq + [dt_sym]), np.array(qs + [v_max] * nq + [dt_sym]), xg, ug)
+
+    p = direction(rans)
+    qs = [q_min + next(draw) * (q_max - q_min) for _ in range(nq)]
+    q_init_lb, q_init_ub, x_sol_guess, u_sol_guess = start(qs)
+    fmt, dec = ("{:.4f}", 1e-4) if grav else ("{:.3f}", 1e-3)   # doublependulum_testdata.py:80 / :82
+    N = N_start
+    cost = 1e6
+    restarts = 0
+    while True:
+        res = yield Solve(N, x_sol_guess, u_sol_guess, p, q_lb, q_ub, u_lb, u_ub, q_init_lb, q_init_ub,
+                          q_fin_lb, q_fin_ub)
+        if res.status == 0:
+            cost_new = res.cost
+            if cost_new > float(fmt.format(cost)) - dec:
+                return res.x[0][:NX].copy()
+            cost = cost_new
+            x_sol_guess = np.empty((N + 1, NX + 1))
+            u_sol_guess = np.empty((N + 1, nq))
+            x_sol_guess[:N] = res.x[:N]
+            u_sol_guess[:N] = res.u[:N]
+            x_sol_guess[N] = res.x[N]
+            u_sol_guess[N] = _gravity_u(sysd, x_sol_guess[N]) if grav else np.zeros(nq)
+            N = N + 1
+        else:
+            restarts += 1
+            if restarts > max_restarts:
+                return None
+            N = N_start
+            for j in range(nq):
+                rans[j] = rans[j] + rng.random() * rng.choice([-1, 1]) * 0.01
+            p = direction(rans)
+            for j in range(nq):
+                qs[j] = qs[j] + rng.random() * rng.choice([-1, 1]) * 0.01
+            q_init_lb, q_init_ub, x_sol_guess, u_sol_guess = start(qs)
+            cost = 1e6
+
+
+# ------------------------------------------------------------------------------------------------
 # scheduler + backends
 # ------------------------------------------------------------------------------------------------
 class GpuBackend:
@@ -438,3 +532,24 @@ def data_generation_batch(nq, ids, backend, N_start=None, seed=SEED):
     gens = [data_generation_problem(nq, int(pid), U[b], ProblemRNG(int(pid), seed), N_start)
             for b, pid in enumerate(ids)]
     return run_problems(nq, gens, backend, nmax=getattr(backend, "nmax", 200))
+
+
+def testing_batch(nq, ids, backend, N_start=None, seed=SEED, max_restarts=MAX_TEST_RESTARTS):
+    """`testing(v)` for every problem id in `ids`, batched.  Returns (results, stats):
+    results[i] is x_0[:2nq] of problem ids[i] (or None)."""
+    sysd = system(nq)
+    N_start = N_start or sysd.N
+    ids = np.asarray(ids)
+    U = uniforms(ids, 3 * nq + 1, seed, stream=1)
+    gens = [testing_problem(nq, int(pid), U[b], ProblemRNG(int(pid), seed, stream=TEST_STREAM), N_start,
+                            max_restarts) for b, pid in enumerate(ids)]
+    return run_problems(nq, gens, backend, nmax=getattr(backend, "nmax", 200))
+
+
+def heldout_set(nq, results):
+    """The saved held-out array: np.array(data) (triplependulum_testdata.py:144); the pendulum drops the
+    failed problems first (pendulum_testdata.py:68)."""
+    rows = [r for r in results if r is not None]
+    if nq > 1 and len(rows) != len(results):
+        raise ValueError("a problem hit the restart cap; the reference would still be retrying it")
+    return np.array(rows, dtype=np.float64).reshape(len(rows), 2 * nq)

@@ -57,6 +57,12 @@ def uniforms(ids, n, seed=SEED, stream=0):
     return u.reshape(ids.shape[0], -1)[:, :n]
 
 
+def _row_norms(r):
+    """Per-row 2-norms computed as the reference does, numpy.linalg.norm of each 1-D vector
+    (triplependulum_vboc.py:48): the axis=1 reduction rounds differently in the last bit."""
+    return np.array([[np.linalg.norm(row)] for row in r]).reshape(r.shape[0], 1)
+
+
 def _choice(u, options):
     options = np.asarray(options)
     return options[np.minimum((u * len(options)).astype(np.int64), len(options) - 1)]
@@ -83,7 +89,7 @@ def data_generation_ics(nq, ids, N=None, seed=SEED):
     for j in range(1, nq):
         rans.append(_choice(U[:, 2 + 2 * j - 1], [-1.0, 1.0]) * U[:, 2 + 2 * j])
     rans = np.stack(rans, axis=1)
-    rans /= np.linalg.norm(rans, axis=1, keepdims=True)
+    rans /= _row_norms(rans)
     p = np.zeros((B, nq + 1))
     # joint_sel == j: p = [others..., ran1 at position j] following :49-54 / double :45-50
     for j in range(nq):
@@ -93,10 +99,12 @@ def data_generation_ics(nq, ids, N=None, seed=SEED):
         p[m, j] = rans[m, 0]
         for c, o in zip(cols, order):
             p[m, c] = rans[m, o]
-    # positions of the other joints ~U, clamped by eps (:57-73)
+    # positions of the other joints ~U, clamped by eps (:57-73): the triple draws one per joint
+    # (draws 8-10), the double one for the other joint (its 6th draw, VBOC/doublependulum_vboc.py:56)
     qi = np.zeros((B, nq))
     for j in range(nq):
-        v = q_min + U[:, 2 * nq + 1 + j] * (q_max - q_min)
+        col = 2 * nq + 1 + j if nq != 2 else 2 * nq + 1
+        v = q_min + U[:, col] * (q_max - q_min)
         v = np.where(v > q_max - eps, v - eps, v)
         v = np.where(v < q_min + eps, v + eps, v)
         qi[:, j] = v
@@ -137,8 +145,10 @@ def heldout_ics(nq, ids, N=None, seed=SEED):
     else:
         r = np.stack([_choice(U[:, 2 * j], [-1.0, 1.0]) * U[:, 2 * j + 1] for j in range(nq)], axis=1)
         p = np.zeros((B, nq + 1))
-        p[:, :nq] = r / np.linalg.norm(r, axis=1, keepdims=True)
-    qi = sysd.q_min + U[:, 2 * nq: 3 * nq] * (sysd.q_max - sysd.q_min)
+        p[:, :nq] = r / _row_norms(r)
+    # draw order of the reference: (choice, random) per joint, then one position per joint; the
+    # pendulum draws choice, then its position (pendulum_testdata.py:14-18)
+    qi = sysd.q_min + (U[:, 1:2] if nq == 1 else U[:, 2 * nq: 3 * nq]) * (sysd.q_max - sysd.q_min)
     dt = sysd.dt
     lbx0 = np.concatenate([qi, np.full((B, nq), -sysd.v_max), np.full((B, 1), dt)], axis=1)
     ubx0 = np.concatenate([qi, np.full((B, nq), sysd.v_max), np.full((B, 1), dt)], axis=1)
@@ -146,6 +156,12 @@ def heldout_ics(nq, ids, N=None, seed=SEED):
     xg[:, :, :nq] = qi[:, None, :]
     xg[:, :, 2 * nq] = dt
     ug = np.zeros((B, N, nq))
+    if sysd.gravity_guess:
+        # double pendulum: constant gravity-compensation guess (doublependulum_testdata.py:37), with
+        # the reference's scalar math.sin
+        import math
+        ug[:, :, 0] = (sysd.g * sysd.l[0] * (sysd.m[0] + sysd.m[1]) * np.array([math.sin(q) for q in qi[:, 0]]))[:, None]
+        ug[:, :, 1] = (sysd.g * sysd.l[1] * sysd.m[1] * np.array([math.sin(q) for q in qi[:, 1]]))[:, None]
     return _bounds(sysd, B, N, xg, ug, p, lbx0, ubx0)
 
 

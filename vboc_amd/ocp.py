@@ -15,7 +15,7 @@ update_qp_solver_cond_N - SURVEY.md section 8b).  `SYM<sys>INIT().acados_integra
 set('x'|'u'|'T'), solve(), get('x') of AcadosSimSolver.
 
 Each solve() is a batch-of-one call of the C ABI (vboc_solve_batch_host); the batched drivers
-in vboc_amd.vboc call the library directly with whole batches.  Structures outside what the
+(vboc_amd.drivers) call the library directly with whole batches.  Structures outside what the
 boundary-OCP solver implements raise NotImplementedError (loudly - no silent fallback).
 """
 from types import SimpleNamespace
@@ -26,10 +26,21 @@ from . import lib
 from .systems import system
 
 _SOLVERS = {}
+_BACKEND = None
+
+
+def use_backend(backend):
+    """Test hook: route subsequently created solvers / integrators through `backend` (an object with
+    solve_host(batch) -> dict and rk4(nq, T, x, u) -> x1), e.g. the CPU oracle in tests/.  None (the
+    default) = the HIP library; there is no automatic fallback."""
+    global _BACKEND
+    _BACKEND = backend
 
 
 def _shared_solver(nq, nmax):
     """One HIP handle per (nq, nmax) per process (the reference builds one solver per process)."""
+    if _BACKEND is not None:
+        return _BACKEND
     key = (nq, nmax)
     if key not in _SOLVERS:
         _SOLVERS[key] = lib.Solver(nq, nmax, slots=256)
@@ -336,7 +347,10 @@ class _Integrator:
             raise ValueError(f"integrator set: unsupported field '{field}'")
 
     def solve(self):
-        self.xo = lib.rk4_host(self.nq, self.T, self.x[None], self.u[None])[0]
+        if _BACKEND is not None:
+            self.xo = np.asarray(_BACKEND.rk4(self.nq, self.T, self.x, self.u), dtype=float)
+        else:
+            self.xo = lib.rk4_host(self.nq, self.T, self.x[None], self.u[None])[0]
         return 0
 
     def get(self, field):
