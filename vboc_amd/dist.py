@@ -29,3 +29,25 @@ def gather_boundary_states(x0, group=None):
     out = torch.empty((world * x0.shape[0],) + tuple(x0.shape[1:]), dtype=x0.dtype, device=x0.device)
     dist.all_gather_into_tensor(out, x0, group=group)   # concatenated along dim 0 (RCCL and gloo)
     return out
+
+
+def gather_samples(rows, group=None):
+    """All-gather variable-length per-rank sample blocks rows [n_r, d] (float64) into
+    [sum n_r, d] ordered by rank: one all-gather of the counts, then one all-gather of
+    the blocks padded to max n_r (an all-gatherv emulation; RCCL over xGMI on GPU, gloo on CPU)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rows = rows.contiguous()
+    n = torch.tensor([rows.shape[0]], dtype=torch.int64, device=rows.device)
+    counts = torch.empty(world, dtype=torch.int64, device=rows.device)
+    dist.all_gather_into_tensor(counts, n, group=group)
+    counts = counts.tolist()
+    cap = max(counts)
+    d = rows.shape[1]
+    pad = torch.zeros((cap, d), dtype=rows.dtype, device=rows.device)
+    pad[:rows.shape[0]] = rows
+    out = torch.empty((world * cap, d), dtype=rows.dtype, device=rows.device)
+    if cap:
+        dist.all_gather_into_tensor(out, pad, group=group)
+    return torch.cat([out[r * cap: r * cap + c] for r, c in enumerate(counts)])

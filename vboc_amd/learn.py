@@ -1,0 +1,225 @@
+"""Boundary-velocity regressor of VBOC: the NN fit on the generated boundary states and its RMSE on
+the held-out set.
+
+Reference: my_nn.py:20-34 (NeuralNetDIR), VBOC/triplependulum_vboc.py:407-491 (first fit + RMSE),
+:493-566 (refits as data arrives), the double VBOC/doublependulum_vboc.py:440-560 and the pendulum
+VBOC/pendulum_vboc.py:35-41,228-292.
+
+Model input = [ (q - mean) / std , qdot / |qdot| ], target = |qdot|  (:55-65); mean/std are the
+scalar mean and (unbiased) std over ALL position entries, computed in float32 as the reference does
+with torch.tensor(X[:, :nq].tolist()) (:50).  Training: Adam(lr 1e-3) on MSE, minibatch 4096 drawn
+without replacement, EMA of the loss `val = 0.95 val + 0.05 loss` starting at max|qdot|; stop when
+val <= 1e-3 or after it_max = 10 * int(n_0 * 100 / 4096) steps (:67-99), n_0 = size of the first
+dataset (B and it_max are fixed once, :68-69).  Refits sample half of each minibatch from the old
+rows and half from the new ones (:156-166).
+
+MI355X design (the NN stays PyTorch-ROCm): the reference rebuilds each minibatch on
+the host from Python lists (:164-165) and syncs on loss.item() every step.  Here the feature matrix
+lives in HBM as float32, minibatch indices are drawn on the device (a uniform random k-subset = the
+top-k of n uniform keys), and one training step - sampling, forward, backward, Adam, the EMA and the
+stop test - is captured once in a HIP graph and replayed.  The stop test is evaluated on the device
+and gates the update (a step taken after the stop condition is a no-op), so the host only polls the
+`active` flag every `poll` steps while the iteration count and the final model are exactly those of
+the reference's per-step loop.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+
+# ------------------------------------------------------------------------------------------------
+# models (my_nn.py): same module structure, so state_dicts load in the reference's scripts
+# ------------------------------------------------------------------------------------------------
+class NeuralNetDIR(nn.Module):
+    """my_nn.py:20-34: Linear-ReLU-Linear-ReLU-Linear-ReLU (non-negative output = |qdot|)."""
+
+    def __init__(self, input_size, hidden_size, output_size):
+        super().__init__()
+        self.linear_relu_stack = nn.Sequential(
+            nn.Linear(input_size, hidden_size), nn.ReLU(),
+            nn.Linear(hidden_size, hidden_size), nn.ReLU(),
+            nn.Linear(hidden_size, output_size), nn.ReLU())
+
+    def forward(self, x):
+        return self.linear_relu_stack(x)
+
+
+class NeuralNetCLS(nn.Module):
+    """my_nn.py:4-18 (the AL / HJR classifiers' architecture; loaded by the comparison scripts)."""
+
+    def __init__(self, input_size, hidden_size, output_size):
+        super().__init__()
+        self.linear_relu_stack = nn.Sequential(
+            nn.Linear(input_size, hidden_size), nn.ReLU(),
+            nn.Linear(hidden_size, hidden_size), nn.ReLU(),
+            nn.Linear(hidden_size, output_size))
+
+    def forward(self, x):
+        return self.linear_relu_stack(x)
+
+
+# layer sizes per system: triple 6-500-1 (:38-41), double 4-300-1 (doublependulum_vboc.py:448-451),
+# pendulum 2-100-1 (pendulum_vboc.py:35-37), minibatch 4096 / 4096 / 64
+HIDDEN = {3: 500, 2: 300, 1: 100}
+MINIBATCH = {3: 4096, 2: 4096, 1: 64}
+
+
+# ------------------------------------------------------------------------------------------------
+# data transforms
+# ------------------------------------------------------------------------------------------------
+def position_stats(X, nq):
+    """(mean, std) of all position entries X[:, :nq], in float32 like
+    torch.mean(torch.tensor(X[:, :nq].tolist())) (:50); returned as Python floats."""
+    t = torch.from_numpy(np.ascontiguousarray(X[:, :nq], dtype=np.float64)).to(torch.float32)
+    return torch.mean(t).item(), torch.std(t).item()
+
+
+def dir_features(X, mean, std, nq):
+    """[n, 2nq+1] float64: normalised positions, velocity direction (0 if qdot = 0), |qdot|
+    (:55-65).  |qdot| is the sequential sum of squares; the reference's per-row numpy.linalg.norm
+    can differ in the last bit of the float64 value, never after the cast to float32 the model sees."""
+    X = np.asarray(X, dtype=np.float64)
+    out = np.zeros((X.shape[0], 2 * nq + 1))
+    out[:, :nq] = (X[:, :nq] - mean) / std
+    V = X[:, nq:2 * nq]
+    s = V[:, 0] * V[:, 0]
+    for j in range(1, nq):
+        s = s + V[:, j] * V[:, j]
+    vn = np.sqrt(s)
+    nz = vn != 0
+    out[nz, nq:2 * nq] = V[nz] / vn[nz, None]
+    out[:, 2 * nq] = vn
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# trainer
+# ------------------------------------------------------------------------------------------------
+class DirTrainer:
+    """Adam/MSE fit of NeuralNetDIR with the reference's stop rule, device-resident.
+
+    fit(F, n_new) trains on the feature matrix F ([n, 2nq+1], float) - the whole set for the first
+    fit (:77-99), or old rows F[:n-n_new] and new rows F[n-n_new:] half-and-half for a refit
+    (:156-184)."""
+
+    def __init__(self, nq, device="cpu", hidden=None, minibatch=None, lr=1e-3, beta=0.95, stop_val=1e-3,
+                 seed=0, graphs=None, poll=64):
+        self.nq = nq
+        self.nin = 2 * nq
+        self.device = torch.device(device)
+        torch.manual_seed(seed)
+        self.model = NeuralNetDIR(self.nin, hidden or HIDDEN[nq], 1).to(self.device)
+        self.k = minibatch or MINIBATCH[nq]
+        self.lr, self.beta, self.stop_val = lr, beta, stop_val
+        self.b1, self.b2, self.eps = 0.9, 0.999, 1e-8       # torch.optim.Adam defaults (:44)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed)
+        self.params = [p for p in self.model.parameters()]
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+        self.step_t = torch.zeros((), device=self.device)   # Adam step count (device-side)
+        self.graphs = (self.device.type == "cuda") if graphs is None else graphs
+        self.poll = poll
+        self.it_max = None
+        self.total_steps = 0
+
+    # -- one gated step, written with device tensors only (capturable) ---------------------------------
+    def _sample(self, lo, hi, k):
+        keys = torch.rand(hi - lo, device=self.device, generator=self.gen)
+        return torch.topk(keys, k, sorted=False).indices + lo
+
+    def _step(self, F, X, y, n, n_new):
+        if n_new:
+            idx = torch.cat([self._sample(0, n - n_new, self.k // 2), self._sample(n - n_new, n, self.k // 2)])
+        else:
+            idx = self._sample(0, n, self.k)
+        xb = X.index_select(0, idx)
+        yb = y.index_select(0, idx)
+        active = (self.val > self.stop_val) & (self.it < self.it_lim)
+        a = active.to(torch.float32)
+        for p in self.params:
+            p.grad = None
+        loss = torch.mean((self.model(xb) - yb) ** 2)
+        loss.backward()
+        grads = [p.grad for p in self.params]
+        with torch.no_grad():
+            # Adam, torch.optim.Adam's arithmetic (single-tensor path), every update scaled by the gate
+            self.step_t.add_(a)
+            w1 = a * (1 - self.b1)
+            w2 = a * (1 - self.b2)
+            for m, v, g in zip(self.m, self.v, grads):
+                m.lerp_(g, w1)
+                v.mul_(1 - w2).addcmul_(g * w2, g)
+            t = torch.clamp(self.step_t, min=1.0)
+            bc1 = 1 - torch.pow(self.b1, t)
+            bc2s = torch.sqrt(1 - torch.pow(self.b2, t))
+            step = -(a * self.lr) / bc1
+            for p, m, v in zip(self.params, self.m, self.v):
+                p.addcdiv_(m * step, v.sqrt().div_(bc2s).add_(self.eps))
+            # the reference's EMA and counter (:95-96), gated as well
+            self.val.copy_(torch.where(active, self.beta * self.val + (1 - self.beta) * loss.detach(), self.val))
+            self.it.add_(active.to(self.it.dtype))
+            self.active.copy_(active)
+
+    def fit(self, F, n_new=0, it_max=None):
+        """Train until val <= stop_val or it_max steps.  Returns dict(iterations, val)."""
+        F = torch.as_tensor(np.asarray(F), dtype=torch.float32).to(self.device) if not torch.is_tensor(F) \
+            else F.to(self.device, torch.float32)
+        n = F.shape[0]
+        if self.it_max is None:
+            B = int(n * 100 / self.k)   # :68, from the first dataset only
+            self.it_max = B * 10
+        it_max = it_max or self.it_max
+        if n_new and (n_new < self.k // 2 or n - n_new < self.k // 2):
+            raise ValueError("a refit needs at least minibatch/2 old and new rows")
+        if not n_new and n < self.k:
+            raise ValueError(f"need at least {self.k} rows (random.sample of a minibatch)")
+        X = F[:, :self.nin].contiguous()
+        y = F[:, self.nin:self.nin + 1].contiguous()
+        self.val = torch.max(F[:, self.nin]).reshape(())     # :73 val = max |qdot|
+        self.it = torch.ones((), dtype=torch.int64, device=self.device)
+        self.it_lim = torch.tensor(it_max, dtype=torch.int64, device=self.device)
+        self.active = torch.ones((), dtype=torch.bool, device=self.device)
+        steps = 0
+        if self.graphs:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):                      # warm-up outside capture (allocations)
+                self._step(F, X, y, n, n_new)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            steps += 1
+            g = torch.cuda.CUDAGraph()
+            g.register_generator_state(self.gen)             # replays advance the sampler's Philox offset
+            for p in self.params:
+                p.grad = None
+            with torch.cuda.graph(g):
+                self._step(F, X, y, n, n_new)
+            while bool(self.active.item()):
+                for _ in range(self.poll):
+                    g.replay()
+                steps += self.poll
+            del g
+        else:
+            while bool(self.active.item()):
+                self._step(F, X, y, n, n_new)
+                steps += 1
+        self.total_steps += steps
+        return dict(iterations=int(self.it.item()) - 1, val=float(self.val.item()), launched=steps)
+
+    @torch.no_grad()
+    def predict(self, Xin, batch=1 << 15):
+        """Model output for [n, 2nq] inputs in minibatches of 2^15 (VBOC/vboc.py:532-541)."""
+        X = torch.as_tensor(np.asarray(Xin), dtype=torch.float32).to(self.device) if not torch.is_tensor(Xin) \
+            else Xin.to(self.device, torch.float32)
+        return torch.cat([self.model(X[i:i + batch]) for i in range(0, X.shape[0], batch)]) if X.shape[0] else \
+            torch.zeros((0, 1), device=self.device)
+
+    @torch.no_grad()
+    def rmse(self, F):
+        """sqrt(MSELoss(model(F[:, :2nq]), F[:, 2nq:])) (:117-120)."""
+        F = torch.as_tensor(np.asarray(F), dtype=torch.float32).to(self.device) if not torch.is_tensor(F) \
+            else F.to(self.device, torch.float32)
+        out = self.predict(F[:, :self.nin])
+        return math.sqrt(torch.mean((out - F[:, self.nin:self.nin + 1]) ** 2).item())

@@ -1,0 +1,151 @@
+"""The VBOC main loop: batched boundary data generation, NN fit, RMSE on the held-out set, repeated
+until the time budget is spent, and the reference's artefact files.
+
+Reference: VBOC/triplependulum_vboc.py:372-585 (the double VBOC/doublependulum_vboc.py:404-620).
+  iteration 0: data_generation over num_prob problems (:399-405), X_save = all saved rows (:404-405),
+               mean/std (:50), first fit (:77-99), times/rmse (:102-120);
+  iteration i: more data (:127-134), X_save grows, refit half old / half new (:152-184), times/rmse
+               appended (:187-197), until stop_time (:122);
+  artefacts:   times_/rmse_/data_<n>dof_vboc.npy, mean_/std_<n>dof_vboc (torch.save of a float),
+               model_<n>dof_vboc (state_dict) (:50-52, :204-215).
+The held-out set comes from `drivers.testing_batch` (triplependulum_testdata.py, saved as
+data<n>_test.npy, :145).
+
+Quirk kept (documented in DESIGN.md): the triple driver recomputes the refit's "new" feature rows
+from the WHOLE X_save (:140-150) rather than from X_new as the double does (doublependulum :138-146),
+so old rows are duplicated into the new half; `triple_refit_quirk=False` uses X_new.
+
+Problem ids: iteration i solves ids [i*num_prob, (i+1)*num_prob) (the reference's forked workers draw
+fresh unseeded ICs every iteration); with torch.distributed initialised, each rank solves a
+contiguous shard and the saved rows are all-gathered (vboc_amd.dist.gather_samples); rank 0 trains.
+"""
+import os
+import time
+
+import numpy as np
+
+from .drivers import data_generation_batch, heldout_set, testing_batch
+from .ics import SEED
+from .learn import DirTrainer, dir_features, position_stats
+
+
+def samples_array(nq, results):
+    """Saved rows of one data-generation round: flatten the non-None sample lists (:404-405; the
+    double unpacks its 3-tuples first, doublependulum_vboc.py:436-438)."""
+    traj = results if nq != 2 else [r[0] for r in results]
+    rows = [row for t in traj if t is not None for row in t]
+    return np.array(rows, dtype=np.float64).reshape(len(rows), 2 * nq)
+
+
+def save_artifacts(out_dir, nq, X_save, mean, std, model, times, rmse):
+    """The reference's file names and formats (VBOC/triplependulum_vboc.py:51-52,204-215)."""
+    import torch
+    os.makedirs(out_dir, exist_ok=True)
+    tag = f"{nq}dof_vboc"
+    np.save(os.path.join(out_dir, f"times_{tag}.npy"), np.asarray(times))
+    np.save(os.path.join(out_dir, f"rmse_{tag}.npy"), np.asarray(rmse))
+    np.save(os.path.join(out_dir, f"data_{tag}.npy"), np.asarray(X_save))
+    torch.save(mean, os.path.join(out_dir, f"mean_{tag}"))
+    torch.save(std, os.path.join(out_dir, f"std_{tag}"))
+    torch.save({k: v.detach().cpu() for k, v in model.state_dict().items()}, os.path.join(out_dir, f"model_{tag}"))
+
+
+def load_artifacts(out_dir, nq, device="cpu"):
+    """Read the artefacts back the way triplependulum_comparison.py:31-36 does (weights_only loads)."""
+    import torch
+    from .learn import NeuralNetDIR
+    tag = f"{nq}dof_vboc"
+    sd = torch.load(os.path.join(out_dir, f"model_{tag}"), weights_only=True)
+    model = NeuralNetDIR(2 * nq, sd["linear_relu_stack.0.weight"].shape[0], 1).to(device)
+    model.load_state_dict(sd)
+    return dict(model=model, data=np.load(os.path.join(out_dir, f"data_{tag}.npy")),
+                mean=torch.load(os.path.join(out_dir, f"mean_{tag}"), weights_only=True),
+                std=torch.load(os.path.join(out_dir, f"std_{tag}"), weights_only=True),
+                times=np.load(os.path.join(out_dir, f"times_{tag}.npy")),
+                rmse=np.load(os.path.join(out_dir, f"rmse_{tag}.npy")))
+
+
+def make_test_set(nq, backend, num_prob=1000, first_id=0, out_dir=None, seed=SEED):
+    """`testing` over num_prob problems -> X_test (data<n>_test.npy, triplependulum_testdata.py:137-145)."""
+    res, stats = testing_batch(nq, np.arange(first_id, first_id + num_prob), backend, seed=seed)
+    X = heldout_set(nq, res)
+    if out_dir is not None:
+        os.makedirs(out_dir, exist_ok=True)
+        np.save(os.path.join(out_dir, f"data{nq}_test.npy"), X)
+    return X, stats
+
+
+def _round(nq, backend, iteration, num_prob, N_start, seed):
+    """One data-generation round, sharded over ranks when torch.distributed is initialised."""
+    import torch.distributed as dist
+    from .dist import gather_samples, shard_ids
+    if dist.is_available() and dist.is_initialized():
+        import torch
+        world, rank = dist.get_world_size(), dist.get_rank()
+        per = -(-num_prob // world)
+        ids = shard_ids(iteration, world, rank, per)
+        res, stats = data_generation_batch(nq, ids, backend, N_start=N_start, seed=seed)
+        local = torch.from_numpy(samples_array(nq, res))
+        if dist.get_backend() == "nccl":
+            local = local.cuda()
+        return gather_samples(local).cpu().numpy(), stats
+    ids = np.arange(iteration * num_prob, (iteration + 1) * num_prob)
+    res, stats = data_generation_batch(nq, ids, backend, N_start=N_start, seed=seed)
+    return samples_array(nq, res), stats
+
+
+def _agree(flag):
+    """Rank 0's decision on every rank (the time budget must not split the ranks' loop counts)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return flag
+    t = torch.tensor([int(flag)], dtype=torch.int64)
+    if dist.get_backend() == "nccl":
+        t = t.cuda()
+    dist.broadcast(t, 0)
+    return bool(t.item())
+
+
+def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None, N_start=None, seed=SEED,
+             out_dir=None, device=None, trainer_kw=None, triple_refit_quirk=True, log=None):
+    """Run the VBOC loop; returns dict(X_save, mean, std, trainer, times, rmse, stats)."""
+    import torch
+    import torch.distributed as dist
+    if nq not in (2, 3):
+        raise NotImplementedError("the pendulum VBOC driver uses the free-time OCP (pendulum_vboc.py:54), "
+                                  "which the boundary solver does not implement")
+    log = log or (lambda *a: None)
+    rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+    device = device or ("cuda" if torch.cuda.is_available() else "cpu")
+    t0 = time.time()
+    iteration = 0
+    X_save, st = _round(nq, backend, iteration, num_prob, N_start, seed)
+    stats = [st]
+    log(f"iteration 0: {X_save.shape[0]} rows")
+    mean, std = position_stats(X_save, nq)
+    F = dir_features(X_save, mean, std, nq)
+    F_test = dir_features(X_test, mean, std, nq)
+    trainer = DirTrainer(nq, device, **(trainer_kw or {})) if rank0 else None
+    times, rmse, fits = [], [], []
+    if rank0:
+        fits.append(trainer.fit(F))
+        times.append(time.time() - t0)
+        rmse.append(trainer.rmse(F_test))
+        log(f"fit: {fits[-1]}  rmse {rmse[-1]:.4g}")
+    while _agree(time.time() - t0 < stop_time and (max_iterations is None or iteration < max_iterations)):
+        iteration += 1
+        X_new, st = _round(nq, backend, iteration, num_prob, N_start, seed)
+        stats.append(st)
+        X_save = np.concatenate((X_save, X_new))
+        if rank0:
+            src = X_save if (nq == 3 and triple_refit_quirk) else X_new
+            F_new = dir_features(src, mean, std, nq)
+            F = np.concatenate((F, F_new))
+            fits.append(trainer.fit(F, n_new=F_new.shape[0]))
+            times.append(time.time() - t0)
+            rmse.append(trainer.rmse(F_test))
+            log(f"iteration {iteration}: {X_save.shape[0]} rows, fit {fits[-1]}, rmse {rmse[-1]:.4g}")
+    if rank0 and out_dir is not None:
+        save_artifacts(out_dir, nq, X_save, mean, std, trainer.model, times, rmse)
+    return dict(X_save=X_save, mean=mean, std=std, trainer=trainer, times=times, rmse=rmse, stats=stats, fits=fits)
