@@ -41,7 +41,10 @@ for B, coop in [(B, c) for B in sizes for c in coops]:
     dc = lib.debug_counters()
     if dc["sqp_iters"]:
         ip = max(1, dc["ipm_iters"])
-        print("  wave phase cycles per IPM iteration:", {k: round(v / ip) for k, v in dc.items() if k not in
-              ("sqp_iters", "ipm_iters")}, "| per SQP iteration:", round(sum(v for k, v in dc.items() if k not in
-              ("sqp_iters", "ipm_iters")) / dc["sqp_iters"]), flush=True)
+        main = {k: v for k, v in dc.items() if k not in ("sqp_iters", "ipm_iters") and not k.startswith("split")}
+        print("  wave phase cycles per IPM iteration:", {k: round(v / ip) for k, v in main.items()},
+              "| per SQP iteration:", round(sum(main.values()) / dc["sqp_iters"]), flush=True)
+        if any(dc[f"split{i}"] for i in range(5)):
+            print("  split of the profiled pass, cycles per IPM iteration:",
+                  [round(dc[f"split{i}"] / ip) for i in range(5)], flush=True)
     s.close()

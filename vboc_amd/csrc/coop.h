@@ -27,6 +27,8 @@ namespace vboc {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) dbl2 gdbl2;
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
 
 __host__ __device__ constexpr int even_up(int v) { return (v + 1) & ~1; }
 
@@ -45,13 +47,18 @@ struct WaveLayout {
   // ring windows [lo, lo + W): factor [0, OC) (writes back [OK, OC)); vector pass [OPE, OX);
   // forward sweep [OC, OX); costate [0, OE)
   static constexpr int W_FAC = OC, LO_VEC = OPE, W_VEC = OX - OPE, LO_FWD = OC, W_FWD = OX - OC, W_COS = even_up(OE);
-  static constexpr int RS = even_up(W_FAC > W_COS ? W_FAC : W_COS);
+  // LDS-DMA rings (global_load_lds_dwordx4: one wave-instruction lands 64 lanes x 16 B = 128 doubles):
+  // the factorisation streams its window two stages ahead through 4 slots of 2 KiB (two DMAs per
+  // stage), the vector / forward / costate recursions six stages ahead through 8 slots of 1 KiB
+  static constexpr int RSF = 256, NSF = 4, DF = 2, RSV = 128, NSV = 8, DV = 6;
+  static constexpr int RING_D = NSF * RSF > NSV * RSV ? NSF * RSF : NSV * RSV;
   static_assert(OB % 2 == 0 && OZ % 2 == 0 && OD % 2 == 0 && OK % 2 == 0 && OPE % 2 == 0 && OC % 2 == 0 &&
                     OACL % 2 == 0 && OX % 2 == 0,
                 "16-byte aligned field ranges");
-  static_assert(RS <= 256 && W_VEC <= RS && W_FWD <= RS, "ring window: two 16-B chunks per lane");
+  static_assert(W_FAC <= RSF && W_VEC <= RSV && W_FWD <= RSV && W_COS <= RSV, "ring windows fit their slots");
+  static_assert(NSF >= DF + 2 && NSV >= DV + 2, "a slot is refilled >= 2 stages after its last read");
   // LDS (doubles): ring, then the fixed region
-  static constexpr int RING = 0, F0 = RING + 3 * RS, LR0 = F0 + NX * M0, MM0 = LR0 + M0 * M0, Y0 = MM0 + M0 * NQ,
+  static constexpr int RING = 0, F0 = RING + RING_D, LR0 = F0 + NX * M0, MM0 = LR0 + M0 * M0, Y0 = MM0 + M0 * NQ,
                        PE0 = Y0 + M0 * NQ, P = PE0 + NX, PA = P + NX * NX, PB = PA + NX * NX, APA = PB + NX * NU,
                        RU = APA + NX * NX, S = RU + NU * NU, PI = S + NU * NX, PV = PI + NX * NQ, DXV = PV + 2 * NX,
                        SC = DXV + 2 * NX, LINE = SC + NQ * NQ, ZERO = LINE + NQ, TRASH = ZERO + 16, PAR = TRASH + 64,
@@ -169,12 +176,25 @@ __device__ unsigned long long g_wave_prof[16];
 #define CPROF(i)
 #define CPROF_FLUSH(sq, ip)
 #endif
+// Sub-step split of ONE pass (-DVBOC_COOP_PROF -DVBOC_PROF_SPLIT=1 factor / 2 vec / 3 fwd): cycles of up
+// to five consecutive sections of that pass's stage loop into g_wave_prof[11..15]
+#if defined(VBOC_COOP_PROF) && defined(VBOC_PROF_SPLIT)
+#define SPROF_DECL(P) unsigned long long sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0, sp4 = 0, sp_t = 0; \
+  constexpr bool sp_on = (VBOC_PROF_SPLIT == (P)); if (sp_on) sp_t = __builtin_amdgcn_s_memtime();
+#define SPROF(i) if (sp_on) { const unsigned long long n_ = __builtin_amdgcn_s_memtime(); sp##i += n_ - sp_t; sp_t = n_; }
+#define SPROF_FLUSH if (sp_on && t == 0) { atomicAdd(&g_wave_prof[11], sp0); atomicAdd(&g_wave_prof[12], sp1); \
+  atomicAdd(&g_wave_prof[13], sp2); atomicAdd(&g_wave_prof[14], sp3); atomicAdd(&g_wave_prof[15], sp4); }
+#else
+#define SPROF_DECL(P)
+#define SPROF(i)
+#define SPROF_FLUSH
+#endif
 
 template <int NQ>
 struct Coop {
   using L = WaveLayout<NQ>;
   using PF = Par<NQ>;
-  static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1, REC = L::REC, RS = L::RS;
+  static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1, REC = L::REC;
   static constexpr int OA = L::OA, OB = L::OB, OZ = L::OZ, ODZ = L::ODZ, OQL = L::OQL, OQU = L::OQU,
                        OE = L::OE, OK = L::OK, OKF = L::OKF, OLR = L::OLR, OM = L::OM, OY = L::OY,
                        OPE = L::OPE, OD = L::OD, ODA = L::ODA, OC = L::OC, OACL = L::OACL, OX = L::OX, OU = L::OU,
@@ -185,35 +205,57 @@ struct Coop {
   gdouble* g;       // this workgroup's stage records in HBM
   const Work& w;
   const Opts& o;
-  const int t;      // lane
+  int t;            // lane (re-made opaque at every pass entry, see fresh())
   int N;
   double rs, rd0, e00, mu, nbox;   // interior-point scalars (wave-uniform)
 
   __device__ Coop(double* s_, gdouble* g_, const Work& w_, const Opts& o_, int t_)
       : s(s_), g(g_), w(w_), o(o_), t(t_), N(0) {}
 
+  // The lane index as a fresh opaque value: lane-derived addresses and descriptors are then recomputed
+  // in each pass instead of being hoisted to the kernel prologue and held live across the whole job
+  // loop (that hoisting alone pushed the kernel past 256 registers, i.e. one wave per SIMD).
+  __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(t)); }
+
   __device__ __forceinline__ gdouble& st(int k, int off) const { return g[(long long)k * REC + off]; }
   __device__ __forceinline__ double& par(int f) const { return s[L::PAR + f]; }
-  __device__ __forceinline__ static constexpr int slot_base(int slot) { return L::RING + slot * RS; }
+  __device__ __forceinline__ static constexpr int fslot(int slot) { return L::RING + slot * L::RSF; }
+  __device__ __forceinline__ static constexpr int vslot(int slot) { return L::RING + slot * L::RSV; }
 
-  // ---- ring of stage windows: lane t moves 16-B chunks t and t + 64 ---------------------------------
-  __device__ __forceinline__ void ring_issue(int k, int lo, int W, dbl2 (&b)[2]) const {
-    // unconditional (clamped) loads: no exec-masked blocks around VMEM, so the waitcnt pass can keep
-    // the prefetch in flight across iterations
-    const gdbl2* src = (const gdbl2*)(g + (long long)k * REC + lo);
+  // ---- LDS-DMA rings of stage windows -----------------------------------------------------------------
+  // One wave-instruction: lane t copies 16-B chunk (part*64 + t) of stage k's window [lo, lo + W) to LDS
+  // doubles [dst + part*128 + 2t] (dst wave-uniform).  Chunk indices are clamped, never exec-masked, so
+  // every call is exactly one VMEM op and the counted waits below stay exact.
+  // Issued as inline asm: with the builtin, the compiler cannot tell the ring slots apart inside the one
+  // dynamic LDS array and drains every in-flight DMA (vmcnt(0)) before each ds_read of the ring.  The asm
+  // op is invisible to the compiler's own VMEM count, which can then only over-wait, never under-wait.
+  __device__ __forceinline__ void dma(int k, int lo, int W, int dst, int part) const {
     const int nc = W / 2;
-    b[0] = src[t < nc ? t : nc - 1];
-    b[1] = src[t + 64 < nc ? t + 64 : nc - 1];
+    const int c = part * 64 + t < nc ? part * 64 + t : nc - 1;
+    const gdouble* src = g + (long long)k * REC + lo + 2 * c;
+    const unsigned lds = (unsigned)__builtin_amdgcn_readfirstlane(
+        (int)(unsigned)(size_t)(lvoid*)(s + dst + part * 128));
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds)
+                 : "memory");
   }
-  __device__ __forceinline__ void ring_put(int slot, int W, const dbl2 (&b)[2]) const {
-    dbl2* dst = (dbl2*)(s + slot_base(slot));
-    if (2 * t < W) dst[t] = b[0];
-    if (2 * (t + 64) < W) dst[t + 64] = b[1];
-  }
-  __device__ __forceinline__ void ring_wb(int slot, int k, int lo, int hi) const {
-    const dbl2* src = (const dbl2*)(s + slot_base(slot));
+  // wait until at most N VMEM ops of this wave are outstanding (LDS-DMA landings are ordered for this
+  // wave's own ds_reads by this wait alone)
+  template <int N>
+  __device__ __forceinline__ static void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+  // retire every ordinary VMEM op in a way the compiler's waitcnt pass sees (the builtin, vmcnt(0)):
+  // called before a ring's first DMA, so no loop-carried register is still "pending" in the pass's
+  // bookkeeping - otherwise it re-waits vmcnt(0) inside the loop and drains the ring every stage
+  __device__ __forceinline__ static void settle() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+  // write fields [LO, HI) of a factor slot back to stage k's record: exactly one VMEM op
+  template <int LO, int HI>
+  __device__ __forceinline__ void ring_wb(int slot, int k) const {
+    static_assert((HI - LO) / 2 <= 64 && LO % 2 == 0, "one 16-B chunk per lane");
+    const dbl2* src = (const dbl2*)(s + fslot(slot));
     gdbl2* dst = (gdbl2*)(g + (long long)k * REC);
-    for (int c = lo / 2 + t; c < hi / 2; c += 64) dst[c] = src[c];
+    if (t < (HI - LO) / 2) dst[LO / 2 + t] = src[LO / 2 + t];
   }
 
   // box of component i of stage k (the Lane::stage_box pattern)
@@ -425,6 +467,7 @@ struct Coop {
   // problem set-up: from the inputs (wave mode) or from a lane-mode slot (hand-off)
   // ---------------------------------------------------------------------------------------------
   __device__ void from_inputs(const Inputs& in, int pid) {
+    fresh();
     constexpr int NXR = NX + 1, NP = NQ + 1;
     N = in.N[pid];
     const double* p = in.p + (long long)pid * NP;
@@ -478,6 +521,7 @@ struct Coop {
     __syncthreads();
   }
   __device__ void from_slot(const SlotState& ss, unsigned slot) {
+    fresh();
     Lane<NQ> G(w, o, slot);
     N = ss(IS_N, slot);
     for (int f = t; f < PF::COUNT; f += 64) par(f) = G.par(f);
@@ -496,6 +540,7 @@ struct Coop {
   // linearisation (stage-parallel): ERK4 + sensitivities, defects, current z, NLP residuals
   // ---------------------------------------------------------------------------------------------
   __device__ void linearize(double& rstat, double& req, double& rineq, double& rcomp) {
+    fresh();
     const double h = par(PF::H), sv = par(PF::S);
     double stt = 0.0, eq = 0.0, inq = 0.0, cp = 0.0;
     for (int k = t; k <= N; k += 64) {
@@ -590,6 +635,7 @@ struct Coop {
   // interior-point QP
   // ---------------------------------------------------------------------------------------------
   __device__ void qp_init() {
+    fresh();
     double musum = 0.0, nb = 0.0, rd = 0.0, e0 = 0.0;
     for (int k = t; k <= N; k += 64) {
       gdouble* rec = &g[(long long)k * REC];
@@ -648,6 +694,7 @@ struct Coop {
 
   // H -> D slot, predictor gradient -> DA slot
   __device__ void prep_pred() {
+    fresh();
     for (int k = t; k <= N; k += 64) {
       IP r;
       ld_ip(k, r);
@@ -663,6 +710,7 @@ struct Coop {
   }
   // corrector gradient (uses the affine direction in DA) -> D slot
   __device__ void prep_corr(double smu) {
+    fresh();
     for (int k = t; k <= N; k += 64) {
       IP r;
       double da[2 * ((2 * NZ + 1) / 2)];
@@ -686,6 +734,7 @@ struct Coop {
 
   // Riccati factorisation (matrix part) of stages N-1..0 through the LDS ring; the vector part is vec()
   __device__ bool factor() {
+    fresh();
     for (int e = t; e < NX * NX; e += 64) {
       const int i = e / NX, j = e % NX;
       s[L::P + e] = (i == j) ? (double)st(N, OD + i) : 0.0;
@@ -696,27 +745,38 @@ struct Coop {
     }
     for (int e = t; e < NQ * NQ; e += 64) s[L::SC + e] = 0.0;
     if (t < NQ) s[L::LINE + t] = 0.0;
-    dbl2 b[2];
-    ring_issue(N - 1, 0, L::W_FAC, b);
-    ring_put(0, L::W_FAC, b);
-    if (N >= 2) {
-      ring_issue(N - 2, 0, L::W_FAC, b);
-      ring_put(1, L::W_FAC, b);
-    }
-    __syncthreads();
+    // stage windows through the 4-slot LDS-DMA ring, landing two stages ahead (sweep index j <-> stage
+    // N-1-j, clamped at 0); P = DMAs per stage
+    constexpr int P = L::W_FAC > 128 ? 2 : 1;
+    auto fdma = [&](int j) {
+      const int kk = N - 1 - j >= 0 ? N - 1 - j : 0;
+      dma(kk, 0, L::W_FAC, fslot(j % L::NSF), 0);
+      if (P == 2) dma(kk, 0, L::W_FAC, fslot(j % L::NSF), 1);
+    };
+    __syncthreads();   // before any DMA is in flight: this barrier's fence would drain them
+    settle();
+    fdma(0);
+    fdma(1);
     bool ok = true;
     Dsc d1, d2, d4;
     desc_mid(d1, d2, d4);
+    SPROF_DECL(1)
     for (int j = 0; j < N; ++j) {
-      const int k = N - 1 - j, slot = j % 3, kb = slot_base(slot);
-      const bool pf = k >= 2;
-      // outputs of the previous stage (k + 1) go out first, so their stores complete under this
-      // stage's arithmetic instead of stalling the ring put at its end
-      if (j >= 1) ring_wb((j - 1) % 3, k + 1, OK, OC);
-      if (pf) ring_issue(k - 2, 0, L::W_FAC, b);
+      const int k = N - 1 - j, kb = fslot(j % L::NSF);
+      // outputs of the previous stage (k + 1) go out first (one store), then the DMA two stages ahead
+      if (j >= 1) ring_wb<OK, OC>((j - 1) % L::NSF, k + 1);
+      fdma(j + 2);
+      SPROF(4)
+      // VMEM ops issued after stage k's DMAs: j = 0: 2P, j = 1: 2P + 1, else 2P + 2
+      if (j == 0) vmwait<2 * P>();
+      else if (j == 1) vmwait<2 * P + 1>();
+      else vmwait<2 * P + 2>();
+      SPROF(3)
       if (k >= 1) {
         dstep<NX, 0>(d1, kb);
+        SPROF(0)
         dstep<NX, 0>(d2, kb);
+        SPROF(1)
         int rb = L::ZERO, rstr = 0, db = L::TRASH + t, dstr = 0;
         double sgn = 1.0;
         if (t < NX) { rb = L::S + t; rstr = NX; db = kb + OK + t; dstr = NX; sgn = -1.0; }
@@ -724,6 +784,7 @@ struct Coop {
         const bool okk = sstep<NU>(L::RU, kb + OLR, rb, rstr, db, dstr, sgn);
         ok = ok && okk;
         dstep<NX, NU>(d4, kb);
+        SPROF(2)
       } else {
         Dsc z1, z2, z4;
         desc_s0(z1, z2, z4);
@@ -735,9 +796,10 @@ struct Coop {
         ok = ok && ok0;
         dstep<0, M0>(z4, kb);
       }
-      if (pf) ring_put((j + 2) % 3, L::W_FAC, b);
       lsync();
+      SPROF(4)
     }
+    SPROF_FLUSH
     __syncthreads();   // write-back visible to the next sweep's ring loads
     return ok;
   }
@@ -746,6 +808,7 @@ struct Coop {
   // factorisation, stage-parallel, and shared by both vector passes (columns) and both forward
   // sweeps (rows) of the interior-point iteration
   __device__ void acl_pass() {
+    fresh();
     constexpr int NAB = (NX * NX + NX * NU) / 2, NKK = (NU * NX) / 2;
     for (int k = 1 + t; k < N; k += 64) {
       double ab[2 * NAB], kk[2 * NKK];
@@ -773,8 +836,10 @@ struct Coop {
   // vector pass with the gradient in slot OG; leaves the stage-0 open-loop step w0 and the
   // terminal multiplier nu (wave-uniform).  False if S = sum Y'M is not positive definite.
   __device__ bool vec(int OG, double (&w0)[M0], double (&nun)[NQ]) {
+    fresh();
     // p_k = c'_k + A_cl,k' p_{k+1},  c'_k = g_x + K'g_u + A_cl' PE_k  (lane i: row i of p);
     // v_k = PE_k + p_{k+1} is kept for k_f.  c' is formed stage-parallel first (-> OC).
+    SPROF_DECL(2)
     {
       constexpr int NZH = (2 * NZ + 1) / 2, NKK = (NU * NX) / 2;
       for (int k = 1 + t; k < N; k += 64) {
@@ -802,14 +867,17 @@ struct Coop {
       }
       __syncthreads();
     }
+    SPROF(0)
     double pcur = st(N, OG + (t < NX ? t : NX - 1));
     if (t < NX) s[L::PV + t] = pcur;
     const int cnt = N - 1;   // stages N-1 .. 1
-    dbl2 b[2];
-    if (cnt >= 1) { ring_issue(N - 1, L::LO_VEC, L::W_VEC, b); ring_put(0, L::W_VEC, b); }
-    if (cnt >= 2) { ring_issue(N - 2, L::LO_VEC, L::W_VEC, b); ring_put(1, L::W_VEC, b); }
     __syncthreads();
-    // ring slot of the vector pass: [PE | C | ACL]
+    // stage windows [PE | C | ACL] through the 8-slot LDS-DMA ring, DV stages ahead (sweep index j <->
+    // stage N-1-j, clamped at 1): one DMA per stage, so DV - 1 are younger than the one waited for
+    auto vdma = [&](int j) {
+      const int kk = N - 1 - j >= 1 ? N - 1 - j : 1;
+      dma(kk, L::LO_VEC, L::W_VEC, vslot(j % L::NSV), 0);
+    };
     auto vld = [&](int kb, double (&acl)[NX], double& cc, double& pe) {
       const int i = t < NX ? t : NX - 1;
       UNR for (int q = 0; q < NX; ++q) acl[q] = s[kb + (OACL - OPE) + q * NX + i];
@@ -817,18 +885,20 @@ struct Coop {
       pe = s[kb + i];
     };
     double acl[NX], cc = 0.0, pe = 0.0;
-    if (cnt >= 1) vld(slot_base(0), acl, cc, pe);
-    // prefetch distance 2: stage S[j+3] is loaded into one register buffer while the other (S[j+2],
-    // loaded one iteration earlier) goes to its ring slot; the loop is unrolled x2 to alternate them
-    dbl2 bA[2], bB[2];
-    if (cnt >= 3) ring_issue(N - 3, L::LO_VEC, L::W_VEC, bB);
-    auto vbody = [&](int j, dbl2 (&bl)[2], dbl2 (&bp)[2]) {
+    settle();
+    if (cnt >= 1) {
+      UNR for (int d = 0; d < L::DV; ++d) vdma(d);
+      vmwait<L::DV - 1>();
+      vld(vslot(0), acl, cc, pe);
+    }
+    for (int j = 0; j < cnt; ++j) {
       const int k = N - 1 - j;
       const int rb = L::PV + (j & 1) * NX, wb = L::PV + ((j + 1) & 1) * NX;
-      ring_issue(k - 3 >= 0 ? k - 3 : 0, L::LO_VEC, L::W_VEC, bl);
+      vdma(j + L::DV);
+      vmwait<L::DV - 1>();   // stage of sweep index j + 1 has landed
       double pv[NX], an[NX], cn, pn;
       UNR for (int q = 0; q < NX; ++q) pv[q] = s[rb + q];
-      vld(slot_base((j + 1 < cnt ? j + 1 : j) % 3), an, cn, pn);
+      vld(vslot((j + 1) % L::NSV), an, cn, pn);
       __builtin_amdgcn_sched_barrier(0);
       double p0 = cc, p1 = 0.0;
       UNR for (int q = 0; q < NX; q += 2) p0 += acl[q] * pv[q];
@@ -839,15 +909,11 @@ struct Coop {
       UNR for (int q = 0; q < NX; ++q) acl[q] = an[q];
       cc = cn;
       pe = pn;
-      if (j + 2 < cnt) ring_put((j + 2) % 3, L::W_VEC, bp);
       lsync();
-    };
-    for (int j = 0; j < cnt; j += 2) {
-      vbody(j, bA, bB);
-      if (j + 1 < cnt) vbody(j + 1, bB, bA);
     }
     if (t < NX) s[L::PV + t] = pcur;
     __syncthreads();
+    SPROF(1)
     // k_f = -Ru^-1 (g_u + B'v) per stage, lin = sum Y'k_f  (stage-parallel)
     double lin[NQ];
     UNR for (int j = 0; j < NQ; ++j) lin[j] = 0.0;
@@ -876,6 +942,7 @@ struct Coop {
         UNR for (int a = 0; a < NU; ++a) lin[j] += ly[Y_ + a * NQ + j] * r[a];
     }
     UNR for (int j = 0; j < NQ; ++j) lin[j] = wsum(lin[j]);
+    SPROF(2)
     // stage 0 (every lane, identical)
     {
       double v[NX], Lm[M0 * M0];
@@ -897,6 +964,8 @@ struct Coop {
     UNR for (int j = 0; j < NQ; ++j) nun[j] = lin[j] + s[L::LINE + j] - rs * par(PF::E0N + j);
     chol_solve<NQ>(Sl, nun);
     __syncthreads();
+    SPROF(3)
+    SPROF_FLUSH
     return ok;
   }
 
@@ -905,7 +974,9 @@ struct Coop {
   template <bool CORR>
   __device__ void fwd(const double (&w0in)[M0], const double (&nun)[NQ], double smu, double& amax, double& c0,
                       double& c1, double& c2) {
+    fresh();
     constexpr int OT = CORR ? OD : ODA;
+    SPROF_DECL(3)
     {
       double w0[M0];
       UNR for (int a = 0; a < M0; ++a) {
@@ -923,6 +994,7 @@ struct Coop {
         s[L::DXV + t] = x;
       }
     }
+    SPROF(0)
     // dx_{k+1} = c_k + A_cl,k dx_k,  c_k = rs e_k + B_k (k_f - M_k nu)  (lane i: row i); c is formed
     // stage-parallel first (-> OC)
     {
@@ -955,12 +1027,15 @@ struct Coop {
       }
       __syncthreads();
     }
+    SPROF(1)
     const int cnt = N - 1;   // stages 1 .. N-1
-    dbl2 b[2];
-    if (cnt >= 1) { ring_issue(1, L::LO_FWD, L::W_FWD, b); ring_put(0, L::W_FWD, b); }
-    if (cnt >= 2) { ring_issue(2, L::LO_FWD, L::W_FWD, b); ring_put(1, L::W_FWD, b); }
     __syncthreads();
-    // ring slot of the forward sweep: [C | ACL]
+    // stage windows [C | ACL] through the 8-slot LDS-DMA ring, DV stages ahead (sweep index j <-> stage
+    // 1 + j, clamped at N - 1)
+    auto wdma = [&](int j) {
+      const int kk = 1 + j < N ? 1 + j : N - 1;
+      dma(kk, L::LO_FWD, L::W_FWD, vslot(j % L::NSV), 0);
+    };
     auto fld = [&](int kb, double (&acl)[NX], double& cc) {
       const int i = t < NX ? t : NX - 1;
       UNR for (int q = 0; q < NX; ++q) acl[q] = s[kb + (OACL - OC) + i * NX + q];
@@ -968,16 +1043,20 @@ struct Coop {
     };
     {
       double acl[NX], cc = 0.0;
-      if (cnt >= 1) fld(slot_base(0), acl, cc);
-      dbl2 bA[2], bB[2];
-      if (cnt >= 3) ring_issue(3, L::LO_FWD, L::W_FWD, bB);
-      auto fbody = [&](int j, dbl2 (&bl)[2], dbl2 (&bp)[2]) {
+      settle();
+      if (cnt >= 1) {
+        UNR for (int d = 0; d < L::DV; ++d) wdma(d);
+        vmwait<L::DV - 1>();
+        fld(vslot(0), acl, cc);
+      }
+      for (int j = 0; j < cnt; ++j) {
         const int k = 1 + j;
         const int rb = L::DXV + (j & 1) * NX, wb = L::DXV + ((j + 1) & 1) * NX;
-        ring_issue(k + 3 < N ? k + 3 : N - 1, L::LO_FWD, L::W_FWD, bl);
+        wdma(j + L::DV);
+        vmwait<L::DV - 1>();
         double dx[NX], an[NX], cn;
         UNR for (int q = 0; q < NX; ++q) dx[q] = s[rb + q];
-        fld(slot_base((j + 1 < cnt ? j + 1 : j) % 3), an, cn);
+        fld(vslot((j + 1) % L::NSV), an, cn);
         __builtin_amdgcn_sched_barrier(0);
         double p0 = cc, p1 = 0.0;
         UNR for (int q = 0; q < NX; q += 2) p0 += acl[q] * dx[q];
@@ -989,15 +1068,11 @@ struct Coop {
         }
         UNR for (int q = 0; q < NX; ++q) acl[q] = an[q];
         cc = cn;
-        if (j + 2 < cnt) ring_put((j + 2) % 3, L::W_FWD, bp);
         lsync();
-      };
-      for (int j = 0; j < cnt; j += 2) {
-        fbody(j, bA, bB);
-        if (j + 1 < cnt) fbody(j + 1, bB, bA);
       }
     }
     __syncthreads();   // dx rows (global) visible to the stage-parallel pass
+    SPROF(2)
     // controls of the middle stages, then the step-length tests (stage-parallel)
     typename Lane<NQ>::MinRatio mr{1.0, CORR ? o.tau : 1.0};
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
@@ -1052,9 +1127,12 @@ struct Coop {
     amax = wmind(mr.value());
     c0 = wsum(a0); c1 = wsum(a1); c2 = wsum(a2);
     __syncthreads();
+    SPROF(3)
+    SPROF_FLUSH
   }
 
   __device__ void update(double alpha, double smu) {
+    fresh();
     double musum = 0.0;
     for (int k = t; k <= N; k += 64) {
       IP r;
@@ -1083,6 +1161,7 @@ struct Coop {
 
   // costate recovery into the DA slot (x part) of stages 0..N-1
   __device__ bool costate() {
+    fresh();
     bool fin = true;
     if (t < NX) {
       const int i = t;
@@ -1095,26 +1174,32 @@ struct Coop {
     }
     fin = __ballot(!fin) == 0ull;
     const int cnt = N - 1;   // stages N-1 .. 1
-    dbl2 b[2];
-    if (cnt >= 1) { ring_issue(N - 1, 0, L::W_COS, b); ring_put(0, L::W_COS, b); }
-    if (cnt >= 2) { ring_issue(N - 2, 0, L::W_COS, b); ring_put(1, L::W_COS, b); }
     __syncthreads();
+    // stage windows [A, e) through the 8-slot LDS-DMA ring (sweep index j <-> stage N-1-j, clamped at 1)
+    auto cdma = [&](int j) {
+      const int kk = N - 1 - j >= 1 ? N - 1 - j : 1;
+      dma(kk, 0, L::W_COS, vslot(j % L::NSV), 0);
+    };
     auto cterms = [&](int kb, double (&ac)[NX], double& cc) {
       const int i = t < NX ? t : NX - 1;
       cc = o.lm * s[kb + ODZ + i] - s[kb + OQL + i] + s[kb + OQU + i];
       UNR for (int q = 0; q < NX; ++q) ac[q] = s[kb + OA + q * NX + i];
     };
     double ac[NX], cc = 0.0;
-    if (cnt >= 1) cterms(slot_base(0), ac, cc);
-    dbl2 bA[2], bB[2];
-    if (cnt >= 3) ring_issue(N - 3, 0, L::W_COS, bB);
-    auto cbody = [&](int j, dbl2 (&bl)[2], dbl2 (&bp)[2]) {
+    settle();
+    if (cnt >= 1) {
+      UNR for (int d = 0; d < L::DV; ++d) cdma(d);
+      vmwait<L::DV - 1>();
+      cterms(vslot(0), ac, cc);
+    }
+    for (int j = 0; j < cnt; ++j) {
       const int k = N - 1 - j;
       const int rb = L::DXV + (j & 1) * NX, wb = L::DXV + ((j + 1) & 1) * NX;
-      ring_issue(k - 3 >= 0 ? k - 3 : 0, 0, L::W_COS, bl);
+      cdma(j + L::DV);
+      vmwait<L::DV - 1>();
       double lam[NX], an[NX], cn;
       UNR for (int q = 0; q < NX; ++q) lam[q] = s[rb + q];
-      cterms(slot_base((j + 1 < cnt ? j + 1 : j) % 3), an, cn);
+      cterms(vslot((j + 1) % L::NSV), an, cn);
       __builtin_amdgcn_sched_barrier(0);
       double p0 = cc, p1 = 0.0;
       UNR for (int q = 0; q < NX; q += 2) p0 += ac[q] * lam[q];
@@ -1126,13 +1211,9 @@ struct Coop {
       }
       UNR for (int q = 0; q < NX; ++q) ac[q] = an[q];
       cc = cn;
-      if (j + 2 < cnt) ring_put((j + 2) % 3, L::W_COS, bp);
       lsync();
-    };
-    for (int j = 0; j < cnt; j += 2) {
-      cbody(j, bA, bB);
-      if (j + 1 < cnt) cbody(j + 1, bB, bA);
     }
+    __syncthreads();   // drains the clamped tail DMAs before the ring is reused
     for (int k = t; k < N; k += 64) {
       UNR for (int i = 0; i < NX; ++i) st(k, ODA + i) = s[L::XS + k * NX + i];
     }
@@ -1144,6 +1225,7 @@ struct Coop {
   // merit line search + update (stage-parallel)
   // ---------------------------------------------------------------------------------------------
   __device__ void update_weights() {
+    fresh();
     double lmax = 0.0;
     for (int k = t; k <= N; k += 64) {
       if (k < N) {
@@ -1159,7 +1241,8 @@ struct Coop {
     __syncthreads();
   }
 
-  __device__ double merit(double alpha) const {
+  __device__ double merit(double alpha) {
+    fresh();
     const double h = par(PF::H);
     const double sv = par(PF::S) + alpha * st(0, ODZ);
     double val = 0.0, viol = 0.0;
@@ -1196,6 +1279,7 @@ struct Coop {
   }
 
   __device__ void apply(double alpha) {
+    fresh();
     for (int k = t; k <= N; k += 64) {
       gdouble* rec = &g[(long long)k * REC];
       if (k == 0) {
@@ -1222,7 +1306,8 @@ struct Coop {
     __syncthreads();
   }
 
-  __device__ void store(const Inputs& in, int pid, int status, int it, int qit) const {
+  __device__ void store(const Inputs& in, int pid, int status, int it, int qit) {
+    fresh();
     constexpr int NXR = NX + 1;
     double* xo = in.xo + (long long)pid * (in.nmax + 1) * NXR;
     double* uo = in.uo + (long long)pid * in.nmax * NU;
@@ -1336,11 +1421,11 @@ struct WaveJobs {
   long long region_doubles;
 };
 
-// Register budget of the wave kernel.  Default: unrestricted (~470 VGPR+AGPR, 1 wave per SIMD, 4
-// problems per CU).  Forcing 2 waves per SIMD (-DVBOC_WAVE_WPE='__attribute__((amdgpu_waves_per_eu(2,2)))')
-// spills inside the recursions and measured 1.6x slower on the 100k bench (profiles/r01_*wave*).
+// Register budget of the wave kernel: two waves per SIMD (<= 256 VGPRs, eight problems per CU).  It
+// fits without spills only because every pass re-derives its lane-dependent values (Coop::fresh());
+// override with -DVBOC_WAVE_WPE= (empty) for the unconstrained one-wave build.
 #ifndef VBOC_WAVE_WPE
-#define VBOC_WAVE_WPE
+#define VBOC_WAVE_WPE __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
 
 // one workgroup = one wave = one problem at a time; workgroups pull jobs until none are left

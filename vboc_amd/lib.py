@@ -187,7 +187,7 @@ def debug_counters():
     buf = (ctypes.c_ulonglong * 16)()
     _check(load().vboc_debug_counters(buf))
     names = ("linearize", "qp_init", "prep", "factor", "vec", "fwd", "update", "costate", "linesearch",
-             "sqp_iters", "ipm_iters")
+             "sqp_iters", "ipm_iters", "split0", "split1", "split2", "split3", "split4")
     return {n: int(buf[i]) for i, n in enumerate(names)}
 
 
