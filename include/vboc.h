@@ -19,6 +19,8 @@
  *                             get_cost(), solve() status (:115,126-129,189)
  *   vboc_rk4_batch         <- SYMtriplependulumINIT().acados_integrator set('x','u','T')/solve()/get('x')
  *                             VBOC/triplependulum_class_vboc.py:235-239, VBOC/triplependulum_vboc.py:346-353
+ *   vboc_solve_batch_ft    <- one OCPpendulum.OCP_solve(...) per problem (free-time OCP, dt a state):
+ *                             VBOC/pendulum_class_vboc.py:107-130, called from VBOC/pendulum_vboc.py:94,181
  *   vboc_destroy           <- solver object destruction (acados_template __del__ -> free)
  *   vboc_last_error        <- Python exceptions raised by acados_template on bad fields
  *
@@ -104,6 +106,20 @@ int vboc_get_option(vboc_handle h, const char* field, double* value);
 int vboc_solve_batch(vboc_handle h, const vboc_batch_t* batch, void* stream);
 /* Same with HOST pointers: staged through the handle's device buffers; synchronous. */
 int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* batch);
+
+/* Free-time box OCP (OCP<sys>.OCP_solve with dt a decision state; the pendulum's
+ * OCPpendulum.OCP_solve(x_guess, u_guess, cost_dir, q_lb, q_ub, q_init, q_fin),
+ * VBOC/pendulum_class_vboc.py:107-130, called from VBOC/pendulum_vboc.py:94,181).  Same batch
+ * layout; the semantics differ from vboc_solve_batch:
+ *   x_k = [theta, dtheta, dt] with dt a state (dt_{k+1} = dt_k), RK4 with h = dt per interval;
+ *   cost p[:nq] . dtheta_0 + p[nq] * sum_{k<N} dt_k  (EXTERNAL cost, :70-74);
+ *   stage 0: components with lbx_0 == ubx_0 fixed, others boxed; stages 1..N-1: boxes lbx/ubx (every
+ *   component must have lb < ub) and lbu/ubu; stage N: components with lbx_e == ubx_e are equality
+ *   constraints, others boxed; no general constraint.  Anything else: status 5.
+ * vboc_solve_batch_ft enqueues ONE kernel on `stream` and returns without waiting (device pointers);
+ * the _host variant is synchronous. */
+int vboc_solve_batch_ft(vboc_handle h, const vboc_batch_t* batch, void* stream);
+int vboc_solve_batch_ft_host(vboc_handle h, const vboc_batch_t* batch);
 
 /* Twin integrator: one ERK4 step of length T of the unscaled 2nq-state model for B states.
  * x[B][2nq], u[B][nq] -> x_out[B][2nq].  Device pointers (async) / host pointers (sync). */

@@ -80,10 +80,20 @@ def rk4_sens(nq, h, x, u):
     return x1, A, B
 
 
+def ft_rk4_sens(nq, x, u):
+    """Shooting map of the free-time model (x = [q, v, dt]) and its Jacobians (vboc_oracle_ft.c)."""
+    x, u = (np.ascontiguousarray(a, dtype=np.float64) for a in (x, u))
+    nx = 2 * nq + 1
+    x1, A, B = np.zeros(nx), np.zeros((nx, nx)), np.zeros((nx, nq))
+    lib().vboc_oracle_ft_rk4_sens(nq, _p(x), _p(u), _p(x1), _p(A), _p(B))
+    return x1, A, B
+
+
 def solve_batch(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe, ubxe,
-                opts=None, nthreads=None):
+                opts=None, nthreads=None, free_time=False):
     """Problem-major batch in the reference layout (see vboc_oracle.c).  Returns
-    (x_out, u_out, results)."""
+    (x_out, u_out, results).  free_time: the free-time box OCP of vboc_oracle_ft.c
+    (OCPpendulum.OCP_solve); an unsupported structure there gives status 5."""
     N = np.ascontiguousarray(N, dtype=np.int32)
     B = N.shape[0]
     arrs = [np.ascontiguousarray(a, dtype=np.float64)
@@ -95,7 +105,8 @@ def solve_batch(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe
     res = np.zeros(B, dtype=RESULT_DTYPE)
     o = opts if opts is not None else default_opts()
     nthreads = nthreads or os.cpu_count()
-    rc = lib().vboc_oracle_solve_batch(nq, B, Nmax, _p(N), *[_p(a) for a in arrs], ctypes.byref(o),
+    fn = lib().vboc_oracle_ft_solve_batch if free_time else lib().vboc_oracle_solve_batch
+    rc = fn(nq, B, Nmax, _p(N), *[_p(a) for a in arrs], ctypes.byref(o),
                                        int(nthreads), _p(x_out), _p(u_out), _p(res))
     if rc != 0:
         raise RuntimeError(f"oracle solve_batch failed rc={rc}")

@@ -33,6 +33,17 @@ int vboc_oracle_solve_batch(int nq, int B, int Nmax, const int* N, const double*
                             const double* lbu, const double* ubu, const double* lbx0, const double* ubx0,
                             const double* lbxe, const double* ubxe, const vboc_opts_t* opts, int nthreads,
                             double* x_out, double* u_out, vboc_result_t* res);
+/* free-time box OCP (vboc_oracle_ft.c): dt a state, terminal/stage-0 fixed components by lb == ub */
+void vboc_oracle_ft_rk4_sens(int nq, const double* x, const double* u, double* x1, double* A, double* B);
+int vboc_oracle_ft_solve(int nq, int N, const double* x_guess, const double* u_guess, const double* p,
+                         const double* lbx, const double* ubx, const double* lbu, const double* ubu,
+                         const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
+                         const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res);
+int vboc_oracle_ft_solve_batch(int nq, int B, int Nmax, const int* N, const double* x_guess,
+                               const double* u_guess, const double* p, const double* lbx, const double* ubx,
+                               const double* lbu, const double* ubu, const double* lbx0, const double* ubx0,
+                               const double* lbxe, const double* ubxe, const vboc_opts_t* opts, int nthreads,
+                               double* x_out, double* u_out, vboc_result_t* res);
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,790 @@
+/*
+ * ORACLE - TEST INFRASTRUCTURE ONLY.  Never linked into, loaded by or called from the product
+ * path (vboc_amd/).  Only tests/ use it, and only as the checker.
+ *
+ * Plain-C FP64 restatement of the FREE-TIME box OCP of the reference's OCP<sys> classes, i.e. what
+ *   OCPpendulum.OCP_solve(x_guess, u_guess, cost_dir, q_lb, q_ub, q_init, q_fin)
+ *   (VBOC/pendulum_class_vboc.py:107-130, model and options :8-103)
+ * asks ACADOS to do.  Differences from the boundary OCP of vboc_oracle.c:
+ *  - dt is a genuine state: x = [theta, dtheta, dt], f_expl = dt * [dtheta, acc, 0]
+ *    (pendulum_class_vboc.py:23-40), bounded dt in [0, 1e-2] at every stage (:80-89); one ERK4 step
+ *    of length 1 per interval (tf = N, :55-58) = RK4 with h = dt on the physics rhs, and the
+ *    shooting map's Jacobian carries the d/d(dt) column;
+ *  - cost EXTERNAL, linear: w1 * dtheta + wt * dt at stage 0, wt * dt at stages 1..N-1, none at N
+ *    (:70-74, p = [cost_dir, 1] from OCP_solve :116);
+ *  - no general constraint (ng = 0); stage 0 fixes the components with lbx_0 == ubx_0 (theta,
+ *    :119-120), the terminal stage the components with lbx_e == ubx_e (theta and dtheta, :121-122).
+ * Same SQP / merit / Mehrotra-IPM / Riccati algorithm and options as vboc_oracle.c (that file's
+ * header lists them), generalised to:
+ *  - stage-0 decision variables = the free components of x_0 plus u_0 (fixed ones are constants);
+ *  - terminal equalities E x_N = x_fix on any subset of components (Schur complement in the
+ *    backward sweep through Pi = E', exactly as the terminal-velocity equality of vboc_oracle.c);
+ *  - per-stage linear cost gradients.
+ * Path bounds must be proper boxes (lb < ub on every component); otherwise -2 (unsupported).
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "vboc_oracle.h"
+
+#define FQ 3
+#define FX (2 * FQ + 1)
+#define FU FQ
+#define FZ (FX + FU)
+
+typedef struct {
+  double x[FX], u[FU];
+  double pi[FX], ll[FZ], lu[FZ], wpi[FX];
+  double A[FX * FX], B[FX * FU], F0[FX * FZ], b[FX];
+  double Lb[FZ], Ub[FZ], dz[FZ], ql[FZ], qu[FZ], e0[FX];
+  double H[FZ], g[FZ], d[FZ], daff[FZ];
+  double K[FU * FX], kf[FU], Lr[FZ * FZ], M[FZ * FX], Y[FZ * FX], Pe[FX], qpi[FX];
+} fstage_t;
+
+typedef struct {
+  int nq, nx, nu, N;
+  int nf0, f0[FX];              /* free stage-0 components */
+  int ne, ei[FX];               /* fixed terminal components */
+  double ev[FX];                /* their values */
+  double c0[FX], cp[FX];        /* cost gradients: stage 0, stages 1..N-1 */
+  double x0lb[FX], x0ub[FX], xlb[FX], xub[FX], xNlb[FX], xNub[FX], ulb[FU], uub[FU];
+  int xNfix[FX];
+  double tnu[FX], wnu[FX], wbnd, qnu[FX];   /* terminal multipliers, merit weights */
+  double S[FX * FX], lin_e[FX], rs;
+  fstage_t* st;
+  vboc_opts_t o;
+} fprob_t;
+
+/* ------------------------------------------------------------------------------------------ */
+/* dynamics: physics rhs with analytic Jacobians (vboc_oracle_model), ERK4 with h = dt and the   */
+/* exact derivative of the discrete map w.r.t. (theta, dtheta, dt, u)                           */
+/* ------------------------------------------------------------------------------------------ */
+
+/* k = f(X, u); dk[:, c] = J(X) T[:, c] + df/du e_{c - ncol_u}  for the given tangent columns */
+static void rhs_t(int nq, const double* X, const double* u, const double* T, int nc, int cu0, double* k,
+                  double* dk) {
+  double acc[FQ], Jth[FQ * FQ], Jom[FQ * FQ], Ju[FQ * FQ];
+  vboc_oracle_model(nq, X, X + nq, u, acc, Jth, Jom, Ju);
+  for (int j = 0; j < nq; ++j) { k[j] = X[nq + j]; k[nq + j] = acc[j]; }
+  for (int c = 0; c < nc; ++c) {
+    for (int j = 0; j < nq; ++j) dk[j * nc + c] = T[(nq + j) * nc + c];
+    for (int j = 0; j < nq; ++j) {
+      double t = (c >= cu0 && c < cu0 + nq) ? Ju[j * nq + (c - cu0)] : 0.0;
+      for (int q = 0; q < nq; ++q) t += Jth[j * nq + q] * T[q * nc + c] + Jom[j * nq + q] * T[(nq + q) * nc + c];
+      dk[(nq + j) * nc + c] = t;
+    }
+  }
+}
+
+/* Phi(x, u) for x = [q, v, dt]; A = dPhi/dx (nx x nx, last column d/d(dt)), B = dPhi/du */
+static void ft_rk4_sens(int nq, const double* x, const double* u, double* phi, double* A, double* B) {
+  const int n2 = 2 * nq, nx = n2 + 1, nu = nq;
+  const int nc = n2 + nu + 1, cu0 = n2, ch = n2 + nu; /* tangent columns: (q,v), u, h */
+  const double h = x[n2];
+  double X[2 * FQ], T[2 * FQ * (FX + FU)], k[2 * FQ], dk[2 * FQ * (FX + FU)];
+  double ks[2 * FQ], Ts[2 * FQ * (FX + FU)], kp[2 * FQ], dkp[2 * FQ * (FX + FU)];
+  static const double cst[4] = {0.0, 0.5, 0.5, 1.0}, wgt[4] = {1.0, 2.0, 2.0, 1.0};
+  memset(ks, 0, sizeof(ks));
+  memset(Ts, 0, sizeof(Ts));
+  memset(kp, 0, sizeof(kp));
+  memset(dkp, 0, sizeof(dkp));
+  for (int s = 0; s < 4; ++s) {
+    /* stage point X = x + c h k_prev, tangent d X / d(col) */
+    for (int i = 0; i < n2; ++i) {
+      X[i] = x[i] + cst[s] * h * kp[i];
+      for (int c = 0; c < nc; ++c) {
+        double t = cst[s] * h * dkp[i * nc + c];
+        if (c == i) t += 1.0;
+        if (c == ch) t += cst[s] * kp[i];
+        T[i * nc + c] = t;
+      }
+    }
+    rhs_t(nq, X, u, T, nc, cu0, k, dk);
+    for (int i = 0; i < n2; ++i) {
+      ks[i] += wgt[s] * k[i];
+      for (int c = 0; c < nc; ++c) Ts[i * nc + c] += wgt[s] * dk[i * nc + c];
+    }
+    memcpy(kp, k, sizeof(kp));
+    memcpy(dkp, dk, sizeof(dkp));
+  }
+  for (int i = 0; i < n2; ++i) {
+    phi[i] = x[i] + h / 6.0 * ks[i];
+    for (int c = 0; c < n2; ++c) A[i * nx + c] = (c == i ? 1.0 : 0.0) + h / 6.0 * Ts[i * nc + c];
+    A[i * nx + n2] = ks[i] / 6.0 + h / 6.0 * Ts[i * nc + ch];
+    for (int a = 0; a < nu; ++a) B[i * nu + a] = h / 6.0 * Ts[i * nc + cu0 + a];
+  }
+  phi[n2] = h;
+  for (int c = 0; c < nx; ++c) A[n2 * nx + c] = (c == n2) ? 1.0 : 0.0;
+  for (int a = 0; a < nu; ++a) B[n2 * nu + a] = 0.0;
+}
+
+static void ft_rk4(int nq, const double* x, const double* u, double* phi) {
+  double A[FX * FX], B[FX * FU];
+  ft_rk4_sens(nq, x, u, phi, A, B);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* stage variables                                                                             */
+/* ------------------------------------------------------------------------------------------ */
+
+static int fnz(const fprob_t* P, int k) {
+  if (k == 0) return P->nf0 + P->nu;
+  if (k == P->N) return P->nx;
+  return P->nx + P->nu;
+}
+
+static void fcomp(const fprob_t* P, int k, int i, double* val, double* lb, double* ub, int* boxed) {
+  const fstage_t* s = &P->st[k];
+  const int nx = P->nx;
+  *boxed = 1;
+  if (k == 0) {
+    if (i < P->nf0) { const int c = P->f0[i]; *val = s->x[c]; *lb = P->x0lb[c]; *ub = P->x0ub[c]; }
+    else { *val = s->u[i - P->nf0]; *lb = P->ulb[i - P->nf0]; *ub = P->uub[i - P->nf0]; }
+    return;
+  }
+  if (k == P->N) {
+    *val = s->x[i];
+    if (P->xNfix[i]) { *lb = -INFINITY; *ub = INFINITY; *boxed = 0; }
+    else { *lb = P->xNlb[i]; *ub = P->xNub[i]; }
+    return;
+  }
+  if (i < nx) { *val = s->x[i]; *lb = P->xlb[i]; *ub = P->xub[i]; }
+  else { *val = s->u[i - nx]; *lb = P->ulb[i - nx]; *ub = P->uub[i - nx]; }
+}
+
+static double fgrad(const fprob_t* P, int k, int i) {
+  if (k == 0) return i < P->nf0 ? P->c0[P->f0[i]] : 0.0;
+  if (k == P->N) return 0.0;
+  return i < P->nx ? P->cp[i] : 0.0;
+}
+
+static double fcost(const fprob_t* P) {
+  double c = 0.0;
+  for (int i = 0; i < P->nx; ++i) c += P->c0[i] * P->st[0].x[i];
+  for (int k = 1; k < P->N; ++k)
+    for (int i = 0; i < P->nx; ++i) c += P->cp[i] * P->st[k].x[i];
+  return c;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* linearisation + NLP residuals                                                               */
+/* ------------------------------------------------------------------------------------------ */
+
+static void flinearize(fprob_t* P) {
+  const int nx = P->nx, nu = P->nu, m0 = P->nf0 + nu;
+  for (int k = 0; k < P->N; ++k) {
+    fstage_t* s = &P->st[k];
+    double phi[FX];
+    ft_rk4_sens(P->nq, s->x, s->u, phi, s->A, s->B);
+    for (int i = 0; i < nx; ++i) s->b[i] = phi[i] - P->st[k + 1].x[i];
+  }
+  fstage_t* s0 = &P->st[0];
+  for (int i = 0; i < nx; ++i) {
+    for (int j = 0; j < P->nf0; ++j) s0->F0[i * m0 + j] = s0->A[i * nx + P->f0[j]];
+    for (int a = 0; a < nu; ++a) s0->F0[i * m0 + P->nf0 + a] = s0->B[i * nu + a];
+  }
+}
+
+static void fresiduals(const fprob_t* P, double* rstat, double* req, double* rineq, double* rcomp) {
+  const int nx = P->nx, nu = P->nu, N = P->N, m0 = P->nf0 + nu;
+  double st = 0, eq = 0, in = 0, cp = 0;
+  for (int k = 0; k < N; ++k)
+    for (int i = 0; i < nx; ++i) eq = fmax(eq, fabs(P->st[k].b[i]));
+  for (int j = 0; j < P->ne; ++j) eq = fmax(eq, fabs(P->st[N].x[P->ei[j]] - P->ev[j]));
+  for (int k = 0; k <= N; ++k) {
+    const fstage_t* s = &P->st[k];
+    for (int i = 0; i < fnz(P, k); ++i) {
+      double v, lb, ub; int boxed;
+      fcomp(P, k, i, &v, &lb, &ub, &boxed);
+      double gr = fgrad(P, k, i) - s->ll[i] + s->lu[i];
+      if (k == 0) {
+        for (int r = 0; r < nx; ++r) gr += s->F0[r * m0 + i] * s->pi[r];
+      } else if (k < N) {
+        if (i < nx) {
+          for (int r = 0; r < nx; ++r) gr += s->A[r * nx + i] * s->pi[r];
+          gr -= P->st[k - 1].pi[i];
+        } else {
+          for (int r = 0; r < nx; ++r) gr += s->B[r * nu + (i - nx)] * s->pi[r];
+        }
+      } else {
+        gr -= P->st[N - 1].pi[i];
+        for (int j = 0; j < P->ne; ++j) if (P->ei[j] == i) gr += P->tnu[j];
+      }
+      st = fmax(st, fabs(gr));
+      if (boxed) {
+        in = fmax(in, fmax(lb - v, v - ub));
+        cp = fmax(cp, fmax(fabs(s->ll[i] * (v - lb)), fabs(s->lu[i] * (ub - v))));
+      }
+    }
+  }
+  *rstat = st; *req = eq; *rineq = in; *rcomp = cp;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Riccati solve of the Newton system (see newton_solve in vboc_oracle.c; Pi = E' here)        */
+/* ------------------------------------------------------------------------------------------ */
+
+static int fchol(int n, double* A) {
+  for (int j = 0; j < n; ++j) {
+    double s = A[j * n + j];
+    for (int k = 0; k < j; ++k) s -= A[j * n + k] * A[j * n + k];
+    if (!(s > 0.0)) return -1;
+    const double d = sqrt(s);
+    A[j * n + j] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double t = A[i * n + j];
+      for (int k = 0; k < j; ++k) t -= A[i * n + k] * A[j * n + k];
+      A[i * n + j] = t / d;
+    }
+    for (int i = 0; i < j; ++i) A[i * n + j] = 0.0;
+  }
+  return 0;
+}
+
+static void fchol_solve(int n, const double* L, double* b) {
+  for (int i = 0; i < n; ++i) {
+    double t = b[i];
+    for (int k = 0; k < i; ++k) t -= L[i * n + k] * b[k];
+    b[i] = t / L[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double t = b[i];
+    for (int k = i + 1; k < n; ++k) t -= L[k * n + i] * b[k];
+    b[i] = t / L[i * n + i];
+  }
+}
+
+static int fnewton(fprob_t* P, int factor, double* nu_new) {
+  const int nx = P->nx, nu = P->nu, ne = P->ne, N = P->N, m0 = P->nf0 + nu;
+  const double rs = P->rs;
+  double Pm[FX * FX], p[FX], Pi[FX * FX], lin[FX];
+  fstage_t* sN = &P->st[N];
+  memset(Pm, 0, sizeof(Pm));
+  for (int i = 0; i < nx; ++i) { Pm[i * nx + i] = sN->H[i]; p[i] = sN->g[i]; }
+  memset(Pi, 0, sizeof(Pi));
+  for (int j = 0; j < ne; ++j) Pi[P->ei[j] * ne + j] = 1.0;
+  memset(lin, 0, sizeof(lin));
+  if (factor) { memset(P->S, 0, sizeof(P->S)); memset(P->lin_e, 0, sizeof(P->lin_e)); }
+
+  for (int k = N - 1; k >= 0; --k) {
+    fstage_t* s = &P->st[k];
+    const int mk = (k == 0) ? m0 : nu;
+    const double* Bk = (k == 0) ? s->F0 : s->B;
+    const int uoff = (k == 0) ? 0 : nx;
+    double e[FX], v[FX], r[FZ];
+    for (int i = 0; i < nx; ++i) e[i] = rs * s->e0[i];
+    if (factor) {
+      for (int i = 0; i < nx; ++i) {
+        double t = 0; for (int j = 0; j < nx; ++j) t += Pm[i * nx + j] * e[j];
+        s->Pe[i] = t;
+      }
+      for (int j = 0; j < ne; ++j) {
+        double t = 0; for (int i = 0; i < nx; ++i) t += Pi[i * ne + j] * e[i];
+        P->lin_e[j] += t;
+      }
+      double BP[FZ * FX], Ru[FZ * FZ];
+      for (int a = 0; a < mk; ++a)
+        for (int j = 0; j < nx; ++j) {
+          double t = 0; for (int i = 0; i < nx; ++i) t += Bk[i * mk + a] * Pm[i * nx + j];
+          BP[a * nx + j] = t;
+        }
+      for (int a = 0; a < mk; ++a)
+        for (int c = 0; c < mk; ++c) {
+          double t = (a == c) ? s->H[uoff + a] : 0.0;
+          for (int i = 0; i < nx; ++i) t += BP[a * nx + i] * Bk[i * mk + c];
+          Ru[a * mk + c] = t;
+        }
+      for (int a = 0; a < mk; ++a)
+        for (int c = 0; c < a; ++c) { const double t = 0.5 * (Ru[a * mk + c] + Ru[c * mk + a]); Ru[a * mk + c] = Ru[c * mk + a] = t; }
+      if (fchol(mk, Ru)) return -1;
+      memcpy(s->Lr, Ru, sizeof(double) * mk * mk);
+      for (int a = 0; a < mk; ++a)
+        for (int j = 0; j < ne; ++j) {
+          double t = 0; for (int i = 0; i < nx; ++i) t += Bk[i * mk + a] * Pi[i * ne + j];
+          s->Y[a * ne + j] = t;
+        }
+      for (int j = 0; j < ne; ++j) {
+        double col[FZ];
+        for (int a = 0; a < mk; ++a) col[a] = s->Y[a * ne + j];
+        fchol_solve(mk, s->Lr, col);
+        for (int a = 0; a < mk; ++a) s->M[a * ne + j] = col[a];
+      }
+      for (int i = 0; i < ne; ++i)
+        for (int j = 0; j < ne; ++j) {
+          double t = 0; for (int a = 0; a < mk; ++a) t += s->Y[a * ne + i] * s->M[a * ne + j];
+          P->S[i * ne + j] += t;
+        }
+      if (k > 0) {
+        double Sux[FU * FX];
+        for (int a = 0; a < nu; ++a)
+          for (int j = 0; j < nx; ++j) {
+            double t = 0; for (int i = 0; i < nx; ++i) t += BP[a * nx + i] * s->A[i * nx + j];
+            Sux[a * nx + j] = t;
+          }
+        for (int j = 0; j < nx; ++j) {
+          double col[FU];
+          for (int a = 0; a < nu; ++a) col[a] = Sux[a * nx + j];
+          fchol_solve(nu, s->Lr, col);
+          for (int a = 0; a < nu; ++a) s->K[a * nx + j] = -col[a];
+        }
+        double AP[FX * FX], Pn[FX * FX], Acl[FX * FX], Pin[FX * FX];
+        for (int i = 0; i < nx; ++i)
+          for (int j = 0; j < nx; ++j) {
+            double t = 0; for (int q = 0; q < nx; ++q) t += s->A[q * nx + i] * Pm[q * nx + j];
+            AP[i * nx + j] = t;
+          }
+        for (int i = 0; i < nx; ++i)
+          for (int j = 0; j < nx; ++j) {
+            double t = (i == j) ? s->H[i] : 0.0;
+            for (int q = 0; q < nx; ++q) t += AP[i * nx + q] * s->A[q * nx + j];
+            for (int a = 0; a < nu; ++a) t += Sux[a * nx + i] * s->K[a * nx + j];
+            Pn[i * nx + j] = t;
+          }
+        for (int i = 0; i < nx; ++i)
+          for (int j = 0; j < i; ++j) { const double t = 0.5 * (Pn[i * nx + j] + Pn[j * nx + i]); Pn[i * nx + j] = Pn[j * nx + i] = t; }
+        for (int i = 0; i < nx; ++i)
+          for (int j = 0; j < nx; ++j) {
+            double t = s->A[i * nx + j];
+            for (int a = 0; a < nu; ++a) t += s->B[i * nu + a] * s->K[a * nx + j];
+            Acl[i * nx + j] = t;
+          }
+        for (int i = 0; i < nx; ++i)
+          for (int j = 0; j < ne; ++j) {
+            double t = 0; for (int q = 0; q < nx; ++q) t += Acl[q * nx + i] * Pi[q * ne + j];
+            Pin[i * ne + j] = t;
+          }
+        memcpy(Pm, Pn, sizeof(Pm));
+        memcpy(Pi, Pin, sizeof(Pi));
+      }
+    }
+    for (int i = 0; i < nx; ++i) v[i] = s->Pe[i] + p[i];
+    for (int a = 0; a < mk; ++a) {
+      double t = s->g[uoff + a];
+      for (int i = 0; i < nx; ++i) t += Bk[i * mk + a] * v[i];
+      r[a] = t;
+    }
+    double kf[FZ];
+    for (int a = 0; a < mk; ++a) kf[a] = r[a];
+    fchol_solve(mk, s->Lr, kf);
+    for (int a = 0; a < mk; ++a) kf[a] = -kf[a];
+    if (k > 0) {
+      for (int a = 0; a < nu; ++a) s->kf[a] = kf[a];
+      double pn[FX];
+      for (int i = 0; i < nx; ++i) {
+        double t = s->g[i];
+        for (int q = 0; q < nx; ++q) t += s->A[q * nx + i] * v[q];
+        for (int a = 0; a < nu; ++a) t += s->K[a * nx + i] * r[a];
+        pn[i] = t;
+      }
+      memcpy(p, pn, sizeof(p));
+    } else {
+      for (int a = 0; a < mk; ++a) s->d[a] = kf[a];
+    }
+    for (int j = 0; j < ne; ++j) {
+      double t = 0; for (int a = 0; a < mk; ++a) t += s->Y[a * ne + j] * kf[a];
+      lin[j] += t;
+    }
+  }
+  /* nu = S^-1 (E d_N^0 - e_N) */
+  if (ne > 0) {
+    double Sc[FX * FX], rhsn[FX];
+    memcpy(Sc, P->S, sizeof(double) * ne * ne);
+    if (fchol(ne, Sc)) return -1;
+    for (int j = 0; j < ne; ++j) rhsn[j] = lin[j] + P->lin_e[j] - rs * P->st[N].e0[j];
+    fchol_solve(ne, Sc, rhsn);
+    for (int j = 0; j < ne; ++j) nu_new[j] = rhsn[j];
+  }
+  /* forward pass */
+  {
+    fstage_t* s0 = &P->st[0];
+    double w[FZ], dx[FX];
+    for (int a = 0; a < m0; ++a) {
+      double t = s0->d[a];
+      for (int j = 0; j < ne; ++j) t -= s0->M[a * ne + j] * nu_new[j];
+      w[a] = t;
+    }
+    for (int a = 0; a < m0; ++a) s0->d[a] = w[a];
+    for (int i = 0; i < nx; ++i) {
+      double t = rs * s0->e0[i];
+      for (int a = 0; a < m0; ++a) t += s0->F0[i * m0 + a] * w[a];
+      dx[i] = t;
+    }
+    for (int k = 1; k < N; ++k) {
+      fstage_t* s = &P->st[k];
+      double du[FU], dn[FX];
+      for (int a = 0; a < nu; ++a) {
+        double t = s->kf[a];
+        for (int i = 0; i < nx; ++i) t += s->K[a * nx + i] * dx[i];
+        for (int j = 0; j < ne; ++j) t -= s->M[a * ne + j] * nu_new[j];
+        du[a] = t;
+      }
+      for (int i = 0; i < nx; ++i) s->d[i] = dx[i];
+      for (int a = 0; a < nu; ++a) s->d[nx + a] = du[a];
+      for (int i = 0; i < nx; ++i) {
+        double t = rs * s->e0[i];
+        for (int q = 0; q < nx; ++q) t += s->A[i * nx + q] * dx[q];
+        for (int a = 0; a < nu; ++a) t += s->B[i * nu + a] * du[a];
+        dn[i] = t;
+      }
+      memcpy(dx, dn, sizeof(dx));
+    }
+    for (int i = 0; i < nx; ++i) P->st[N].d[i] = dx[i];
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* interior-point QP (qp_solve of vboc_oracle.c over the generalised stage variables)           */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct { double n, d; } fratio_t;
+static void fr_add(fratio_t* m, double t, double dt) {
+  if (dt < 0.0 && t * m->d < m->n * (-dt)) { m->n = t; m->d = -dt; }
+}
+
+static int fqp(fprob_t* P, int* iters) {
+  const int nx = P->nx, nu = P->nu, ne = P->ne, N = P->N, m0 = P->nf0 + nu;
+  const vboc_opts_t* o = &P->o;
+  const double rho = o->lm;
+  int nbox = 0;
+  for (int k = 0; k <= N; ++k) {
+    fstage_t* s = &P->st[k];
+    for (int i = 0; i < fnz(P, k); ++i) {
+      double v, lb, ub; int boxed;
+      fcomp(P, k, i, &v, &lb, &ub, &boxed);
+      if (!boxed) { s->dz[i] = 0.0; s->ql[i] = s->qu[i] = 0.0; s->Lb[i] = -INFINITY; s->Ub[i] = INFINITY; continue; }
+      const double L = lb - v, U = ub - v, del = o->ipm_push * (U - L);
+      double z0 = 0.0;
+      if (z0 < L + del) z0 = L + del;
+      if (z0 > U - del) z0 = U - del;
+      s->Lb[i] = L; s->Ub[i] = U; s->dz[i] = z0;
+      s->ql[i] = o->mu0 / (z0 - L);
+      s->qu[i] = o->mu0 / (U - z0);
+      nbox += 2;
+    }
+  }
+  for (int j = 0; j < ne; ++j) P->qnu[j] = 0.0;
+  double e00 = 0.0, rd0 = 0.0;
+  for (int k = 0; k < N; ++k) {
+    fstage_t* s = &P->st[k];
+    const fstage_t* s1 = &P->st[k + 1];
+    for (int i = 0; i < nx; ++i) {
+      double t = s->b[i] - s1->dz[i];
+      if (k == 0) for (int a = 0; a < m0; ++a) t += s->F0[i * m0 + a] * s->dz[a];
+      else {
+        for (int q = 0; q < nx; ++q) t += s->A[i * nx + q] * s->dz[q];
+        for (int a = 0; a < nu; ++a) t += s->B[i * nu + a] * s->dz[nx + a];
+      }
+      s->e0[i] = t;
+      e00 = fmax(e00, fabs(t));
+    }
+  }
+  for (int j = 0; j < ne; ++j) {
+    const double t = P->ev[j] - P->st[N].x[P->ei[j]] - P->st[N].dz[P->ei[j]];
+    P->st[N].e0[j] = t;
+    e00 = fmax(e00, fabs(t));
+  }
+  for (int k = 0; k <= N; ++k) {
+    const fstage_t* s = &P->st[k];
+    for (int i = 0; i < fnz(P, k); ++i)
+      rd0 = fmax(rd0, fabs(rho * s->dz[i] + fgrad(P, k, i) - s->ql[i] + s->qu[i]));
+  }
+  P->rs = 1.0;
+  int it, status = 1;
+  double nu_new[FX] = {0};
+  for (it = 0; it < o->qp_max_iter; ++it) {
+    double mu = 0.0;
+    for (int k = 0; k <= N; ++k) {
+      const fstage_t* s = &P->st[k];
+      for (int i = 0; i < fnz(P, k); ++i) {
+        if (!isfinite(s->Lb[i])) continue;
+        mu += (s->dz[i] - s->Lb[i]) * s->ql[i] + (s->Ub[i] - s->dz[i]) * s->qu[i];
+      }
+    }
+    mu /= (double)nbox;
+    if (!isfinite(mu)) { status = -1; break; }
+    if (mu < o->qp_tol_comp && P->rs * rd0 < o->qp_tol_stat && P->rs * e00 < o->qp_tol_eq) { status = 0; break; }
+    for (int k = 0; k <= N; ++k) {
+      fstage_t* s = &P->st[k];
+      for (int i = 0; i < fnz(P, k); ++i) {
+        double H = rho;
+        const double g = rho * s->dz[i] + fgrad(P, k, i);
+        if (isfinite(s->Lb[i])) H += s->ql[i] / (s->dz[i] - s->Lb[i]) + s->qu[i] / (s->Ub[i] - s->dz[i]);
+        s->H[i] = H; s->g[i] = g;
+      }
+    }
+    if (fnewton(P, 1, nu_new)) { status = -1; break; }
+    fratio_t ma = {1.0, 1.0};
+    for (int k = 0; k <= N; ++k) {
+      fstage_t* s = &P->st[k];
+      for (int i = 0; i < fnz(P, k); ++i) {
+        s->daff[i] = s->d[i];
+        if (!isfinite(s->Lb[i])) continue;
+        const double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], d = s->d[i];
+        const double dll = -s->ql[i] - s->ql[i] * d / tl, dlu = -s->qu[i] + s->qu[i] * d / tu;
+        fr_add(&ma, tl, d);
+        fr_add(&ma, tu, -d);
+        fr_add(&ma, s->ql[i], dll);
+        fr_add(&ma, s->qu[i], dlu);
+      }
+    }
+    const double aa = ma.n / ma.d;
+    double muaff = 0.0;
+    for (int k = 0; k <= N; ++k) {
+      const fstage_t* s = &P->st[k];
+      for (int i = 0; i < fnz(P, k); ++i) {
+        if (!isfinite(s->Lb[i])) continue;
+        const double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], d = s->d[i];
+        const double dll = -s->ql[i] - s->ql[i] * d / tl, dlu = -s->qu[i] + s->qu[i] * d / tu;
+        muaff += (tl + aa * d) * (s->ql[i] + aa * dll) + (tu - aa * d) * (s->qu[i] + aa * dlu);
+      }
+    }
+    muaff /= (double)nbox;
+    double sig = muaff / mu;
+    sig = sig * sig * sig;
+    if (sig > 1.0) sig = 1.0;
+    const double smu = sig * mu;
+    for (int k = 0; k <= N; ++k) {
+      fstage_t* s = &P->st[k];
+      for (int i = 0; i < fnz(P, k); ++i) {
+        if (!isfinite(s->Lb[i])) continue;
+        const double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu, d = s->daff[i];
+        const double dll = -s->ql[i] - s->ql[i] * d * itl, dlu = -s->qu[i] + s->qu[i] * d * itu;
+        const double rl = smu - tl * s->ql[i] - d * dll, ru = smu - tu * s->qu[i] + d * dlu;
+        s->g[i] = rho * s->dz[i] + fgrad(P, k, i) - s->ql[i] - rl * itl + s->qu[i] + ru * itu;
+      }
+    }
+    if (fnewton(P, 0, nu_new)) { status = -1; break; }
+    fratio_t mx = {1.0, o->ipm_tau};
+    for (int k = 0; k <= N; ++k) {
+      const fstage_t* s = &P->st[k];
+      for (int i = 0; i < fnz(P, k); ++i) {
+        if (!isfinite(s->Lb[i])) continue;
+        const double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu;
+        const double d = s->d[i], da = s->daff[i];
+        const double dlla = -s->ql[i] - s->ql[i] * da * itl, dlua = -s->qu[i] + s->qu[i] * da * itu;
+        const double rl = smu - tl * s->ql[i] - da * dlla, ru = smu - tu * s->qu[i] + da * dlua;
+        const double dll = (rl - s->ql[i] * d) * itl, dlu = (ru + s->qu[i] * d) * itu;
+        fr_add(&mx, tl, d);
+        fr_add(&mx, tu, -d);
+        fr_add(&mx, s->ql[i], dll);
+        fr_add(&mx, s->qu[i], dlu);
+      }
+    }
+    const double alpha = fmin(1.0, o->ipm_tau * (mx.n / mx.d));
+    for (int k = 0; k <= N; ++k) {
+      fstage_t* s = &P->st[k];
+      for (int i = 0; i < fnz(P, k); ++i) {
+        const double d = s->d[i];
+        if (isfinite(s->Lb[i])) {
+          const double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu, da = s->daff[i];
+          const double dlla = -s->ql[i] - s->ql[i] * da * itl, dlua = -s->qu[i] + s->qu[i] * da * itu;
+          const double rl = smu - tl * s->ql[i] - da * dlla, ru = smu - tu * s->qu[i] + da * dlua;
+          s->ql[i] += alpha * (rl - s->ql[i] * d) * itl;
+          s->qu[i] += alpha * (ru + s->qu[i] * d) * itu;
+        }
+        s->dz[i] += alpha * d;
+      }
+    }
+    for (int j = 0; j < ne; ++j) P->qnu[j] += alpha * (nu_new[j] - P->qnu[j]);
+    P->rs *= (1.0 - alpha);
+  }
+  *iters = it;
+  if (status < 0) return -1;
+  /* costates by the backward adjoint from the final iterate */
+  {
+    double lam[FX];
+    const fstage_t* sN = &P->st[N];
+    for (int i = 0; i < nx; ++i) lam[i] = rho * sN->dz[i] - sN->ql[i] + sN->qu[i];
+    for (int j = 0; j < ne; ++j) lam[P->ei[j]] += P->qnu[j];
+    for (int k = N - 1; k >= 0; --k) {
+      fstage_t* s = &P->st[k];
+      memcpy(s->qpi, lam, sizeof(lam));
+      if (k == 0) break;
+      double ln[FX];
+      for (int i = 0; i < nx; ++i) {
+        double t = rho * s->dz[i] + fgrad(P, k, i) - s->ql[i] + s->qu[i];
+        for (int q = 0; q < nx; ++q) t += s->A[q * nx + i] * lam[q];
+        ln[i] = t;
+      }
+      memcpy(lam, ln, sizeof(lam));
+    }
+  }
+  for (int k = 0; k <= N; ++k)
+    for (int i = 0; i < fnz(P, k); ++i)
+      if (!isfinite(P->st[k].dz[i]) || !isfinite(P->st[k].ql[i]) || !isfinite(P->st[k].qu[i])) return -1;
+  return status;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* SQP with L1 merit backtracking                                                              */
+/* ------------------------------------------------------------------------------------------ */
+
+/* x_k + alpha dx_k of the stage state (stage 0: only the free components move) */
+static void fstate_at(const fprob_t* P, int k, double alpha, double* x, double* u) {
+  const fstage_t* s = &P->st[k];
+  const int nx = P->nx, nu = P->nu;
+  if (k == 0) {
+    for (int i = 0; i < nx; ++i) x[i] = s->x[i];
+    for (int j = 0; j < P->nf0; ++j) x[P->f0[j]] += alpha * s->dz[j];
+    for (int a = 0; a < nu; ++a) u[a] = s->u[a] + alpha * s->dz[P->nf0 + a];
+    return;
+  }
+  for (int i = 0; i < nx; ++i) x[i] = s->x[i] + alpha * s->dz[i];
+  if (k < P->N) for (int a = 0; a < nu; ++a) u[a] = s->u[a] + alpha * s->dz[nx + a];
+}
+
+static double fmerit(const fprob_t* P, double alpha) {
+  const int nx = P->nx, N = P->N;
+  double xk[FX], uk[FU], xn[FX], un[FU], phi[FX];
+  double val = 0.0, viol = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    const fstage_t* st = &P->st[k];
+    for (int i = 0; i < fnz(P, k); ++i) {
+      double v, lb, ub; int boxed;
+      fcomp(P, k, i, &v, &lb, &ub, &boxed);
+      if (!boxed) continue;
+      v += alpha * st->dz[i];
+      viol += fmax(0.0, lb - v) + fmax(0.0, v - ub);
+    }
+  }
+  val += P->wbnd * viol;
+  fstate_at(P, 0, alpha, xk, uk);
+  for (int i = 0; i < nx; ++i) val += P->c0[i] * xk[i];
+  for (int k = 0; k < N; ++k) {
+    ft_rk4(P->nq, xk, uk, phi);
+    fstate_at(P, k + 1, alpha, xn, un);
+    for (int i = 0; i < nx; ++i) val += P->st[k].wpi[i] * fabs(phi[i] - xn[i]);
+    if (k + 1 < N) for (int i = 0; i < nx; ++i) val += P->cp[i] * xn[i];
+    memcpy(xk, xn, sizeof(xk));
+    memcpy(uk, un, sizeof(uk));
+  }
+  for (int j = 0; j < P->ne; ++j) val += P->wnu[j] * fabs(xk[P->ei[j]] - P->ev[j]);
+  return val;
+}
+
+static double fwupd(double w, double lam) {
+  const double a = fabs(lam), b = 0.5 * (w + a);
+  return a > b ? a : b;
+}
+
+static void fsqp(fprob_t* P, vboc_result_t* res) {
+  const int nx = P->nx, nu = P->nu, N = P->N;
+  const vboc_opts_t* o = &P->o;
+  int status = 2, it, qp_total = 0;
+  double rstat = 0, req = 0, rineq = 0, rcomp = 0;
+  for (it = 0;; ++it) {
+    flinearize(P);
+    fresiduals(P, &rstat, &req, &rineq, &rcomp);
+    if (!isfinite(rstat) || !isfinite(req)) { status = 1; break; }
+    if (rstat < o->tol_stat && req < o->tol_eq && rineq < o->tol_ineq && rcomp < o->tol_comp) { status = 0; break; }
+    if (it >= o->max_iter) { status = 2; break; }
+    int qit = 0;
+    const int qs = fqp(P, &qit);
+    qp_total += qit;
+    if (qs < 0) { status = 4; break; }
+    double lmax = 0.0;
+    for (int k = 0; k <= N; ++k) {
+      fstage_t* s = &P->st[k];
+      if (k < N) for (int i = 0; i < nx; ++i) s->wpi[i] = fwupd(s->wpi[i], s->qpi[i]);
+      for (int i = 0; i < fnz(P, k); ++i) lmax = fmax(lmax, fmax(s->ql[i], s->qu[i]));
+    }
+    for (int j = 0; j < P->ne; ++j) P->wnu[j] = fwupd(P->wnu[j], P->qnu[j]);
+    P->wbnd = fwupd(P->wbnd, lmax);
+    const double phi0 = fmerit(P, 0.0);
+    double alpha = 1.0;
+    for (;;) {
+      const double pa = fmerit(P, alpha);
+      if (pa < phi0) break;
+      if (alpha * o->alpha_reduction < o->alpha_min) break;
+      alpha *= o->alpha_reduction;
+    }
+    for (int k = 0; k <= N; ++k) {
+      fstage_t* s = &P->st[k];
+      double x[FX], u[FU];
+      fstate_at(P, k, alpha, x, u);
+      memcpy(s->x, x, sizeof(double) * nx);
+      if (k < N) memcpy(s->u, u, sizeof(double) * nu);
+      for (int i = 0; i < fnz(P, k); ++i) {
+        s->ll[i] += alpha * (s->ql[i] - s->ll[i]);
+        s->lu[i] += alpha * (s->qu[i] - s->lu[i]);
+      }
+      if (k < N) for (int i = 0; i < nx; ++i) s->pi[i] += alpha * (s->qpi[i] - s->pi[i]);
+    }
+    for (int j = 0; j < P->ne; ++j) P->tnu[j] += alpha * (P->qnu[j] - P->tnu[j]);
+    if (!isfinite(P->st[0].x[nx - 1])) { status = 1; break; }
+  }
+  res->status = status;
+  res->sqp_iter = it;
+  res->qp_iter = qp_total;
+  res->cost = fcost(P);
+  res->res_stat = rstat; res->res_eq = req; res->res_ineq = rineq; res->res_comp = rcomp;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* public entry points                                                                         */
+/* ------------------------------------------------------------------------------------------ */
+
+void vboc_oracle_ft_rk4_sens(int nq, const double* x, const double* u, double* x1, double* A, double* B) {
+  ft_rk4_sens(nq, x, u, x1, A, B);
+}
+
+/* Layout as vboc_oracle_solve (nx = 2 nq + 1 with the dt column, p = [w_1..w_nq, w_t]). */
+int vboc_oracle_ft_solve(int nq, int N, const double* x_guess, const double* u_guess, const double* p,
+                         const double* lbx, const double* ubx, const double* lbu, const double* ubu,
+                         const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
+                         const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res) {
+  if (nq < 1 || nq > FQ || N < 1) return -1;
+  const int nx = 2 * nq + 1, nu = nq;
+  for (int i = 0; i < nx; ++i) if (!(lbx[i] < ubx[i]) || !(lbx0[i] <= ubx0[i]) || !(lbxe[i] <= ubxe[i])) return -2;
+  for (int a = 0; a < nu; ++a) if (!(lbu[a] < ubu[a])) return -2;
+  fprob_t P;
+  memset(&P, 0, sizeof(P));
+  P.nq = nq; P.nx = nx; P.nu = nu; P.N = N; P.o = *opts;
+  for (int i = 0; i < nx; ++i) {
+    P.xlb[i] = lbx[i]; P.xub[i] = ubx[i]; P.x0lb[i] = lbx0[i]; P.x0ub[i] = ubx0[i];
+    P.xNlb[i] = lbxe[i]; P.xNub[i] = ubxe[i];
+    if (lbx0[i] < ubx0[i]) P.f0[P.nf0++] = i;
+    if (lbxe[i] == ubxe[i]) { P.xNfix[i] = 1; P.ei[P.ne] = i; P.ev[P.ne] = lbxe[i]; P.ne++; }
+  }
+  for (int a = 0; a < nu; ++a) { P.ulb[a] = lbu[a]; P.uub[a] = ubu[a]; }
+  for (int j = 0; j < nq; ++j) P.c0[nq + j] = p[j];
+  P.c0[2 * nq] = p[nq];
+  P.cp[2 * nq] = p[nq];
+  P.st = (fstage_t*)calloc((size_t)N + 1, sizeof(fstage_t));
+  if (!P.st) return -3;
+  for (int k = 0; k <= N; ++k) {
+    for (int i = 0; i < nx; ++i) P.st[k].x[i] = x_guess[k * nx + i];
+    if (k < N) for (int a = 0; a < nu; ++a) P.st[k].u[a] = u_guess[k * nu + a];
+  }
+  for (int i = 0; i < nx; ++i) if (!(lbx0[i] < ubx0[i])) P.st[0].x[i] = lbx0[i];   /* fixed at stage 0 */
+  fsqp(&P, res);
+  for (int k = 0; k <= N; ++k) {
+    for (int i = 0; i < nx; ++i) x_out[k * nx + i] = P.st[k].x[i];
+    if (k < N) for (int a = 0; a < nu; ++a) u_out[k * nu + a] = P.st[k].u[a];
+  }
+  free(P.st);
+  return 0;
+}
+
+int vboc_oracle_ft_solve_batch(int nq, int B, int Nmax, const int* N, const double* x_guess,
+                               const double* u_guess, const double* p, const double* lbx, const double* ubx,
+                               const double* lbu, const double* ubu, const double* lbx0, const double* ubx0,
+                               const double* lbxe, const double* ubxe, const vboc_opts_t* opts, int nthreads,
+                               double* x_out, double* u_out, vboc_result_t* res) {
+  const int nxr = 2 * nq + 1, npr = nq + 1;
+  int err = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(| : err)
+  for (int b = 0; b < B; ++b) {
+    const size_t xo = (size_t)b * (Nmax + 1) * nxr, uo = (size_t)b * Nmax * nq;
+    const int r = vboc_oracle_ft_solve(nq, N[b], x_guess + xo, u_guess + uo, p + (size_t)b * npr,
+                                       lbx + (size_t)b * nxr, ubx + (size_t)b * nxr, lbu + (size_t)b * nq,
+                                       ubu + (size_t)b * nq, lbx0 + (size_t)b * nxr, ubx0 + (size_t)b * nxr,
+                                       lbxe + (size_t)b * nxr, ubxe + (size_t)b * nxr, opts, x_out + xo,
+                                       u_out + uo, res + b);
+    if (r == -2) { res[b].status = 5; res[b].sqp_iter = 0; res[b].qp_iter = 0; res[b].cost = NAN; }
+    else if (r) err |= 1;
+  }
+  return err ? -1 : 0;
+}

@@ -21,8 +21,12 @@ drop-in classes (vboc_amd.ocp.OCP<sys>INIT / OCPpendulum) with the oracle inject
 machine AND the drop-in classes' mapping of the ACADOS calls onto the solver.  `random` serves the
 problem's stream-1 block (ics.heldout_ics) and then the restart stream (drivers.TEST_STREAM).
 
-Usage: python tests/golden/make_driver_golden.py [dg|test]
-  ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json
+The pendulum's data generation (VBOC/pendulum_vboc.py:52-205) lives in the script's main block, not in a
+function: its `for v_sel in [v_min, v_max]:` loop is taken by AST and run against the drop-in
+OCPpendulum (free-time OCP_solve) with the oracle's free-time solver injected; the fixture is X_save.
+
+Usage: python tests/golden/make_driver_golden.py [dg|test|pend]
+  ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json, tests/golden/driver_1.json
 """
 import ast
 import json
@@ -196,9 +200,40 @@ def main_testing():
                        "results": out}, f)
 
 
+def extract_pendulum_sweep(path):
+    """The data-generation loop `for v_sel in [v_min, v_max]:` of VBOC/pendulum_vboc.py's main block
+    (:52-205), taken by AST from the file's text."""
+    tree = ast.parse(open(path).read())
+    main_if = [n for n in tree.body if isinstance(n, ast.If)][-1]
+    loop = [n for n in main_if.body if isinstance(n, ast.For) and isinstance(n.target, ast.Name)
+            and n.target.id == "v_sel"][0]
+    return compile(ast.Module(body=[loop], type_ignores=[]), path, "exec")
+
+
+def main_pendulum():
+    """Pendulum VBOC data generation (free-time OCPs): the reference's own loop on the drop-in
+    OCPpendulum (free-time OCP_solve) with the oracle's free-time solver injected."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_backend import OracleOcpBackend
+    from vboc_amd import ocp as dropin
+    from vboc_amd.drivers import PEND_EPS, PEND_N_START
+    dropin.use_backend(OracleOcpBackend())
+    code = extract_pendulum_sweep(os.path.join(REF, "pendulum_vboc.py"))
+    ocp = dropin.OCPpendulum()
+    g = dict(np=np, ocp=ocp, N_start=PEND_N_START, v_max=ocp.dthetamax, v_min=-ocp.dthetamax,
+             q_max=ocp.thetamax, q_min=ocp.thetamin, eps=PEND_EPS, X_save=np.empty((0, 2)))
+    exec(code, g)
+    X = g["X_save"]
+    print("pendulum X_save", X.shape, flush=True)
+    with open(os.path.join(HERE, "driver_1.json"), "w") as f:
+        json.dump({"nq": 1, "N_start": PEND_N_START, "eps": PEND_EPS, "X_save": X.tolist()}, f)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("dg", "all"):
         main()
     if what in ("test", "all"):
         main_testing()
+    if what in ("pend", "all"):
+        main_pendulum()

@@ -121,6 +121,26 @@ def rk4(fun, x, u, h):
     return x + h / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
 
 
+def rk4_jac(fun, jac, x, u, h):
+    """d RK4(x, u) / d(x, u) by forward sensitivities through the reference's own Jacobian `jac`."""
+    nx, nu = len(x), len(u)
+    E = np.vstack([np.hstack([np.zeros((nu, nx)), np.eye(nu)])])
+    I = np.hstack([np.eye(nx), np.zeros((nx, nu))])
+    Jf = lambda xx: np.asarray(jac(list(xx), list(u)), dtype=float)
+    dk = lambda xx, dX: Jf(xx) @ np.vstack([dX, E])
+    k1 = fun(x, u)
+    d1 = dk(x, I)
+    X2 = x + 0.5 * h * k1
+    k2 = fun(X2, u)
+    d2 = dk(X2, I + 0.5 * h * d1)
+    X3 = x + 0.5 * h * k2
+    k3 = fun(X3, u)
+    d3 = dk(X3, I + 0.5 * h * d2)
+    X4 = x + h * k3
+    d4 = dk(X4, I + h * d3)
+    return I + h / 6.0 * (d1 + 2 * d2 + 2 * d3 + d4)
+
+
 def main():
     rng = np.random.default_rng(20250124)
     flops = {}
@@ -157,6 +177,8 @@ def main():
         # one shooting interval of the OCP model (dt state, tf/N = 1): RK4 with h = 1 on f
         fx = lambda x7, uu: np.asarray(f_num(list(x7), list(uu)), dtype=float).ravel()
         out["shoot_x1"] = np.array([rk4(fx, X[i], ctrl[i], 1.0) for i in range(npts)])
+        # its Jacobian w.r.t. (x incl. the dt state, u): the free-time OCP's A_k | B_k
+        out["shoot_jac"] = np.array([rk4_jac(fx, J_num, X[i], ctrl[i], 1.0) for i in range(npts)])
         out["consts"] = np.array(json.dumps(m["consts"]))
         np.savez(os.path.join(HERE, f"dynamics_{nq}.npz"), **out)
         flops[str(nq)] = {"C_f": cse_ops(list(f)), "C_fJ": cse_ops(list(f) + list(J)),

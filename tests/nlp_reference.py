@@ -69,3 +69,60 @@ def slsqp(nq, b, i, maxiter=500):
                  constraints=[dict(type="eq", fun=eq, jac=eqjac)], method="SLSQP",
                  options=dict(maxiter=maxiter, ftol=1e-10))
     return r.fun, bool(r.success), float(np.abs(eq(r.x)).max())
+
+
+def slsqp_free_time(b, i, maxiter=500, start=None):
+    """The free-time pendulum OCP (OCPpendulum.OCP_solve, VBOC/pendulum_class_vboc.py:107-130) as one
+    NLP for scipy SLSQP: z = (x_0..x_N, u_0..u_{N-1}) with x = [theta, dtheta, dt]; equalities
+    x_{k+1} = Phi(x_k, u_k) (RK4 with h = dt, oracle.ft_rk4_sens), stage-0 and terminal components with
+    lb == ub; boxes; cost p[0] dtheta_0 + p[1] sum_{k<N} dt_k.  Returns (cost, success, max eq viol,
+    x_0).  start: optional (x [N+1, 3], u [N, 1]) initial point (default: the batch's guess; SLSQP does
+    not find a feasible point from the straight-line guess of these minimum-time problems)."""
+    N, nx, nu = int(b["N"][i]), 3, 1
+    nv = (N + 1) * nx + N * nu
+    p = b["p"][i]
+    c = np.zeros(nv)
+    c[1] = p[0]
+    for k in range(N):
+        c[k * nx + 2] += p[1]
+    fix0 = [j for j in range(nx) if b["lbx0"][i, j] == b["ubx0"][i, j]]
+    fixN = [j for j in range(nx) if b["lbxe"][i, j] == b["ubxe"][i, j]]
+    X = lambda z: z[:(N + 1) * nx].reshape(N + 1, nx)
+    U = lambda z: z[(N + 1) * nx:].reshape(N, nu)
+
+    def eq(z):
+        x, u = X(z), U(z)
+        r = [x[k + 1] - oracle.ft_rk4_sens(1, x[k], u[k])[0] for k in range(N)]
+        r.append(np.array([x[0, j] - b["lbx0"][i, j] for j in fix0] + [x[N, j] - b["lbxe"][i, j] for j in fixN]))
+        return np.concatenate(r)
+
+    def eqjac(z):
+        x, u = X(z), U(z)
+        J = np.zeros((N * nx + len(fix0) + len(fixN), nv))
+        for k in range(N):
+            _, A, B = oracle.ft_rk4_sens(1, x[k], u[k])
+            r = slice(k * nx, (k + 1) * nx)
+            J[r, k * nx:(k + 1) * nx] = -A
+            J[r, (k + 1) * nx:(k + 2) * nx] += np.eye(nx)
+            J[r, (N + 1) * nx + k * nu:(N + 1) * nx + (k + 1) * nu] = -B
+        row = N * nx
+        for j in fix0:
+            J[row, j] = 1.0
+            row += 1
+        for j in fixN:
+            J[row, N * nx + j] = 1.0
+            row += 1
+        return J
+
+    bounds = []
+    for k in range(N + 1):
+        lo, hi = (b["lbx0"][i], b["ubx0"][i]) if k == 0 else ((b["lbxe"][i], b["ubxe"][i]) if k == N else
+                                                                (b["lbx"][i], b["ubx"][i]))
+        bounds += [(lo[j], hi[j]) for j in range(nx)]
+    bounds += [(b["lbu"][i, 0], b["ubu"][i, 0])] * N
+    xs, us = start if start is not None else (b["x_guess"][i, :N + 1], b["u_guess"][i, :N])
+    z0 = np.r_[np.ravel(xs), np.ravel(us)]
+    z0 = np.clip(z0, [bb[0] for bb in bounds], [bb[1] for bb in bounds])
+    r = minimize(lambda z: c @ z, z0, jac=lambda z: c, bounds=bounds, constraints=[dict(type="eq", fun=eq, jac=eqjac)],
+                 method="SLSQP", options=dict(maxiter=maxiter, ftol=1e-12))
+    return r.fun, bool(r.success), float(np.abs(eq(r.x)).max()), X(r.x)[0]

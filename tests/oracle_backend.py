@@ -20,10 +20,11 @@ def forced_failure(q0, fail_mod):
     return fail_mod > 0 and int(abs(float(q0)) * 1e6) % fail_mod == 0
 
 
-def _oracle_solve(nq, b, fail_mod=0):
+def _oracle_solve(nq, b, fail_mod=0, free_time=False):
     import oracle
     xo, uo, r = oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"],
-                                   b["lbu"], b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"])
+                                   b["lbu"], b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"],
+                                   free_time=free_time)
     st = np.array(r["status"], copy=True)
     for i in range(st.shape[0]):
         if forced_failure(b["lbx0"][i, 0], fail_mod):
@@ -38,8 +39,8 @@ class OracleBackend:
     def __init__(self, nq, fail_mod=0):
         self.nq, self.fail_mod = nq, fail_mod
 
-    def solve(self, b):
-        return _oracle_solve(self.nq, b, self.fail_mod)
+    def solve(self, b, free_time=False):
+        return _oracle_solve(self.nq, b, self.fail_mod, free_time)
 
     def rk4(self, x, u, T):
         import oracle
@@ -52,9 +53,9 @@ class OracleOcpBackend:
     def __init__(self, fail_mod=0):
         self.fail_mod = fail_mod
 
-    def solve_host(self, b):
+    def solve_host(self, b, free_time=False):
         nq = b["u_guess"].shape[2]
-        return _oracle_solve(nq, b, self.fail_mod)
+        return _oracle_solve(nq, b, self.fail_mod, free_time)
 
     def rk4(self, nq, T, x, u):
         import oracle

@@ -82,5 +82,9 @@ def test_unsupported_structures_raise(oracle_dropin):
         S.solve()
     with pytest.raises(NotImplementedError):
         S.set_new_time_steps(np.full(N, 0.5))
-    with pytest.raises(NotImplementedError):
-        oracle_dropin.OCPpendulum().OCP_solve(None, None, None, None, None, None, None)
+    S.set_new_time_steps(np.full(N, 1.0))
+    ocp.OCP_solve(*args)
+    for k in range(1, N):
+        S.constraints_set(k, "lbx", lb)
+    with pytest.raises(NotImplementedError):              # free time + general constraint C
+        S.solve()

@@ -200,3 +200,80 @@ def test_full_batch_properties():
     v0 = X[:, 0, nq:]
     assert np.abs(v0 - d * np.sum(d * v0, 1, keepdims=True)).max() < 1e-9
     np.testing.assert_allclose(g["cost"][ok], np.sum(b["p"][ok, :nq] * v0, 1), atol=1e-9)
+
+
+# ---- free-time OCP (OCPpendulum.OCP_solve, vboc_solve_batch_ft) --------------------------------------
+def _ft_batch(B, N_range=(20, 60)):
+    from vboc_amd.ics import pendulum_free_time_ics
+    return pendulum_free_time_ics(np.arange(B), N_range)
+
+
+def test_free_time_parity_with_oracle():
+    """Same bars as the boundary solver (module docstring), on free-time pendulum OCPs."""
+    import oracle
+    from vboc_amd import lib
+    b = _ft_batch(256)
+    s = lib.Solver(1, int(b["N"].max()))
+    g = s.solve_host(b, free_time=True)
+    s.close()
+    xo, uo, r = oracle.solve_batch(1, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                                   b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], free_time=True)
+    assert np.mean(g["status"] == r["status"]) >= 0.98, (g["status"], r["status"])
+    assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= 0.95
+    both = (g["status"] == 0) & (r["status"] == 0)
+    assert both.mean() >= 0.9
+    dc = np.abs(g["cost"] - r["cost"])[both]
+    dx = np.abs(g["x"][:, 0] - xo[:, 0]).max(axis=1)[both]
+    assert np.median(dc) <= 1e-9 and dc.max() <= 2e-3, (np.median(dc), dc.max())
+    assert np.median(dx) <= 1e-9 and dx.max() <= 2e-3
+    # one dt along every solution, rest at q_fin
+    for i in np.where(both)[0][:16]:
+        N = b["N"][i]
+        assert np.ptp(g["x"][i, :N + 1, 2]) < 1e-9
+        assert abs(g["x"][i, N, 0] - b["lbxe"][i, 0]) < 1e-6 and abs(g["x"][i, N, 1]) < 1e-6
+
+
+def test_free_time_device_path_and_unsupported():
+    import torch
+    from vboc_amd import lib
+    b = _ft_batch(64)
+    b["lbx"][3, 1] = b["ubx"][3, 1]            # a pinned path component: outside the free-time structure
+    s = lib.Solver(1, int(b["N"].max()))
+    h = s.solve_host(b, free_time=True)
+    dev = {k: torch.as_tensor(np.ascontiguousarray(v), device="cuda:0") for k, v in b.items()}
+    d = s.solve_device(dev, free_time=True)
+    torch.cuda.synchronize()
+    s.close()
+    assert h["status"][3] == 5 and d["status"][3].item() == 5
+    np.testing.assert_array_equal(h["status"], d["status"].cpu().numpy())
+    np.testing.assert_array_equal(h["x"], d["x"].cpu().numpy())
+    np.testing.assert_array_equal(h["cost"], d["cost"].cpu().numpy())
+
+
+def test_dropin_pendulum_ocp_solve_on_gpu():
+    import oracle
+    from vboc_amd import ocp
+    b = _ft_batch(4, (50, 50))
+    xo, uo, r = oracle.solve_batch(1, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                                   b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], free_time=True)
+    o = ocp.OCPpendulum()
+    for i in range(4):
+        st = o.OCP_solve(b["x_guess"][i], b["u_guess"][i], b["p"][i, 0], b["lbx"][i], b["ubx"][i],
+                         b["lbx0"][i, 0], b["lbxe"][i, 0])
+        assert st == r["status"][i]
+        if st == 0:
+            assert abs(o.ocp_solver.get_cost() - r["cost"][i]) < 1e-6
+            np.testing.assert_allclose(o.ocp_solver.get(0, "x"), xo[i, 0], atol=1e-6)
+
+
+def test_pendulum_data_generation_on_gpu_matches_reference_loop():
+    """VBOC/pendulum_vboc.py:52-205 through the batched driver on the GPU against the fixture of the
+    reference's own loop (oracle-backed): same samples to 1e-6."""
+    import json
+    import os
+    from vboc_amd.drivers import GpuBackend, pendulum_data_generation
+    fx = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "driver_1.json")))
+    X, stats = pendulum_data_generation(GpuBackend(1, nmax=200), fx["N_start"], fx["eps"])
+    G = np.array(fx["X_save"])
+    assert X.shape == G.shape
+    np.testing.assert_allclose(X, G, atol=1e-6)

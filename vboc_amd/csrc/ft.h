@@ -1,0 +1,869 @@
+// ft.h - free-time box OCP solver: the reference's OCP<sys>.OCP_solve with dt a decision state
+// (OCPpendulum.OCP_solve, VBOC/pendulum_class_vboc.py:107-130; model and options :8-103), batched.
+//
+// Problem (per batch entry, the vboc_batch_t layout of include/vboc.h, nx = 2 nq + 1):
+//   x_k = [theta, dtheta, dt], x_{k+1} = Phi(x_k, u_k) = [RK4 with h = dt of the physics rhs ; dt]
+//   (f_expl = dt * f, one ERK4 step of length 1 per interval, tf = N: :23-40, :55-58);
+//   cost  w . dtheta_0 + wt * sum_{k<N} dt_k  (EXTERNAL cost :70-74, p = [w, wt]);
+//   stage 0: components with lbx_0 == ubx_0 fixed, the others boxed; stages 1..N-1: boxes lbx/ubx
+//   (lb < ub required) and lbu/ubu; stage N: components with lbx_e == ubx_e are terminal equalities,
+//   the others boxed.  No general constraint.
+// Algorithm: the SQP / L1-merit backtracking / Mehrotra interior-point QP / Riccati recursion of the
+// boundary solver (coop.h, oracle/vboc_oracle.c), generalised to free stage-0 components and
+// terminal equalities on any component subset (Schur complement through Pi = E'); restated on the
+// CPU in oracle/vboc_oracle_ft.c (the checker).
+//
+// Execution: one problem per workgroup of one wave (64 lanes), persistent grid pulling problem ids
+// from a global counter.  Stage records live in the workgroup's HBM region; stage-parallel passes
+// (linearisation with the d/d(dt) sensitivity column, residuals, IPM set-up, barrier Hessians,
+// step-length tests, updates, merit re-simulation) put stage k on lane k mod 64 and reduce with
+// cross-lane shuffles; the Riccati recursions (factorisation + two vector/forward sweeps per IPM
+// iteration) and the costate recursion run on lane 0, which issues each stage's loads as one
+// independent batch.  The workload this serves is small (the pendulum's sequential VBOC sweep), so
+// the kernel favours a direct mapping over the wave solver's LDS-ring machinery.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "model.h"
+
+namespace vboc {
+
+template <int NQ>
+struct FtL {
+  static constexpr int NX = 2 * NQ + 1, NU = NQ, NZ = NX + NU, N2 = 2 * NQ;
+  // stage record (doubles)
+  static constexpr int X = 0, U = X + NX, PI = U + NU, LL = PI + NX, LU = LL + NZ, WPI = LU + NZ, A = WPI + NX,
+                       B = A + NX * NX, BD = B + NX * NU, LB = BD + NX, UB = LB + NZ, DZ = UB + NZ, QL = DZ + NZ,
+                       QU = QL + NZ, E0 = QU + NZ, H = E0 + NX, G = H + NZ, D = G + NZ, DAFF = D + NZ, K = DAFF + NZ,
+                       KF = K + NU * NX, LR = KF + NU, M = LR + NZ * NZ, Y = M + NZ * NX, PE = Y + NZ * NX,
+                       QPI = PE + NX, F0 = QPI + NX, REC = F0 + NX * NZ;
+  static constexpr long long region_doubles(int nmax) { return (long long)REC * (nmax + 1); }
+};
+
+template <int NQ>
+struct FtShared {
+  static constexpr int NX = FtL<NQ>::NX, NU = FtL<NQ>::NU;
+  int N, nf0, ne, pid, bad;
+  int f0[NX], ei[NX], fix[NX];
+  double ev[NX], c0[NX], cp[NX], x0lb[NX], x0ub[NX], xlb[NX], xub[NX], xNlb[NX], xNub[NX], ulb[NU], uub[NU];
+  double tnu[NX], wnu[NX], qnu[NX], nun[NX], S[NX * NX], lin_e[NX];
+  double wbnd, rs;
+  int qp_fail;
+};
+
+__device__ __forceinline__ double ft_wmax(double v) {
+  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ double ft_wsum(double v) {
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// running minimum of t / (-dt) over dt < 0, kept as (n, d) (the oracle's fr_add comparison)
+struct FtRatio {
+  double n, d;
+  __device__ void add(double t, double dt) {
+    if (dt < 0.0 && t * d < n * (-dt)) { n = t; d = -dt; }
+  }
+  __device__ double reduce() {
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double n2 = __shfl_xor(n, o), d2 = __shfl_xor(d, o);
+      if (n2 * d < n * d2) { n = n2; d = d2; }
+    }
+    return n / d;
+  }
+};
+
+// Phi(x, u) of the free-time model and its exact Jacobians A = dPhi/dx (last column d/d(dt)), B = dPhi/du
+template <int NQ>
+__device__ void ft_rk4_sens(const double* x, const double* u, double* phi, double* A, double* B) {
+  constexpr int N2 = 2 * NQ, NX = N2 + 1, NU = NQ, NC = N2 + NU + 1, CU = N2, CH = N2 + NU;
+  const double h = x[N2];
+  double ks[N2], Ts[N2][NC], kp[N2], dkp[N2][NC];
+  for (int i = 0; i < N2; ++i) {
+    ks[i] = kp[i] = 0.0;
+    for (int c = 0; c < NC; ++c) Ts[i][c] = dkp[i][c] = 0.0;
+  }
+#pragma unroll 1
+  for (int s = 0; s < 4; ++s) {
+    const double cs = (s == 0) ? 0.0 : (s == 3 ? 1.0 : 0.5), wg = (s == 0 || s == 3) ? 1.0 : 2.0;
+    double X[N2], T[N2][NC];
+    for (int i = 0; i < N2; ++i) {
+      X[i] = x[i] + cs * h * kp[i];
+      for (int c = 0; c < NC; ++c) {
+        double t = cs * h * dkp[i][c];
+        if (c == i) t += 1.0;
+        if (c == CH) t += cs * kp[i];
+        T[i][c] = t;
+      }
+    }
+    double acc[NQ], Jth[NQ * NQ], Jom[NQ * NQ], Ju[NQ * NQ];
+    model_eval<NQ, true>(X, X + NQ, u, acc, Jth, Jom, Ju);
+    for (int j = 0; j < NQ; ++j) { kp[j] = X[NQ + j]; kp[NQ + j] = acc[j]; }
+    for (int c = 0; c < NC; ++c) {
+      for (int j = 0; j < NQ; ++j) dkp[j][c] = T[NQ + j][c];
+      for (int j = 0; j < NQ; ++j) {
+        double t = (c >= CU && c < CU + NQ) ? Ju[j * NQ + (c - CU)] : 0.0;
+        for (int q = 0; q < NQ; ++q) t += Jth[j * NQ + q] * T[q][c] + Jom[j * NQ + q] * T[NQ + q][c];
+        dkp[NQ + j][c] = t;
+      }
+    }
+    for (int i = 0; i < N2; ++i) {
+      ks[i] += wg * kp[i];
+      for (int c = 0; c < NC; ++c) Ts[i][c] += wg * dkp[i][c];
+    }
+  }
+  for (int i = 0; i < N2; ++i) {
+    phi[i] = x[i] + h / 6.0 * ks[i];
+    if (A) {
+      for (int c = 0; c < N2; ++c) A[i * NX + c] = (c == i ? 1.0 : 0.0) + h / 6.0 * Ts[i][c];
+      A[i * NX + N2] = ks[i] / 6.0 + h / 6.0 * Ts[i][CH];
+      for (int a = 0; a < NU; ++a) B[i * NU + a] = h / 6.0 * Ts[i][CU + a];
+    }
+  }
+  phi[N2] = h;
+  if (A) {
+    for (int c = 0; c < NX; ++c) A[N2 * NX + c] = (c == N2) ? 1.0 : 0.0;
+    for (int a = 0; a < NU; ++a) B[N2 * NU + a] = 0.0;
+  }
+}
+
+template <int n>
+__device__ __forceinline__ bool ft_chol(double* A, int m) {   // m <= n used rows/cols, row stride m
+  for (int j = 0; j < m; ++j) {
+    double s = A[j * m + j];
+    for (int k = 0; k < j; ++k) s -= A[j * m + k] * A[j * m + k];
+    if (!(s > 0.0)) return false;
+    const double d = sqrt(s);
+    A[j * m + j] = d;
+    for (int i = j + 1; i < m; ++i) {
+      double t = A[i * m + j];
+      for (int k = 0; k < j; ++k) t -= A[i * m + k] * A[j * m + k];
+      A[i * m + j] = t / d;
+    }
+    for (int i = 0; i < j; ++i) A[i * m + j] = 0.0;
+  }
+  return true;
+}
+__device__ __forceinline__ void ft_chol_solve(const double* L, int m, double* b) {
+  for (int i = 0; i < m; ++i) {
+    double t = b[i];
+    for (int k = 0; k < i; ++k) t -= L[i * m + k] * b[k];
+    b[i] = t / L[i * m + i];
+  }
+  for (int i = m - 1; i >= 0; --i) {
+    double t = b[i];
+    for (int k = i + 1; k < m; ++k) t -= L[k * m + i] * b[k];
+    b[i] = t / L[i * m + i];
+  }
+}
+
+template <int NQ>
+struct Ft {
+  using L = FtL<NQ>;
+  static constexpr int NX = L::NX, NU = L::NU, NZ = L::NZ;
+  FtShared<NQ>& sh;
+  double* g;     // this workgroup's stage records
+  const Opts& o;
+  int t;
+
+  __device__ Ft(FtShared<NQ>& s_, double* g_, const Opts& o_, int t_) : sh(s_), g(g_), o(o_), t(t_) {}
+
+  __device__ __forceinline__ double* rec(int k) const { return g + (long long)k * L::REC; }
+  __device__ __forceinline__ int nz(int k) const { return k == 0 ? sh.nf0 + NU : (k == sh.N ? NX : NX + NU); }
+  // value, bounds, boxed flag of stage variable i of stage k
+  __device__ __forceinline__ bool comp(int k, int i, double& v, double& lb, double& ub) const {
+    const double* r = rec(k);
+    if (k == 0) {
+      if (i < sh.nf0) { const int c = sh.f0[i]; v = r[L::X + c]; lb = sh.x0lb[c]; ub = sh.x0ub[c]; }
+      else { v = r[L::U + i - sh.nf0]; lb = sh.ulb[i - sh.nf0]; ub = sh.uub[i - sh.nf0]; }
+      return true;
+    }
+    if (k == sh.N) {
+      v = r[L::X + i];
+      if (sh.fix[i]) { lb = -INFINITY; ub = INFINITY; return false; }
+      lb = sh.xNlb[i]; ub = sh.xNub[i];
+      return true;
+    }
+    if (i < NX) { v = r[L::X + i]; lb = sh.xlb[i]; ub = sh.xub[i]; }
+    else { v = r[L::U + i - NX]; lb = sh.ulb[i - NX]; ub = sh.uub[i - NX]; }
+    return true;
+  }
+  __device__ __forceinline__ double grad(int k, int i) const {
+    if (k == 0) return i < sh.nf0 ? sh.c0[sh.f0[i]] : 0.0;
+    if (k == sh.N) return 0.0;
+    return i < NX ? sh.cp[i] : 0.0;
+  }
+
+  // ---- set-up / output ------------------------------------------------------------------------
+  __device__ void load(const Inputs& in, int pid) {
+    constexpr int NP = NQ + 1;
+    if (t == 0) {
+      const int N = in.N[pid];
+      sh.N = N; sh.pid = pid; sh.nf0 = 0; sh.ne = 0;
+      const double* p = in.p + (long long)pid * NP;
+      int bad = (N < 1 || N > in.nmax) ? 1 : 0;
+      for (int i = 0; i < NX; ++i) {
+        const long long o = (long long)pid * NX + i;
+        sh.xlb[i] = in.lbx[o]; sh.xub[i] = in.ubx[o]; sh.x0lb[i] = in.lbx0[o]; sh.x0ub[i] = in.ubx0[o];
+        sh.xNlb[i] = in.lbxe[o]; sh.xNub[i] = in.ubxe[o];
+        if (!(sh.xlb[i] < sh.xub[i]) || !(sh.x0lb[i] <= sh.x0ub[i]) || !(sh.xNlb[i] <= sh.xNub[i])) bad = 1;
+        if (sh.x0lb[i] < sh.x0ub[i]) sh.f0[sh.nf0++] = i;
+        sh.fix[i] = (sh.xNlb[i] == sh.xNub[i]) ? 1 : 0;
+        if (sh.fix[i]) { sh.ei[sh.ne] = i; sh.ev[sh.ne] = sh.xNlb[i]; sh.ne++; }
+        sh.c0[i] = 0.0; sh.cp[i] = 0.0; sh.tnu[i] = 0.0; sh.wnu[i] = 0.0; sh.qnu[i] = 0.0; sh.nun[i] = 0.0;
+      }
+      for (int a = 0; a < NU; ++a) {
+        sh.ulb[a] = in.lbu[(long long)pid * NU + a]; sh.uub[a] = in.ubu[(long long)pid * NU + a];
+        if (!(sh.ulb[a] < sh.uub[a])) bad = 1;
+      }
+      for (int j = 0; j < NQ; ++j) sh.c0[NQ + j] = p[j];
+      sh.c0[2 * NQ] = p[NQ];
+      sh.cp[2 * NQ] = p[NQ];
+      sh.wbnd = 0.0;
+      sh.bad = bad;
+    }
+    __syncthreads();
+    if (sh.bad) return;
+    const int N = sh.N;
+    const double* xg = in.xg + (long long)pid * (in.nmax + 1) * NX;
+    const double* ug = in.ug + (long long)pid * in.nmax * NU;
+    for (int k = t; k <= N; k += 64) {
+      double* r = rec(k);
+      for (int i = 0; i < NX; ++i) r[L::X + i] = (k == 0 && !(sh.x0lb[i] < sh.x0ub[i])) ? sh.x0lb[i] : xg[(long long)k * NX + i];
+      for (int i = 0; i < NZ; ++i) { r[L::LL + i] = 0.0; r[L::LU + i] = 0.0; }
+      for (int i = 0; i < NX; ++i) { r[L::PI + i] = 0.0; r[L::WPI + i] = 0.0; }
+      if (k < N)
+        for (int a = 0; a < NU; ++a) r[L::U + a] = ug[(long long)k * NU + a];
+    }
+    __syncthreads();
+  }
+
+  __device__ double cost() const {
+    double c = 0.0;
+    for (int k = t; k < sh.N; k += 64) {
+      const double* r = rec(k);
+      for (int i = 0; i < NX; ++i) c += (k == 0 ? sh.c0[i] : sh.cp[i]) * r[L::X + i];
+    }
+    return ft_wsum(c);
+  }
+
+  __device__ void store(const Inputs& in, int status, int it, int qit) {
+    const int N = sh.N, pid = sh.pid;
+    double* xo = in.xo + (long long)pid * (in.nmax + 1) * NX;
+    double* uo = in.uo + (long long)pid * in.nmax * NU;
+    for (int k = t; k <= N; k += 64) {
+      const double* r = rec(k);
+      for (int i = 0; i < NX; ++i) xo[(long long)k * NX + i] = r[L::X + i];
+      if (k < N)
+        for (int a = 0; a < NU; ++a) uo[(long long)k * NU + a] = r[L::U + a];
+    }
+    const double c = cost();
+    if (t == 0) {
+      in.status[pid] = status;
+      in.cost[pid] = c;
+      in.sqp_iter[pid] = it;
+      in.qp_iter[pid] = qit;
+    }
+  }
+
+  // ---- linearisation + NLP residuals ------------------------------------------------------------
+  __device__ void linearize() {
+    const int N = sh.N, m0 = sh.nf0 + NU;
+    for (int k = t; k < N; k += 64) {
+      double* r = rec(k);
+      double phi[NX];
+      ft_rk4_sens<NQ>(r + L::X, r + L::U, phi, r + L::A, r + L::B);
+      const double* r1 = rec(k + 1);
+      for (int i = 0; i < NX; ++i) r[L::BD + i] = phi[i] - r1[L::X + i];
+      if (k == 0) {
+        for (int i = 0; i < NX; ++i) {
+          for (int j = 0; j < sh.nf0; ++j) r[L::F0 + i * m0 + j] = r[L::A + i * NX + sh.f0[j]];
+          for (int a = 0; a < NU; ++a) r[L::F0 + i * m0 + sh.nf0 + a] = r[L::B + i * NU + a];
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  __device__ void residuals(double& rstat, double& req, double& rineq, double& rcomp) const {
+    const int N = sh.N, m0 = sh.nf0 + NU;
+    double st = 0.0, eq = 0.0, in = 0.0, cp = 0.0;
+    for (int k = t; k <= N; k += 64) {
+      const double* r = rec(k);
+      if (k < N) for (int i = 0; i < NX; ++i) eq = fmax(eq, fabs(r[L::BD + i]));
+      else for (int j = 0; j < sh.ne; ++j) eq = fmax(eq, fabs(r[L::X + sh.ei[j]] - sh.ev[j]));
+      const double* rp = k > 0 ? rec(k - 1) : r;
+      for (int i = 0; i < nz(k); ++i) {
+        double v, lb, ub;
+        const bool boxed = comp(k, i, v, lb, ub);
+        double gr = grad(k, i) - r[L::LL + i] + r[L::LU + i];
+        if (k == 0) {
+          for (int q = 0; q < NX; ++q) gr += r[L::F0 + q * m0 + i] * r[L::PI + q];
+        } else if (k < N) {
+          if (i < NX) {
+            for (int q = 0; q < NX; ++q) gr += r[L::A + q * NX + i] * r[L::PI + q];
+            gr -= rp[L::PI + i];
+          } else {
+            for (int q = 0; q < NX; ++q) gr += r[L::B + q * NU + (i - NX)] * r[L::PI + q];
+          }
+        } else {
+          gr -= rp[L::PI + i];
+          for (int j = 0; j < sh.ne; ++j) if (sh.ei[j] == i) gr += sh.tnu[j];
+        }
+        st = fmax(st, fabs(gr));
+        if (boxed) {
+          in = fmax(in, fmax(lb - v, v - ub));
+          cp = fmax(cp, fmax(fabs(r[L::LL + i] * (v - lb)), fabs(r[L::LU + i] * (ub - v))));
+        }
+      }
+    }
+    rstat = ft_wmax(st); req = ft_wmax(eq); rineq = ft_wmax(in); rcomp = ft_wmax(cp);
+  }
+
+  // ---- Riccati solve (lane 0): factor = true -> factorisation + vector pass ----------------------
+  __device__ bool newton(bool factor) {
+    bool ok = true;
+    if (t == 0) ok = newton_lane0(factor);
+    __syncthreads();
+    const int okw = __shfl(ok ? 1 : 0, 0);
+    return okw != 0;
+  }
+
+  __device__ bool newton_lane0(bool factor) {
+    const int N = sh.N, ne = sh.ne, m0 = sh.nf0 + NU;
+    const double rs = sh.rs;
+    double Pm[NX * NX], p[NX], Pi[NX * NX], lin[NX];
+    const double* rN = rec(N);
+    for (int i = 0; i < NX * NX; ++i) { Pm[i] = 0.0; Pi[i] = 0.0; }
+    for (int i = 0; i < NX; ++i) { Pm[i * NX + i] = rN[L::H + i]; p[i] = rN[L::G + i]; lin[i] = 0.0; }
+    for (int j = 0; j < ne; ++j) Pi[sh.ei[j] * ne + j] = 1.0;
+    if (factor) {
+      for (int i = 0; i < NX * NX; ++i) sh.S[i] = 0.0;
+      for (int i = 0; i < NX; ++i) sh.lin_e[i] = 0.0;
+    }
+    for (int k = N - 1; k >= 0; --k) {
+      double* r = rec(k);
+      const int mk = (k == 0) ? m0 : NU;
+      const double* Bk = (k == 0) ? r + L::F0 : r + L::B;
+      const int uoff = (k == 0) ? 0 : NX;
+      double e[NX], v[NX], rr[NZ];
+      for (int i = 0; i < NX; ++i) e[i] = rs * r[L::E0 + i];
+      if (factor) {
+        for (int i = 0; i < NX; ++i) {
+          double s = 0.0;
+          for (int j = 0; j < NX; ++j) s += Pm[i * NX + j] * e[j];
+          r[L::PE + i] = s;
+        }
+        for (int j = 0; j < ne; ++j) {
+          double s = 0.0;
+          for (int i = 0; i < NX; ++i) s += Pi[i * ne + j] * e[i];
+          sh.lin_e[j] += s;
+        }
+        double BP[NZ * NX], Ru[NZ * NZ];
+        for (int a = 0; a < mk; ++a)
+          for (int j = 0; j < NX; ++j) {
+            double s = 0.0;
+            for (int i = 0; i < NX; ++i) s += Bk[i * mk + a] * Pm[i * NX + j];
+            BP[a * NX + j] = s;
+          }
+        for (int a = 0; a < mk; ++a)
+          for (int c = 0; c < mk; ++c) {
+            double s = (a == c) ? r[L::H + uoff + a] : 0.0;
+            for (int i = 0; i < NX; ++i) s += BP[a * NX + i] * Bk[i * mk + c];
+            Ru[a * mk + c] = s;
+          }
+        for (int a = 0; a < mk; ++a)
+          for (int c = 0; c < a; ++c) {
+            const double s = 0.5 * (Ru[a * mk + c] + Ru[c * mk + a]);
+            Ru[a * mk + c] = Ru[c * mk + a] = s;
+          }
+        if (!ft_chol<NZ>(Ru, mk)) return false;
+        for (int e2 = 0; e2 < mk * mk; ++e2) r[L::LR + e2] = Ru[e2];
+        for (int a = 0; a < mk; ++a)
+          for (int j = 0; j < ne; ++j) {
+            double s = 0.0;
+            for (int i = 0; i < NX; ++i) s += Bk[i * mk + a] * Pi[i * ne + j];
+            r[L::Y + a * ne + j] = s;
+          }
+        for (int j = 0; j < ne; ++j) {
+          double col[NZ];
+          for (int a = 0; a < mk; ++a) col[a] = r[L::Y + a * ne + j];
+          ft_chol_solve(Ru, mk, col);
+          for (int a = 0; a < mk; ++a) r[L::M + a * ne + j] = col[a];
+        }
+        for (int i = 0; i < ne; ++i)
+          for (int j = 0; j < ne; ++j) {
+            double s = 0.0;
+            for (int a = 0; a < mk; ++a) s += r[L::Y + a * ne + i] * r[L::M + a * ne + j];
+            sh.S[i * ne + j] += s;
+          }
+        if (k > 0) {
+          double Sux[NU * NX];
+          for (int a = 0; a < NU; ++a)
+            for (int j = 0; j < NX; ++j) {
+              double s = 0.0;
+              for (int i = 0; i < NX; ++i) s += BP[a * NX + i] * r[L::A + i * NX + j];
+              Sux[a * NX + j] = s;
+            }
+          for (int j = 0; j < NX; ++j) {
+            double col[NU];
+            for (int a = 0; a < NU; ++a) col[a] = Sux[a * NX + j];
+            ft_chol_solve(Ru, NU, col);
+            for (int a = 0; a < NU; ++a) r[L::K + a * NX + j] = -col[a];
+          }
+          double AP[NX * NX], Pn[NX * NX], Pin[NX * NX];
+          for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < NX; ++j) {
+              double s = 0.0;
+              for (int q = 0; q < NX; ++q) s += r[L::A + q * NX + i] * Pm[q * NX + j];
+              AP[i * NX + j] = s;
+            }
+          for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < NX; ++j) {
+              double s = (i == j) ? r[L::H + i] : 0.0;
+              for (int q = 0; q < NX; ++q) s += AP[i * NX + q] * r[L::A + q * NX + j];
+              for (int a = 0; a < NU; ++a) s += Sux[a * NX + i] * r[L::K + a * NX + j];
+              Pn[i * NX + j] = s;
+            }
+          for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < i; ++j) {
+              const double s = 0.5 * (Pn[i * NX + j] + Pn[j * NX + i]);
+              Pn[i * NX + j] = Pn[j * NX + i] = s;
+            }
+          for (int i = 0; i < NX; ++i)
+            for (int j = 0; j < ne; ++j) {
+              double s = 0.0;
+              for (int q = 0; q < NX; ++q) {
+                double acl = r[L::A + q * NX + i];
+                for (int a = 0; a < NU; ++a) acl += r[L::B + q * NU + a] * r[L::K + a * NX + i];
+                s += acl * Pi[q * ne + j];
+              }
+              Pin[i * ne + j] = s;
+            }
+          for (int i = 0; i < NX * NX; ++i) { Pm[i] = Pn[i]; Pi[i] = Pin[i]; }
+        }
+      }
+      const double* Lr = r + L::LR;
+      for (int i = 0; i < NX; ++i) v[i] = r[L::PE + i] + p[i];
+      for (int a = 0; a < mk; ++a) {
+        double s = r[L::G + uoff + a];
+        for (int i = 0; i < NX; ++i) s += Bk[i * mk + a] * v[i];
+        rr[a] = s;
+      }
+      double kf[NZ], Lc[NZ * NZ];
+      for (int e2 = 0; e2 < mk * mk; ++e2) Lc[e2] = Lr[e2];
+      for (int a = 0; a < mk; ++a) kf[a] = rr[a];
+      ft_chol_solve(Lc, mk, kf);
+      for (int a = 0; a < mk; ++a) kf[a] = -kf[a];
+      if (k > 0) {
+        for (int a = 0; a < NU; ++a) r[L::KF + a] = kf[a];
+        double pn[NX];
+        for (int i = 0; i < NX; ++i) {
+          double s = r[L::G + i];
+          for (int q = 0; q < NX; ++q) s += r[L::A + q * NX + i] * v[q];
+          for (int a = 0; a < NU; ++a) s += r[L::K + a * NX + i] * rr[a];
+          pn[i] = s;
+        }
+        for (int i = 0; i < NX; ++i) p[i] = pn[i];
+      } else {
+        for (int a = 0; a < mk; ++a) r[L::D + a] = kf[a];
+      }
+      for (int j = 0; j < ne; ++j) {
+        double s = 0.0;
+        for (int a = 0; a < mk; ++a) s += r[L::Y + a * ne + j] * kf[a];
+        lin[j] += s;
+      }
+    }
+    // terminal multiplier nu = S^-1 (E d_N^0 - e_N)
+    if (ne > 0) {
+      double Sc[NX * NX], rhs[NX];
+      for (int e2 = 0; e2 < ne * ne; ++e2) Sc[e2] = sh.S[e2];
+      if (!ft_chol<NX>(Sc, ne)) return false;
+      for (int j = 0; j < ne; ++j) rhs[j] = lin[j] + sh.lin_e[j] - rs * rN[L::E0 + j];
+      ft_chol_solve(Sc, ne, rhs);
+      for (int j = 0; j < ne; ++j) sh.nun[j] = rhs[j];
+    }
+    // forward sweep
+    double* r0 = rec(0);
+    double w[NZ], dx[NX];
+    for (int a = 0; a < m0; ++a) {
+      double s = r0[L::D + a];
+      for (int j = 0; j < ne; ++j) s -= r0[L::M + a * ne + j] * sh.nun[j];
+      w[a] = s;
+    }
+    for (int a = 0; a < m0; ++a) r0[L::D + a] = w[a];
+    for (int i = 0; i < NX; ++i) {
+      double s = rs * r0[L::E0 + i];
+      for (int a = 0; a < m0; ++a) s += r0[L::F0 + i * m0 + a] * w[a];
+      dx[i] = s;
+    }
+    for (int k = 1; k < N; ++k) {
+      double* r = rec(k);
+      double du[NU], dn[NX];
+      for (int a = 0; a < NU; ++a) {
+        double s = r[L::KF + a];
+        for (int i = 0; i < NX; ++i) s += r[L::K + a * NX + i] * dx[i];
+        for (int j = 0; j < ne; ++j) s -= r[L::M + a * ne + j] * sh.nun[j];
+        du[a] = s;
+      }
+      for (int i = 0; i < NX; ++i) r[L::D + i] = dx[i];
+      for (int a = 0; a < NU; ++a) r[L::D + NX + a] = du[a];
+      for (int i = 0; i < NX; ++i) {
+        double s = rs * r[L::E0 + i];
+        for (int q = 0; q < NX; ++q) s += r[L::A + i * NX + q] * dx[q];
+        for (int a = 0; a < NU; ++a) s += r[L::B + i * NU + a] * du[a];
+        dn[i] = s;
+      }
+      for (int i = 0; i < NX; ++i) dx[i] = dn[i];
+    }
+    double* rNw = rec(N);
+    for (int i = 0; i < NX; ++i) rNw[L::D + i] = dx[i];
+    return true;
+  }
+
+  // ---- interior-point QP ------------------------------------------------------------------------
+  // returns 0 converged, 1 max-iter, -1 failure; iterations in qit
+  __device__ int qp(int& qit) {
+    const int N = sh.N, ne = sh.ne, m0 = sh.nf0 + NU;
+    const double rho = o.lm;
+    double nb = 0.0;
+    for (int k = t; k <= N; k += 64) {
+      double* r = rec(k);
+      for (int i = 0; i < nz(k); ++i) {
+        double v, lb, ub;
+        if (!comp(k, i, v, lb, ub)) {
+          r[L::DZ + i] = 0.0; r[L::QL + i] = 0.0; r[L::QU + i] = 0.0; r[L::LB + i] = -INFINITY; r[L::UB + i] = INFINITY;
+          continue;
+        }
+        const double Lo = lb - v, Up = ub - v, del = o.push * (Up - Lo);
+        double z0 = 0.0;
+        if (z0 < Lo + del) z0 = Lo + del;
+        if (z0 > Up - del) z0 = Up - del;
+        r[L::LB + i] = Lo; r[L::UB + i] = Up; r[L::DZ + i] = z0;
+        r[L::QL + i] = o.mu0 / (z0 - Lo);
+        r[L::QU + i] = o.mu0 / (Up - z0);
+        nb += 2.0;
+      }
+    }
+    const double nbox = ft_wsum(nb);
+    __syncthreads();
+    double e00 = 0.0, rd0 = 0.0;
+    for (int k = t; k <= N; k += 64) {
+      double* r = rec(k);
+      if (k < N) {
+        const double* r1 = rec(k + 1);
+        for (int i = 0; i < NX; ++i) {
+          double s = r[L::BD + i] - r1[L::DZ + i];
+          if (k == 0) {
+            for (int a = 0; a < m0; ++a) s += r[L::F0 + i * m0 + a] * r[L::DZ + a];
+          } else {
+            for (int q = 0; q < NX; ++q) s += r[L::A + i * NX + q] * r[L::DZ + q];
+            for (int a = 0; a < NU; ++a) s += r[L::B + i * NU + a] * r[L::DZ + NX + a];
+          }
+          r[L::E0 + i] = s;
+          e00 = fmax(e00, fabs(s));
+        }
+      } else {
+        for (int j = 0; j < ne; ++j) {
+          const double s = sh.ev[j] - r[L::X + sh.ei[j]] - r[L::DZ + sh.ei[j]];
+          r[L::E0 + j] = s;
+          e00 = fmax(e00, fabs(s));
+        }
+      }
+      for (int i = 0; i < nz(k); ++i)
+        rd0 = fmax(rd0, fabs(rho * r[L::DZ + i] + grad(k, i) - r[L::QL + i] + r[L::QU + i]));
+    }
+    e00 = ft_wmax(e00);
+    rd0 = ft_wmax(rd0);
+    if (t == 0) {
+      sh.rs = 1.0;
+      for (int j = 0; j < NX; ++j) sh.qnu[j] = 0.0;
+    }
+    __syncthreads();
+    int it, status = 1;
+    for (it = 0; it < o.qp_max_iter; ++it) {
+      double mu = 0.0;
+      for (int k = t; k <= N; k += 64) {
+        const double* r = rec(k);
+        for (int i = 0; i < nz(k); ++i) {
+          if (!isfinite(r[L::LB + i])) continue;
+          mu += (r[L::DZ + i] - r[L::LB + i]) * r[L::QL + i] + (r[L::UB + i] - r[L::DZ + i]) * r[L::QU + i];
+        }
+      }
+      mu = ft_wsum(mu) / nbox;
+      if (!isfinite(mu)) { status = -1; break; }
+      const double rs = sh.rs;
+      if (mu < o.qp_tol_comp && rs * rd0 < o.qp_tol_stat && rs * e00 < o.qp_tol_eq) { status = 0; break; }
+      // predictor: barrier Hessian and gradient
+      for (int k = t; k <= N; k += 64) {
+        double* r = rec(k);
+        for (int i = 0; i < nz(k); ++i) {
+          double Hh = rho;
+          const double gg = rho * r[L::DZ + i] + grad(k, i);
+          if (isfinite(r[L::LB + i]))
+            Hh += r[L::QL + i] / (r[L::DZ + i] - r[L::LB + i]) + r[L::QU + i] / (r[L::UB + i] - r[L::DZ + i]);
+          r[L::H + i] = Hh; r[L::G + i] = gg;
+        }
+      }
+      __syncthreads();
+      if (!newton(true)) { status = -1; break; }
+      FtRatio ma{1.0, 1.0};
+      for (int k = t; k <= N; k += 64) {
+        double* r = rec(k);
+        for (int i = 0; i < nz(k); ++i) {
+          const double d = r[L::D + i];
+          r[L::DAFF + i] = d;
+          if (!isfinite(r[L::LB + i])) continue;
+          const double tl = r[L::DZ + i] - r[L::LB + i], tu = r[L::UB + i] - r[L::DZ + i];
+          const double ql = r[L::QL + i], qu = r[L::QU + i];
+          const double dll = -ql - ql * d / tl, dlu = -qu + qu * d / tu;
+          ma.add(tl, d); ma.add(tu, -d); ma.add(ql, dll); ma.add(qu, dlu);
+        }
+      }
+      const double aa = ma.reduce();
+      double muaff = 0.0;
+      for (int k = t; k <= N; k += 64) {
+        const double* r = rec(k);
+        for (int i = 0; i < nz(k); ++i) {
+          if (!isfinite(r[L::LB + i])) continue;
+          const double d = r[L::D + i], tl = r[L::DZ + i] - r[L::LB + i], tu = r[L::UB + i] - r[L::DZ + i];
+          const double ql = r[L::QL + i], qu = r[L::QU + i];
+          const double dll = -ql - ql * d / tl, dlu = -qu + qu * d / tu;
+          muaff += (tl + aa * d) * (ql + aa * dll) + (tu - aa * d) * (qu + aa * dlu);
+        }
+      }
+      muaff = ft_wsum(muaff) / nbox;
+      double sig = muaff / mu;
+      sig = sig * sig * sig;
+      if (sig > 1.0) sig = 1.0;
+      const double smu = sig * mu;
+      // corrector right-hand side
+      for (int k = t; k <= N; k += 64) {
+        double* r = rec(k);
+        for (int i = 0; i < nz(k); ++i) {
+          if (!isfinite(r[L::LB + i])) continue;
+          const double tl = r[L::DZ + i] - r[L::LB + i], tu = r[L::UB + i] - r[L::DZ + i], itl = 1.0 / tl, itu = 1.0 / tu;
+          const double d = r[L::DAFF + i], ql = r[L::QL + i], qu = r[L::QU + i];
+          const double dll = -ql - ql * d * itl, dlu = -qu + qu * d * itu;
+          const double rl = smu - tl * ql - d * dll, ru = smu - tu * qu + d * dlu;
+          r[L::G + i] = rho * r[L::DZ + i] + grad(k, i) - ql - rl * itl + qu + ru * itu;
+        }
+      }
+      __syncthreads();
+      if (!newton(false)) { status = -1; break; }
+      FtRatio mx{1.0, o.tau};
+      for (int k = t; k <= N; k += 64) {
+        const double* r = rec(k);
+        for (int i = 0; i < nz(k); ++i) {
+          if (!isfinite(r[L::LB + i])) continue;
+          const double tl = r[L::DZ + i] - r[L::LB + i], tu = r[L::UB + i] - r[L::DZ + i], itl = 1.0 / tl, itu = 1.0 / tu;
+          const double d = r[L::D + i], da = r[L::DAFF + i], ql = r[L::QL + i], qu = r[L::QU + i];
+          const double dlla = -ql - ql * da * itl, dlua = -qu + qu * da * itu;
+          const double rl = smu - tl * ql - da * dlla, ru = smu - tu * qu + da * dlua;
+          const double dll = (rl - ql * d) * itl, dlu = (ru + qu * d) * itu;
+          mx.add(tl, d); mx.add(tu, -d); mx.add(ql, dll); mx.add(qu, dlu);
+        }
+      }
+      const double alpha = fmin(1.0, o.tau * mx.reduce());
+      for (int k = t; k <= N; k += 64) {
+        double* r = rec(k);
+        for (int i = 0; i < nz(k); ++i) {
+          const double d = r[L::D + i];
+          if (isfinite(r[L::LB + i])) {
+            const double tl = r[L::DZ + i] - r[L::LB + i], tu = r[L::UB + i] - r[L::DZ + i], itl = 1.0 / tl, itu = 1.0 / tu;
+            const double da = r[L::DAFF + i], ql = r[L::QL + i], qu = r[L::QU + i];
+            const double dlla = -ql - ql * da * itl, dlua = -qu + qu * da * itu;
+            const double rl = smu - tl * ql - da * dlla, ru = smu - tu * qu + da * dlua;
+            r[L::QL + i] = ql + alpha * (rl - ql * d) * itl;
+            r[L::QU + i] = qu + alpha * (ru + qu * d) * itu;
+          }
+          r[L::DZ + i] += alpha * d;
+        }
+      }
+      if (t == 0) {
+        for (int j = 0; j < ne; ++j) sh.qnu[j] += alpha * (sh.nun[j] - sh.qnu[j]);
+        sh.rs = rs * (1.0 - alpha);
+      }
+      __syncthreads();
+    }
+    qit = it;
+    if (status < 0) return -1;
+    // costates by the backward adjoint from the final iterate (lane 0)
+    if (t == 0) {
+      double lam[NX];
+      const double* rN = rec(N);
+      for (int i = 0; i < NX; ++i) lam[i] = rho * rN[L::DZ + i] - rN[L::QL + i] + rN[L::QU + i];
+      for (int j = 0; j < ne; ++j) lam[sh.ei[j]] += sh.qnu[j];
+      for (int k = N - 1; k >= 0; --k) {
+        double* r = rec(k);
+        for (int i = 0; i < NX; ++i) r[L::QPI + i] = lam[i];
+        if (k == 0) break;
+        double ln[NX];
+        for (int i = 0; i < NX; ++i) {
+          double s = rho * r[L::DZ + i] + grad(k, i) - r[L::QL + i] + r[L::QU + i];
+          for (int q = 0; q < NX; ++q) s += r[L::A + q * NX + i] * lam[q];
+          ln[i] = s;
+        }
+        for (int i = 0; i < NX; ++i) lam[i] = ln[i];
+      }
+    }
+    int bad = 0;
+    for (int k = t; k <= N; k += 64) {
+      const double* r = rec(k);
+      for (int i = 0; i < nz(k); ++i)
+        if (!isfinite(r[L::DZ + i]) || !isfinite(r[L::QL + i]) || !isfinite(r[L::QU + i])) bad = 1;
+    }
+    __syncthreads();
+    if (ft_wmax(bad ? 1.0 : 0.0) > 0.0) return -1;
+    return status;
+  }
+
+  // ---- merit line search + step ------------------------------------------------------------------
+  __device__ void state_at(int k, double alpha, double* x, double* u) const {
+    const double* r = rec(k);
+    if (k == 0) {
+      for (int i = 0; i < NX; ++i) x[i] = r[L::X + i];
+      for (int j = 0; j < sh.nf0; ++j) x[sh.f0[j]] += alpha * r[L::DZ + j];
+      for (int a = 0; a < NU; ++a) u[a] = r[L::U + a] + alpha * r[L::DZ + sh.nf0 + a];
+      return;
+    }
+    for (int i = 0; i < NX; ++i) x[i] = r[L::X + i] + alpha * r[L::DZ + i];
+    if (k < sh.N)
+      for (int a = 0; a < NU; ++a) u[a] = r[L::U + a] + alpha * r[L::DZ + NX + a];
+  }
+
+  __device__ double merit(double alpha) const {
+    const int N = sh.N;
+    double val = 0.0, viol = 0.0;
+    for (int k = t; k <= N; k += 64) {
+      const double* r = rec(k);
+      for (int i = 0; i < nz(k); ++i) {
+        double v, lb, ub;
+        if (!comp(k, i, v, lb, ub)) continue;
+        v += alpha * r[L::DZ + i];
+        viol += fmax(0.0, lb - v) + fmax(0.0, v - ub);
+      }
+      double xk[NX], uk[NU], xn[NX], un[NU], phi[NX];
+      if (k < N) {
+        state_at(k, alpha, xk, uk);
+        for (int i = 0; i < NX; ++i) val += (k == 0 ? sh.c0[i] : sh.cp[i]) * xk[i];
+        ft_rk4_sens<NQ>(xk, uk, phi, nullptr, nullptr);
+        state_at(k + 1, alpha, xn, un);
+        for (int i = 0; i < NX; ++i) val += r[L::WPI + i] * fabs(phi[i] - xn[i]);
+      } else {
+        state_at(N, alpha, xn, un);
+        for (int j = 0; j < sh.ne; ++j) val += sh.wnu[j] * fabs(xn[sh.ei[j]] - sh.ev[j]);
+      }
+    }
+    return ft_wsum(val) + sh.wbnd * ft_wsum(viol);
+  }
+
+  __device__ void weights() {
+    const int N = sh.N;
+    double lmax = 0.0;
+    for (int k = t; k <= N; k += 64) {
+      double* r = rec(k);
+      if (k < N)
+        for (int i = 0; i < NX; ++i) {
+          const double a = fabs(r[L::QPI + i]), b = 0.5 * (r[L::WPI + i] + a);
+          r[L::WPI + i] = a > b ? a : b;
+        }
+      for (int i = 0; i < nz(k); ++i) lmax = fmax(lmax, fmax(r[L::QL + i], r[L::QU + i]));
+    }
+    lmax = ft_wmax(lmax);
+    if (t == 0) {
+      for (int j = 0; j < sh.ne; ++j) {
+        const double a = fabs(sh.qnu[j]), b = 0.5 * (sh.wnu[j] + a);
+        sh.wnu[j] = a > b ? a : b;
+      }
+      const double b = 0.5 * (sh.wbnd + lmax);
+      sh.wbnd = lmax > b ? lmax : b;
+    }
+    __syncthreads();
+  }
+
+  __device__ void apply(double alpha) {
+    const int N = sh.N;
+    for (int k = t; k <= N; k += 64) {
+      double* r = rec(k);
+      double x[NX], u[NU];
+      state_at(k, alpha, x, u);
+      for (int i = 0; i < NX; ++i) r[L::X + i] = x[i];
+      if (k < N)
+        for (int a = 0; a < NU; ++a) r[L::U + a] = u[a];
+      for (int i = 0; i < nz(k); ++i) {
+        r[L::LL + i] += alpha * (r[L::QL + i] - r[L::LL + i]);
+        r[L::LU + i] += alpha * (r[L::QU + i] - r[L::LU + i]);
+      }
+      if (k < N)
+        for (int i = 0; i < NX; ++i) r[L::PI + i] += alpha * (r[L::QPI + i] - r[L::PI + i]);
+    }
+    if (t == 0)
+      for (int j = 0; j < sh.ne; ++j) sh.tnu[j] += alpha * (sh.qnu[j] - sh.tnu[j]);
+    __syncthreads();
+  }
+
+  __device__ int run(int& it, int& qtot) {
+    int status = 2;
+    qtot = 0;
+    for (it = 0;; ++it) {
+      linearize();
+      double rstat, req, rineq, rcomp;
+      residuals(rstat, req, rineq, rcomp);
+      if (!isfinite(rstat) || !isfinite(req)) { status = 1; break; }
+      if (rstat < o.tol_stat && req < o.tol_eq && rineq < o.tol_ineq && rcomp < o.tol_comp) { status = 0; break; }
+      if (it >= o.max_iter) { status = 2; break; }
+      int qit = 0;
+      const int qs = qp(qit);
+      qtot += qit;
+      if (qs < 0) { status = 4; break; }
+      weights();
+      const double phi0 = merit(0.0);
+      double alpha = 1.0;
+      for (;;) {
+        const double pa = merit(alpha);
+        if (pa < phi0) break;
+        if (alpha * o.alpha_red < o.alpha_min) break;
+        alpha *= o.alpha_red;
+      }
+      apply(alpha);
+      if (!isfinite(rec(0)[L::X + NX - 1])) { status = 1; break; }
+    }
+    return status;
+  }
+};
+
+// one workgroup = one wave = one problem at a time; workgroups pull problem ids until none are left
+template <int NQ>
+__global__ __launch_bounds__(64) void k_ft(Opts o, Inputs in, double* regions, long long region_doubles,
+                                           unsigned* head) {
+  __shared__ FtShared<NQ> sh;
+  __shared__ int job;
+  const int t = (int)threadIdx.x;
+  Ft<NQ> F(sh, regions + (long long)blockIdx.x * region_doubles, o, t);
+  for (;;) {
+    if (t == 0) job = (int)atomicAdd(head, 1u);
+    __syncthreads();
+    const int pid = job;
+    __syncthreads();
+    if (pid >= in.B) break;
+    F.load(in, pid);
+    if (sh.bad) {
+      if (t == 0) {
+        in.status[pid] = 5;
+        in.cost[pid] = NAN;
+        in.sqp_iter[pid] = 0;
+        in.qp_iter[pid] = 0;
+      }
+      __syncthreads();
+      continue;
+    }
+    int it = 0, qit = 0;
+    const int status = F.run(it, qit);
+    F.store(in, status, it, qit);
+    __syncthreads();
+  }
+}
+
+}  // namespace vboc

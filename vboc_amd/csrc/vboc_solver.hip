@@ -1266,6 +1266,7 @@ __global__ __launch_bounds__(256) void rk4_kernel(int B, double T, const double*
 }  // namespace vboc
 
 #include "coop.h"
+#include "ft.h"
 
 // =================================================================================================
 // C ABI
@@ -1315,6 +1316,9 @@ struct vboc_solver {
   size_t wave_lds = 0;
   bool coop_ok = false;
   long long coop_count = 0;
+  // free-time solver (ft.h): one problem per wave, per-workgroup stage-record regions
+  double* ft_regions = nullptr;
+  size_t ft_bytes = 0;
 };
 
 static void default_opts(Opts& o) {
@@ -1401,6 +1405,23 @@ static hipError_t launch_round(vboc_solver* h, dim3 grid, dim3 block, hipStream_
   hipLaunchKernelGGL(k_ls<NQ>, grid, block, 0, st, w, o, in, ss);
   h->launches += 2;
   return hipGetLastError();
+}
+
+// free-time solver: a persistent grid of one-wave workgroups, each with its own stage-record region
+template <int NQ>
+static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st) {
+  const long long rd = FtL<NQ>::region_doubles(in.nmax);
+  long long groups = in.B < 1024 ? in.B : 1024;
+  const size_t need = (size_t)groups * (size_t)rd * sizeof(double);
+  if (need > h->ft_bytes) {
+    if (h->ft_regions) (void)hipFree(h->ft_regions);
+    h->ft_regions = nullptr;
+    h->ft_bytes = 0;
+    if (hipMalloc(&h->ft_regions, need) != hipSuccess) return -1;
+    h->ft_bytes = need;
+  }
+  hipLaunchKernelGGL(k_ft<NQ>, dim3((unsigned)groups), dim3(64), 0, st, h->o, in, h->ft_regions, rd, h->head);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs, hipStream_t st, const Work& w,
@@ -1509,6 +1530,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->regions) (void)hipFree(h->regions);
   if (h->host_done) (void)hipHostFree(h->host_done);
   if (h->stage) (void)hipFree(h->stage);
+  if (h->ft_regions) (void)hipFree(h->ft_regions);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   for (auto ev : h->pev) (void)hipEventDestroy(ev);
@@ -1719,7 +1741,40 @@ int vboc_kernel_stats(vboc_handle h, double* factor_ms, long long* factor_launch
   return VBOC_OK;
 }
 
-int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) {
+int vboc_solve_batch_ft(vboc_handle h, const vboc_batch_t* b, void* stream) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: NULL argument");
+  if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: B < 0");
+  if (b->nmax > h->nmax || b->nmax < 1)
+    return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: batch nmax exceeds the handle's nmax");
+  if (b->B == 0) { h->launches = 0; return VBOC_OK; }
+  const void* ptrs[] = {b->N, b->x_guess, b->u_guess, b->p, b->lbx, b->ubx, b->lbu, b->ubu, b->lbx_0, b->ubx_0,
+                        b->lbx_e, b->ubx_e, b->status, b->x_out, b->u_out, b->cost, b->sqp_iter, b->qp_iter};
+  for (const void* q : ptrs)
+    if (!q) return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: NULL array in batch");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  Inputs in;
+  in.B = b->B; in.nmax = b->nmax; in.N = b->N;
+  in.xg = b->x_guess; in.ug = b->u_guess; in.p = b->p; in.lbx = b->lbx; in.ubx = b->ubx; in.lbu = b->lbu;
+  in.ubu = b->ubu; in.lbx0 = b->lbx_0; in.ubx0 = b->ubx_0; in.lbxe = b->lbx_e; in.ubxe = b->ubx_e;
+  in.status = b->status; in.xo = b->x_out; in.uo = b->u_out; in.cost = b->cost; in.sqp_iter = b->sqp_iter;
+  in.qp_iter = b->qp_iter; in.head = h->head;
+  HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
+  HIPCHK(hipEventRecord(h->ev0, st));
+  int rc;
+  switch (h->nq) {
+    case 1: rc = launch_ft<1>(h, in, st); break;
+    case 2: rc = launch_ft<2>(h, in, st); break;
+    default: rc = launch_ft<3>(h, in, st); break;
+  }
+  if (rc == -1) return fail(VBOC_ERR_NOMEM, "vboc_solve_batch_ft: hipMalloc of the stage regions");
+  if (rc) return fail(VBOC_ERR_HIP, std::string("vboc_solve_batch_ft: ") + hipGetErrorString(hipGetLastError()));
+  HIPCHK(hipEventRecord(h->ev1, st));
+  h->launches = 1;
+  return VBOC_OK;
+}
+
+static int solve_host(vboc_handle h, const vboc_batch_t* b, bool ft) {
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_solve_batch_host: NULL argument");
   if (b->B == 0) return VBOC_OK;
   HIPCHK(hipSetDevice(h->device));
@@ -1763,7 +1818,7 @@ int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) {
   db.qp_iter = ip; ip += B;
   HIPCHK(cerr);
   HIPCHK(hipMemcpy((void*)db.N, b->N, B * sizeof(int), hipMemcpyHostToDevice));
-  int rc = vboc_solve_batch(h, &db, nullptr);
+  int rc = ft ? vboc_solve_batch_ft(h, &db, nullptr) : vboc_solve_batch(h, &db, nullptr);
   if (rc) return rc;
   HIPCHK(hipDeviceSynchronize());
   HIPCHK(hipMemcpy(b->x_out, db.x_out, sz_xg * sizeof(double), hipMemcpyDeviceToHost));
@@ -1774,6 +1829,9 @@ int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) {
   HIPCHK(hipMemcpy(b->qp_iter, db.qp_iter, B * sizeof(int), hipMemcpyDeviceToHost));
   return VBOC_OK;
 }
+
+int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, false); }
+int vboc_solve_batch_ft_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, true); }
 
 int vboc_rk4_batch(int nq, int B, double T, const double* x, const double* u, double* x_out, void* stream) {
   if (nq < 1 || nq > 3 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_batch: bad nq/B");

@@ -50,6 +50,7 @@ class Solve:
     q_init_ub: np.ndarray
     q_fin_lb: np.ndarray
     q_fin_ub: np.ndarray
+    free_time: bool = False    # OCPpendulum.OCP_solve (free-time box OCP, vboc_solve_batch_ft)
 
 
 @dataclass
@@ -450,8 +451,8 @@ class GpuBackend:
         self.nmax = nmax
         self.solver = lib.Solver(nq, nmax, device=device, **options)
 
-    def solve(self, batch):
-        return self.solver.solve_host(batch)
+    def solve(self, batch, free_time=False):
+        return self.solver.solve_host(batch, free_time=free_time)
 
     def rk4(self, x, u, T):
         return self.lib.rk4_host(self.nq, T, x, u)
@@ -505,13 +506,18 @@ def run_problems(nq, gens, backend, nmax=200):
         if sv and not rk:
             # solves are the expensive part: batch them only once no twin steps are outstanding, so
             # problems that are sweeping catch up and join the next solve batch
-            reqs = [pending[i] for i in sv]
-            out = backend.solve(_pack(nq, reqs, nmax))
-            for k, i in enumerate(sv):
-                Nk = reqs[k].N
-                answers[i] = Solution(int(out["status"][k]), out["x"][k, :Nk + 1], out["u"][k, :Nk],
-                                      float(out["cost"][k]))
-            stats["solves"] += len(sv)
+            for ft in (False, True):
+                grp = [i for i in sv if pending[i].free_time == ft]
+                if not grp:
+                    continue
+                reqs = [pending[i] for i in grp]
+                b = _pack(nq, reqs, nmax)
+                out = backend.solve(b, free_time=True) if ft else backend.solve(b)
+                for k, i in enumerate(grp):
+                    Nk = reqs[k].N
+                    answers[i] = Solution(int(out["status"][k]), out["x"][k, :Nk + 1], out["u"][k, :Nk],
+                                          float(out["cost"][k]))
+                stats["solves"] += len(grp)
         for i, a in answers.items():
             try:
                 pending[i] = gens[i].send(a)
@@ -544,6 +550,112 @@ def testing_batch(nq, ids, backend, N_start=None, seed=SEED, max_restarts=MAX_TE
     gens = [testing_problem(nq, int(pid), U[b], ProblemRNG(int(pid), seed, stream=TEST_STREAM), N_start,
                             max_restarts) for b, pid in enumerate(ids)]
     return run_problems(nq, gens, backend, nmax=getattr(backend, "nmax", 200))
+
+
+# ------------------------------------------------------------------------------------------------
+# pendulum VBOC data generation (free-time OCPs)
+# ------------------------------------------------------------------------------------------------
+PEND_N_START, PEND_EPS = 50, 1e-3   # VBOC/pendulum_vboc.py:21, :47
+
+
+def pendulum_sweep_problem(v_sel_max, N_start=PEND_N_START, eps=PEND_EPS):
+    """Generator for one of the two sweeps of the pendulum's simplified data generation
+    (VBOC/pendulum_vboc.py:52-205, `for v_sel in [v_min, v_max]`).  Yields free-time Solve requests
+    (OCPpendulum.OCP_solve); returns the rows it appends to X_save (lists [theta, dtheta]).
+    Kept as in the reference: the horizon loop re-solves with N + 1 while |dtheta_0| grows by more
+    than 1e-4 (:96-138); the verification solve is warm-started from the FIRST N_test + 1 rows of
+    x_sol (:181), its status is not read (the test at :183 sees the horizon loop's status, SURVEY
+    App. A.6), and a failed horizon solve raises like the reference (:138)."""
+    sysd = system(1)
+    v_max, q_max, q_min = sysd.v_max, sysd.q_max, sysd.q_min
+    v_min = -v_max
+    v_sel = v_max if v_sel_max else v_min
+    N = N_start
+    dt = 1e-2
+    if v_sel == v_min:
+        q_init, q_fin = q_max, q_min
+        lb, ub = np.array([q_min, v_min, 0.]), np.array([q_max, 0., 1e-2])
+        cost_dir = 1.
+    else:
+        q_init, q_fin = q_min, q_max
+        lb, ub = np.array([q_min, 0., 0.]), np.array([q_max, v_max, 1e-2])
+        cost_dir = -1.
+    u_lb, u_ub = np.array([-sysd.u_max]), np.array([sysd.u_max])
+
+    def solve(Nc, xg, ug, qi):
+        # OCPpendulum.OCP_solve: stages i < Nc from the guess rows, stage Nc from row Nc
+        return Solve(Nc, np.array(xg[:Nc + 1], dtype=float), np.array(ug[:Nc], dtype=float),
+                     np.array([cost_dir, 1.]), lb, ub, u_lb, u_ub, np.array([qi, -v_max, 0.]),
+                     np.array([qi, v_max, 1e-2]), np.array([q_fin, 0., 0.]), np.array([q_fin, 0., 1e-2]),
+                     free_time=True)
+
+    x_guess = np.empty((N + 1, 3))
+    u_guess = np.zeros((N, 1))
+    q_guess = np.linspace(q_init, q_fin, N + 1, endpoint=True)
+    for i in range(N + 1):
+        x_guess[i] = [q_guess[i], v_sel, dt]
+    norm_old = v_max
+    while True:
+        if x_guess.shape[0] < N + 1:
+            raise IndexError("stage-N guess row missing (the reference's OCP_solve indexes x_sol_guess[N])")
+        res = yield solve(N, x_guess, u_guess, q_init)
+        status = res.status
+        if status != 0:
+            raise RuntimeError("Sorry, the solver failed")
+        norm_new = abs(res.x[0][1])
+        if norm_new > norm_old + 1e-4:
+            norm_old = norm_new
+            x_guess = np.empty((N + 1, 3))
+            u_guess = np.empty((N + 1, 1))
+            x_guess[:N] = res.x[:N]
+            u_guess[:N] = res.u[:N]
+            x_guess[N] = res.x[N]
+            u_guess[N] = 0.
+            N = N + 1
+        else:
+            x_sol = np.array(res.x[:N + 1], dtype=float)
+            u_sol = np.array(res.u[:N], dtype=float)
+            break
+    rows = [x_sol[0][:2].tolist()]
+    x_out = np.copy(x_sol[0][:2])
+    x_out[1] = x_out[1] - eps * cost_dir
+    x_at_limit = bool(x_out[1] > v_max or x_out[1] < v_min)
+    for f in range(1, N):
+        if x_at_limit:
+            v_out = x_sol[f][1] - eps * cost_dir
+            if v_out > v_max or v_out < v_min:
+                rows.append(x_sol[f][:2].tolist())
+            else:
+                norm_old = abs(x_sol[f][1])
+                N_test = N - f
+                ver = yield solve(N_test, x_sol, u_sol, x_sol[f][0])
+                if status == 0:          # the horizon loop's status (quirk A.6): always 0 here
+                    x0_new = ver.x[0]
+                    norm_new = abs(x0_new[1])
+                    if norm_new > norm_old + 1e-4:
+                        for i in range(N - f):
+                            x_sol[i + f] = ver.x[i]
+                            u_sol[i + f] = ver.u[i]
+                        x_out = np.copy(x0_new[:2])
+                        x_out[1] = x_out[1] - eps * cost_dir
+                        x_at_limit = bool(x_out[1] > v_max or x_out[1] < v_min)
+                    else:
+                        x_at_limit = False
+                    rows.append(x_sol[f][:2].tolist())
+        else:
+            if abs(x_sol[f][0] - q_fin) <= 1e-3:
+                break
+            rows.append(x_sol[f][:2].tolist())
+    return rows
+
+
+def pendulum_data_generation(backend, N_start=PEND_N_START, eps=PEND_EPS):
+    """X_save of VBOC/pendulum_vboc.py:50-205: both sweeps (v_min, then v_max) run as one batch of two
+    problems.  Returns (X_save [n x 2] float64, stats)."""
+    gens = [pendulum_sweep_problem(False, N_start, eps), pendulum_sweep_problem(True, N_start, eps)]
+    res, stats = run_problems(1, gens, backend, nmax=getattr(backend, "nmax", 200))
+    rows = res[0] + res[1]
+    return np.array(rows, dtype=np.float64).reshape(len(rows), 2), stats
 
 
 def heldout_set(nq, results):

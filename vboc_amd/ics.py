@@ -179,3 +179,40 @@ def _bounds(sysd, B, N, xg, ug, p, lbx0, ubx0, extra=None):
     if extra:
         b.update(extra)
     return b
+
+
+def pendulum_free_time_ics(ids, N_range=(20, 60), seed=SEED):
+    """Free-time pendulum OCPs shaped like VBOC/pendulum_vboc.py's solves (OCPpendulum.OCP_solve,
+    VBOC/pendulum_class_vboc.py:107-130): sweep direction v_sel = +-v_max (:55-77), a fixed initial
+    position q_init (the sweep's first solve starts at the box edge, :61/:70; its verification solves
+    anywhere along the trajectory, :181 - here uniform in the box, kept 0.05 rad away from q_fin),
+    terminal rest at q_fin, dt free in [0, 1e-2], straight-line guess (:79-84), horizon uniform in
+    N_range.  Philox stream 4.  For parity tests and benchmarks of the free-time solver."""
+    sysd = system(1)
+    ids = np.asarray(ids)
+    B = ids.shape[0]
+    U = uniforms(ids, 4, seed, stream=4)
+    q_min, q_max, v_max = sysd.q_min, sysd.q_max, sysd.v_max
+    vsel = np.where(U[:, 0] < 0.5, -v_max, v_max)
+    N = (N_range[0] + np.floor(U[:, 2] * (N_range[1] - N_range[0] + 1))).astype(np.int32)
+    N = np.minimum(N, N_range[1])
+    Nm = int(N.max())
+    span = q_max - q_min - 0.05
+    q_init = np.where(vsel < 0, q_min + 0.05 + U[:, 1] * span, q_max - 0.05 - U[:, 1] * span)
+    q_fin = np.where(vsel < 0, q_min, q_max)
+    lbx = np.stack([np.full(B, q_min), np.where(vsel < 0, -v_max, 0.0), np.zeros(B)], axis=1)
+    ubx = np.stack([np.full(B, q_max), np.where(vsel < 0, 0.0, v_max), np.full(B, 1e-2)], axis=1)
+    xg = np.zeros((B, Nm + 1, 3))
+    for b in range(B):
+        n = int(N[b])
+        xg[b, :n + 1, 0] = np.linspace(q_init[b], q_fin[b], n + 1)
+        xg[b, :n + 1, 1] = vsel[b]
+        xg[b, :n + 1, 2] = 1e-2
+        xg[b, n + 1:] = xg[b, n]
+    p = np.stack([np.where(vsel < 0, 1.0, -1.0), np.ones(B)], axis=1)
+    return Batch(N=N, x_guess=xg, u_guess=np.zeros((B, Nm, 1)), p=p, lbx=lbx, ubx=ubx,
+                 lbu=np.full((B, 1), -sysd.u_max), ubu=np.full((B, 1), sysd.u_max),
+                 lbx0=np.stack([q_init, np.full(B, -v_max), np.zeros(B)], axis=1),
+                 ubx0=np.stack([q_init, np.full(B, v_max), np.full(B, 1e-2)], axis=1),
+                 lbxe=np.stack([q_fin, np.zeros(B), np.zeros(B)], axis=1),
+                 ubxe=np.stack([q_fin, np.zeros(B), np.full(B, 1e-2)], axis=1))

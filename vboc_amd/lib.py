@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("VBOC_LIB") or os.path.join(HERE, "libvboc_amd.so")
 SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
-           "vboc_solve_batch_host", "vboc_rk4_batch", "vboc_rk4_batch_host", "vboc_last_kernel_ms",
+           "vboc_solve_batch_host", "vboc_solve_batch_ft", "vboc_solve_batch_ft_host", "vboc_rk4_batch", "vboc_rk4_batch_host", "vboc_last_kernel_ms",
            "vboc_kernel_stats", "vboc_debug_counters", "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
@@ -68,6 +68,8 @@ def load():
     lib.vboc_get_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
     lib.vboc_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch), ctypes.c_void_p]
     lib.vboc_solve_batch_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch)]
+    lib.vboc_solve_batch_ft.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch), ctypes.c_void_p]
+    lib.vboc_solve_batch_ft_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch)]
     lib.vboc_rk4_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.vboc_rk4_batch_host.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
@@ -123,9 +125,10 @@ class Solver:
         return v.value
 
     # -- host path --------------------------------------------------------------------------------
-    def solve_host(self, batch):
+    def solve_host(self, batch, free_time=False):
         """batch: dict with N, x_guess[B,nmax+1,nx], u_guess[B,nmax,nu], p, bounds (ics.Batch).
-        Returns dict(status, x, u, cost, sqp_iter, qp_iter)."""
+        Returns dict(status, x, u, cost, sqp_iter, qp_iter).  free_time: the free-time box OCP
+        (vboc_solve_batch_ft_host, OCPpendulum.OCP_solve) instead of the boundary OCP."""
         N = np.ascontiguousarray(batch["N"], dtype=np.int32)
         B = N.shape[0]
         arrs = {k: np.ascontiguousarray(batch[k], dtype=np.float64) for k in FIELDS_IN}
@@ -141,13 +144,15 @@ class Solver:
                   sqp_iter=sqp_iter.ctypes.data, qp_iter=qp_iter.ctypes.data)
         for k, a in arrs.items():
             setattr(b, _CFIELD.get(k, k), a.ctypes.data)
-        _check(self.lib.vboc_solve_batch_host(self.h, ctypes.byref(b)))
+        fn = self.lib.vboc_solve_batch_ft_host if free_time else self.lib.vboc_solve_batch_host
+        _check(fn(self.h, ctypes.byref(b)))
         return dict(status=status, x=x_out, u=u_out, cost=cost, sqp_iter=sqp_iter, qp_iter=qp_iter)
 
     # -- device path (torch tensors resident in HBM) ---------------------------------------------
-    def solve_device(self, tb, out=None, stream=None):
+    def solve_device(self, tb, out=None, stream=None, free_time=False):
         """tb: dict of torch cuda tensors (float64 / int32 for N).  Asynchronous on `stream`
-        (default: torch's current stream).  Returns the output tensor dict."""
+        (default: torch's current stream).  Returns the output tensor dict.  free_time: the
+        free-time box OCP (vboc_solve_batch_ft)."""
         import torch
         N = tb["N"]
         B = N.shape[0]
@@ -166,7 +171,8 @@ class Solver:
             assert t.is_cuda and t.dtype == torch.float64 and t.is_contiguous(), k
             setattr(b, _CFIELD.get(k, k), t.data_ptr())
         st = stream if stream is not None else torch.cuda.current_stream()
-        _check(self.lib.vboc_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        fn = self.lib.vboc_solve_batch_ft if free_time else self.lib.vboc_solve_batch
+        _check(fn(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
         return out
 
     def kernel_stats(self):

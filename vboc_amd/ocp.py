@@ -165,8 +165,8 @@ class OcpSolver:
         return self._stats[field]
 
     def solve(self):
-        b = self._pack()
-        r = self._lib.solve_host(b)
+        b, free_time = self._pack()
+        r = self._lib.solve_host(b, free_time=True) if free_time else self._lib.solve_host(b)
         N = self.N
         self._x_sol = r["x"][0, :N + 1].copy()
         self._u_sol = r["u"][0, :N].copy()
@@ -188,6 +188,9 @@ class OcpSolver:
             raise NotImplementedError("general constraints other than the stage-0 direction "
                                       "constraint (I - d d^T) dtheta_0 = 0 are not supported")
         p = self._p[0]
+        dt = self._lbx[:, 2 * nq]
+        if not (np.all(dt == self._ubx[:, 2 * nq]) and np.all(dt == dt[0])):
+            return self._pack_free_time(p), True
         if nq > 1:
             d = p[:nq] / np.linalg.norm(p[:nq])
             Cexp = np.zeros((nq, 2 * nq + 1))
@@ -201,14 +204,25 @@ class OcpSolver:
             raise NotImplementedError("stage-0 positions must be fixed (lbx_0 == ubx_0)")
         if not np.all(self._lbx[N, nq:2 * nq] == self._ubx[N, nq:2 * nq]):
             raise NotImplementedError("terminal velocities must be fixed (lbx_e == ubx_e)")
-        dt = self._lbx[:, 2 * nq]
-        if not (np.all(dt == self._ubx[:, 2 * nq]) and np.all(dt == dt[0])):
-            raise NotImplementedError("free time (dt not pinned by the bounds) is not supported")
         xg = self._x.copy()
         return dict(N=np.array([N], np.int32), x_guess=xg[None], u_guess=self._u[None].copy(), p=p[None],
                     lbx=self._lbx[1 if N > 1 else 0][None], ubx=self._ubx[1 if N > 1 else 0][None],
                     lbu=self._lbu[0][None], ubu=self._ubu[0][None], lbx0=lbx0[None], ubx0=ubx0[None],
-                    lbxe=self._lbx[N][None], ubxe=self._ubx[N][None])
+                    lbxe=self._lbx[N][None], ubxe=self._ubx[N][None]), False
+
+    def _pack_free_time(self, p):
+        """dt free somewhere: the free-time box OCP (vboc_solve_batch_ft, include/vboc.h) - what
+        OCPpendulum.OCP_solve builds (VBOC/pendulum_class_vboc.py:107-130)."""
+        N = self.N
+        if np.any(self._C):
+            raise NotImplementedError("free-time OCPs with a general constraint C are not supported")
+        lbx, ubx = self._lbx[1 if N > 1 else 0], self._ubx[1 if N > 1 else 0]
+        if N > 1 and not np.all(lbx < ubx):
+            raise NotImplementedError("free-time OCP: path bounds must satisfy lb < ub on every component")
+        return dict(N=np.array([N], np.int32), x_guess=self._x.copy()[None], u_guess=self._u[None].copy(),
+                    p=p[None], lbx=lbx[None], ubx=ubx[None], lbu=self._lbu[0][None], ubu=self._ubu[0][None],
+                    lbx0=self._lbx[0][None], ubx0=self._ubx[0][None], lbxe=self._lbx[N][None],
+                    ubxe=self._ubx[N][None])
 
 
 class _Constraints(SimpleNamespace):
@@ -320,10 +334,26 @@ class OCPpendulum(_Base):
         self.ocp_solver = OcpSolver(self)
 
     def OCP_solve(self, x_sol_guess, u_sol_guess, cost_dir, q_lb, q_ub, q_init, q_fin):
-        # The reference's variant frees dt in [0, 1e-2] with a time-weighted cost (:107-130):
-        # a free-time OCP, which the boundary solver does not implement.
-        raise NotImplementedError("pendulum free-time OCP_solve (VBOC/pendulum_class_vboc.py:107) is not "
-                                  "supported; use the ocp_solver API with pinned dt as pendulum_testdata.py does")
+        """Same contract as VBOC/pendulum_class_vboc.py:107-130: a free-time OCP (dt a state in
+        [0, 1e-2], cost cost_dir * dtheta_0 + sum_k dt_k), solved by vboc_solve_batch_ft."""
+        S = self.ocp_solver
+        if S.N != self.N:
+            S.set_new_time_steps(np.full((self.N,), 1.0))
+        S.reset()
+        N = self.N
+        for i in range(N):
+            S.set(i, "x", np.array(x_sol_guess[i]))
+            S.set(i, "u", np.array(u_sol_guess[i]))
+            S.set(i, "p", np.array([cost_dir, 1.0]))
+            S.constraints_set(i, "lbx", q_lb)
+            S.constraints_set(i, "ubx", q_ub)
+        S.constraints_set(0, "lbx", np.array([q_init, -self.dthetamax, 0.0]))
+        S.constraints_set(0, "ubx", np.array([q_init, self.dthetamax, 1e-2]))
+        S.constraints_set(N, "lbx", np.array([q_fin, 0.0, 0.0]))
+        S.constraints_set(N, "ubx", np.array([q_fin, 0.0, 1e-2]))
+        S.set(N, "x", np.array(x_sol_guess[N]))
+        S.set(N, "p", np.array([cost_dir, 1.0]))
+        return S.solve()
 
 
 class _Integrator:
