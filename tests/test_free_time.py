@@ -98,3 +98,17 @@ def test_dropin_pendulum_ocp_solve_is_the_free_time_problem():
             np.testing.assert_array_equal(o.ocp_solver.get(o.N, "x"), ref["x"][i, o.N])
     finally:
         dropin.use_backend(None)
+
+
+def test_pendulum_vboc_run_on_cpu(tmp_path):
+    """The pendulum main block end to end on the oracle backend (CPU): data, fit, RMSE, artefacts."""
+    import torch
+    from vboc_amd.pipeline import pendulum_vboc_run
+    r = pendulum_vboc_run(str(tmp_path), device="cpu", backend=OracleBackend(1), it_max=300)
+    fx = json.load(open(os.path.join(HERE, "golden", "driver_1.json")))
+    np.testing.assert_array_equal(r["X"], np.array(fx["X_save"]))
+    assert r["fit"]["iterations"] <= 300 and np.isfinite(r["rmse"])
+    np.testing.assert_array_equal(np.load(tmp_path / "data_1dof_vboc_10.npy"), r["X"])
+    sd = torch.load(tmp_path / "model_1dof_vboc_10", weights_only=True)
+    assert sd["linear_relu_stack.0.weight"].shape == (100, 2)
+    assert torch.load(tmp_path / "mean_1dof_vboc_10", weights_only=True) == r["mean"]

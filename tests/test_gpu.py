@@ -277,3 +277,14 @@ def test_pendulum_data_generation_on_gpu_matches_reference_loop():
     G = np.array(fx["X_save"])
     assert X.shape == G.shape
     np.testing.assert_allclose(X, G, atol=1e-6)
+
+
+def test_pendulum_vboc_run_on_gpu(tmp_path):
+    """VBOC/pendulum_vboc.py's main block on one MI355X: free-time data generation on the HIP solver,
+    the 2-100-1 fit replayed from a HIP graph with the reference's stop rule, RMSE, artefacts."""
+    from vboc_amd.pipeline import pendulum_vboc_run
+    r = pendulum_vboc_run(str(tmp_path), device="cuda")
+    assert r["X"].shape[0] > 50
+    assert r["fit"]["val"] <= 1e-4 or r["fit"]["iterations"] >= 100 * int(r["X"].shape[0] * 100 / 64)
+    assert r["rmse"] < 1.0
+    assert (tmp_path / "model_1dof_vboc_10").exists()

@@ -149,3 +149,32 @@ def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None,
     if rank0 and out_dir is not None:
         save_artifacts(out_dir, nq, X_save, mean, std, trainer.model, times, rmse)
     return dict(X_save=X_save, mean=mean, std=std, trainer=trainer, times=times, rmse=rmse, stats=stats, fits=fits)
+
+
+def pendulum_vboc_run(out_dir=None, device="cuda", seed=0, backend=None, it_max=None):
+    """VBOC/pendulum_vboc.py's main block: the simplified data generation (two free-time sweeps,
+    :52-223, drivers.pendulum_data_generation), features [(q - mean) / std, sign(dq), |dq|] (:226-236),
+    the 2-100-1 fit (Adam lr 1e-3, minibatch 64, EMA beta 0.8, stop at val <= 1e-4 or it_max =
+    100 * int(n * 100 / 64) steps, :241-277), the RMSE on the training data (:296-301) and the
+    artefacts data_1dof_vboc_10.npy, model_/mean_/std_1dof_vboc_10 (:239, :290-292).
+    Difference kept explicit: rows with dq = 0 get direction 0 here; the reference leaves that entry
+    of an np.empty array uninitialised (:230-235).  Returns dict(X, rmse, fit, stats)."""
+    import torch
+    from .drivers import GpuBackend, pendulum_data_generation
+    backend = backend or GpuBackend(1, nmax=200)
+    X, stats = pendulum_data_generation(backend)
+    mean, std = position_stats(X, 1)
+    F = dir_features(X, mean, std, 1)
+    tr = DirTrainer(1, device=device, beta=0.8, stop_val=1e-4, seed=seed)
+    B = int(X.shape[0] * 100 / tr.k)
+    # the reference counts it from 0 (`while val > 1e-4 and it < it_max`), the trainer from 1
+    fit = tr.fit(F, it_max=(it_max or B * 100) + 1)
+    rmse = tr.rmse(F)
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        np.save(os.path.join(out_dir, "data_1dof_vboc_10.npy"), np.asarray(X))
+        torch.save({k: v.detach().cpu() for k, v in tr.model.state_dict().items()},
+                   os.path.join(out_dir, "model_1dof_vboc_10"))
+        torch.save(mean, os.path.join(out_dir, "mean_1dof_vboc_10"))
+        torch.save(std, os.path.join(out_dir, "std_1dof_vboc_10"))
+    return dict(X=X, rmse=rmse, fit=fit, stats=stats, mean=mean, std=std)
