@@ -96,7 +96,10 @@ int vboc_destroy(vboc_handle h);
 /* Solver options (names of AcadosOcpOptions): "nlp_solver_tol_stat", "nlp_solver_tol_eq",
  * "nlp_solver_tol_ineq", "nlp_solver_tol_comp", "nlp_solver_max_iter", "qp_solver_iter_max",
  * "qp_solver_tol_stat", "qp_solver_tol_eq", "qp_solver_tol_comp", "levenberg_marquardt",
- * "alpha_min", "alpha_reduction"; interior-point internals "ipm_mu0", "ipm_push", "ipm_tau". */
+ * "alpha_min", "alpha_reduction"; interior-point internals "ipm_mu0", "ipm_push", "ipm_tau";
+ * scheduling: "wave_groups" (resident problems of the wave solver, 0 = automatic) and "mall_mib"
+ * (automatic sizing: the resident problems' hot stage records fit this much Infinity Cache, default
+ * 256). */
 int vboc_set_option(vboc_handle h, const char* field, double value);
 int vboc_get_option(vboc_handle h, const char* field, double* value);
 

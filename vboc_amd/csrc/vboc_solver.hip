@@ -1313,6 +1313,7 @@ struct vboc_solver {
   bool wave_all = true;
   double* regions = nullptr;
   long long n_regions = 0, region_doubles = 0, group_cap = 0;
+  double mall_mib = 256.0;          // MALL budget for the resident problems' hot stage fields (0: off)
   size_t wave_lds = 0;
   bool coop_ok = false;
   long long coop_count = 0;
@@ -1424,10 +1425,23 @@ static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
+// Resident wave-solver problems for a batch whose horizons are <= nmax: every IPM pass streams each
+// problem's hot stage fields [0, OX) (170 KB for the triple at N = 100), so the set of resident problems
+// is sized to stay inside the 256 MiB MALL (Infinity Cache) of MI355X - measured on the 100k triple
+// batch (profiles/r01_wave_groups_sweep.log): 1024 groups 5434, 1408 groups 6212, 2048 groups 5504
+// solves/s.  `wave_groups` overrides; `mall_mib` changes the budget.
+static long long wave_group_budget(const vboc_solver* h, int nmax) {
+  const long long hot = (long long)(h->nq == 1 ? WaveLayout<1>::OX : (h->nq == 2 ? WaveLayout<2>::OX : WaveLayout<3>::OX)) *
+                        (long long)(nmax + 1) * (long long)sizeof(double);
+  const long long g = (long long)(0.92 * h->mall_mib * 1024.0 * 1024.0) / (hot > 0 ? hot : 1);
+  return g < 256 ? 256 : g;
+}
+
 static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs, hipStream_t st, const Work& w,
                               const Inputs& in, const SlotState& ss) {
   long long groups = jobs < h->n_regions ? jobs : h->n_regions;
-  if (h->group_cap > 0 && groups > h->group_cap) groups = h->group_cap;
+  const long long cap = h->group_cap > 0 ? h->group_cap : (h->mall_mib > 0 ? wave_group_budget(h, in.nmax) : 0);
+  if (cap > 0 && groups > cap) groups = cap;
   if (groups < 1) return hipSuccess;
   const dim3 grid((unsigned)groups), block(64);
   switch (h->nq) {
@@ -1560,6 +1574,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "coop_threshold") h->coop_threshold = v;
   else if (s == "wave_all") h->wave_all = v != 0.0;
   else if (s == "wave_groups") h->group_cap = (long long)v;
+  else if (s == "mall_mib") h->mall_mib = v;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
     if (h->profile && h->pev.empty()) {
@@ -1594,6 +1609,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "coop_available") *v = h->coop_ok ? 1.0 : 0.0;
   else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
   else if (s == "wave_groups") *v = (double)h->n_regions;
+  else if (s == "mall_mib") *v = h->mall_mib;
   else if (s == "coop_problems") *v = (double)h->coop_count;
   else if (s == "slots") *v = (double)h->slots;
   else if (s == "workspace_bytes") *v = (double)h->pool_bytes;
