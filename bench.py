@@ -34,6 +34,23 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak
 F_DYN = {3: 6382, 2: 2146, 1: 4 * 14 + 8 * 9 * 4 + 8 * 3 * 4 + 6}
 F_IPM = {3: 3513, 2: 1346, 1: int(2 * 9 * 4 + 2 * 3 * 16 + 64 / 3 + 8 * 16)}
 C_F = {3: 183, 2: 52, 1: 8}
+# UR5 arm (config 5, n = 8, m = 4): same convention; C_f / C_fJ are the sympy CSE op counts of the
+# urdf2casadi-style ABA restatement (oracle/ur5_rbd.py, tools/ur5_flops.py -> tests/golden/flops.json "4")
+_UR5_CF, _UR5_CFJ = None, None
+
+
+def _ur5_counts():
+    import json as _j
+    d = _j.load(open(os.path.join(ROOT, "tests", "golden", "flops.json"))).get("4")
+    return (d["C_f"], d["C_fJ"]) if d else (None, None)
+
+
+_UR5_CF, _UR5_CFJ = _ur5_counts()
+if _UR5_CF:
+    _n, _m = 8, 4
+    F_DYN[4] = 4 * _UR5_CFJ + 8 * _n * _n * (_n + _m) + 8 * _n * (_n + _m) + 2 * _n
+    F_IPM[4] = int(2 * _n * _n * (_n + _m) + 2 * _n * (_n + _m) ** 2 + (_n + _m) ** 3 / 3 + 8 * (_n + _m) ** 2)
+    C_F[4] = _UR5_CF
 
 
 def pmc_traffic(kernel):
@@ -50,8 +67,8 @@ def pmc_traffic(kernel):
 
 def make_batch(nq, ids, device):
     import torch
-    from vboc_amd.ics import data_generation_ics
-    b = data_generation_ics(nq, ids)
+    from vboc_amd.ics import data_generation_ics, ur5_ics
+    b = ur5_ics(ids) if nq == 4 else data_generation_ics(nq, ids)
     keys = ("N", "x_guess", "u_guess", "p", "lbx", "ubx", "lbu", "ubu", "lbx0", "ubx0", "lbxe", "ubxe")
     return {k: torch.as_tensor(np.ascontiguousarray(b[k]), device=device) for k in keys}, b
 
@@ -60,11 +77,11 @@ def cpu_baseline(nq, B, seconds, threads):
     """Oracle (CPU FP64 restatement) on the first problems of the workload for ~`seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    from vboc_amd.ics import data_generation_ics
+    from vboc_amd.ics import data_generation_ics, ur5_ics
     done, t_total, n = 0, 0.0, max(threads, 8)
     start = 0
     while t_total < seconds and start < B:
-        b = data_generation_ics(nq, np.arange(start, start + n))
+        b = ur5_ics(np.arange(start, start + n)) if nq == 4 else data_generation_ics(nq, np.arange(start, start + n))
         t0 = time.time()
         oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
                            b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], nthreads=threads)
@@ -75,13 +92,25 @@ def cpu_baseline(nq, B, seconds, threads):
     return done / t_total, done, t_total
 
 
+NAMES = {1: "pendulum", 2: "double pendulum", 3: "triple pendulum", 4: "UR5 arm"}
+WORKLOAD = {
+    3: "triple-pendulum data_generation first OCP solve, N=100, {B} ICs per GPU per step (configs[2]; configs[3] "
+       "at 8 GPUs)",
+    2: "double-pendulum data_generation first OCP solve, N=100, {B} ICs per GPU per step (configs[1])",
+    1: "pendulum data_generation first OCP solve, N=50, {B} ICs per GPU per step",
+    4: "UR5 (4 revolute joints of ur5.urdf) testing_test first OCP solve, N=100, {B} ICs per GPU per step "
+       "(configs[4]: 100k states; 8 GPUs at N=8)",
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=100_000, help="problems per GPU per step (configs[2]: 100k)")
-    ap.add_argument("--nq", type=int, default=3)
+    ap.add_argument("--nq", type=int, default=3,
+                    help="3: triple pendulum (BASELINE metric); 2 / 1: double / pendulum; 4: UR5 arm (configs[4])")
     ap.add_argument("--slots", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -104,8 +133,11 @@ def main():
 
     from vboc_amd import lib
     nq, B = args.nq, args.batch
+    if nq == 4:
+        args.mode = "lane"   # the UR5 arm is solved by the lane-per-problem kernels
     solver = lib.Solver(nq, 100, slots=args.slots, device=local)
-    solver.set_option("wave_all", 1 if args.mode == "wave" else 0)
+    if nq != 4:
+        solver.set_option("wave_all", 1 if args.mode == "wave" else 0)
     solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
     stream = torch.cuda.current_stream(device)
 
@@ -180,7 +212,7 @@ def main():
                "sample": f"first {n} problems of the same workload (oracle/vboc_oracle.c, OpenMP, {t:.1f} s)"}
 
     if args.mode == "lane":
-        traffic_gb, traffic_src = pmc_traffic("k_qp_factor")
+        traffic_gb, traffic_src = pmc_traffic("k_qp_factor" if nq == 3 else f"k_qp_factor_nq{nq}")
         roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1) if achieved_gbs else None,
                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved_gbs / HBM_PEAK_GBS, 4) if achieved_gbs else None,
@@ -204,7 +236,8 @@ def main():
                     "avg_launch_ms": round(avg_ms, 3), "launches": wave_launch}
     if rank == 0:
         line = {
-            "metric": "VBOC boundary OCP solves/sec, triple pendulum, 1/2/4/8 MI355X",
+            "metric": "VBOC boundary OCP solves/sec, triple pendulum, 1/2/4/8 MI355X" if nq == 3 else
+                      f"VBOC boundary OCP solves/sec, {NAMES[nq]}, 1/2/4/8 MI355X",
             "value": round(value, 2),
             "unit": "solves/s",
             "n_gpus": world,
@@ -215,9 +248,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (Philox-seeded ICs by the reference's data_generation law)",
-            "config": {"workload": f"{'triple' if nq == 3 else nq}-pendulum data_generation first OCP solve, "
-                                   f"N=100, {B} ICs per GPU per step (configs[2]; configs[3] at 8 GPUs)",
+            "data": "synthetic (Philox-seeded ICs by the reference's " +
+                    ("testing_test law, VBOC/UR5/vboc_multiprocessing_ur5.py)" if nq == 4 else "data_generation law)"),
+            "config": {"workload": WORKLOAD[nq].format(B=B),
                        "problems_per_gpu": B, "horizon": 100, "parallelism": f"dp{world}", "mode": args.mode,
                        "allgather": world > 1},
             "roofline": roofline,

@@ -25,8 +25,14 @@
  *   vboc_last_error        <- Python exceptions raised by acados_template on bad fields
  *
  * Problem layout (problem-major, exactly the numpy arrays the reference passes, float64):
- *   nq = number of links (1 pendulum, 2 double, 3 triple); nx = 2*nq+1 (theta, dtheta, dt);
- *   nu = nq; np = nq+1 (w_1..w_nq, w_t).
+ *   nq = number of links (1 pendulum, 2 double, 3 triple) or 4 = the UR5 arm of
+ *   VBOC/UR5/ur5reduced_class_fixedveldir.py (4 revolute joints of ur5.urdf, rigid-body dynamics);
+ *   nx = 2*nq+1 (theta, dtheta, dt); nu = nq; np = nq+1 (w_1..w_nq, w_t).
+ *   The UR5 OCP has no dt state (x = [q, qdot], p = w, tf = 1 over N = 100 intervals): its shooting
+ *   interval (set_new_time_steps, dt_sym = 1e-2) travels in the dt column, and p[nq] = 0.  Its
+ *   OCPUR5INIT.OCP_solve (:145-192) is otherwise the same boundary problem; levenberg_marquardt defaults
+ *   to 1e-2 on an nq = 4 handle (:131).  nq = 4 is solved by the lane-per-problem kernels (wave_all
+ *   is 0 and cannot be set) and has no free-time variant.
  *   N[b]                 horizon of problem b (<= nmax of the handle)
  *   x_guess[b][nmax+1][nx]  stage guesses; row N[b] is the stage-N guess (OCP_solve sets it from
  *                        x_sol_guess[-1], triplependulum_class_vboc.py:185)
@@ -88,7 +94,7 @@ typedef struct {
   int* qp_iter;
 } vboc_batch_t;
 
-/* Create a solver for nq links with horizons up to nmax on HIP device `device`.  `slots` is the
+/* Create a solver for nq links (4 = UR5) with horizons up to nmax on HIP device `device`.  `slots` is the
  * number of concurrently resident problems (lanes) of the persistent kernel; 0 = default. */
 int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out);
 int vboc_destroy(vboc_handle h);
@@ -128,6 +134,11 @@ int vboc_solve_batch_ft_host(vboc_handle h, const vboc_batch_t* batch);
  * x[B][2nq], u[B][nq] -> x_out[B][2nq].  Device pointers (async) / host pointers (sync). */
 int vboc_rk4_batch(int nq, int B, double T, const double* x, const double* u, double* x_out, void* stream);
 int vboc_rk4_batch_host(int nq, int B, double T, const double* x, const double* u, double* x_out);
+/* The solvers' linearisation, standalone: one ERK4 step of length T with its forward sensitivities
+ * (ACADOS ERK forward VDE, the shooting Jacobians of every SQP iteration) for B states, host pointers:
+ * x[B][2nq], u[B][nq] -> x_out[B][2nq], A[B][2nq][2nq] = dx_out/dx, Bm[B][2nq][nq] = dx_out/du. */
+int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const double* u, double* x_out, double* A,
+                             double* Bm);
 
 /* Device time of the last vboc_solve_batch* call's solver kernel in milliseconds (HIP events on
  * the call's stream) and the number of kernel launches it used. */

@@ -103,7 +103,8 @@ def solve_batch(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe
     x_out = np.zeros_like(arrs[0])
     u_out = np.zeros_like(arrs[1])
     res = np.zeros(B, dtype=RESULT_DTYPE)
-    o = opts if opts is not None else default_opts()
+    # the UR5 OCP sets levenberg_marquardt = 1e-2 (VBOC/UR5/ur5reduced_class_fixedveldir.py:135)
+    o = opts if opts is not None else default_opts(**({"lm": 1e-2} if nq == 4 else {}))
     nthreads = nthreads or os.cpu_count()
     fn = lib().vboc_oracle_ft_solve_batch if free_time else lib().vboc_oracle_solve_batch
     rc = fn(nq, B, Nmax, _p(N), *[_p(a) for a in arrs], ctypes.byref(o),

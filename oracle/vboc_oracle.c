@@ -31,6 +31,7 @@
  *  - stage N: velocities fixed by lbx_e == ubx_e (q_fin, :183-184) => equality E x_N = v_fin,
  *    handled exactly in the Riccati recursion through its multiplier nu.
  */
+#include <complex.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -40,17 +41,18 @@
 #include <stdio.h>
 #endif
 
-#define NQ 3
-#define NX 6
-#define NU 3
-#define NZ 9
+/* capacities: up to 4 joints (pendulum 1, double 2, triple 3, UR5 arm 4) */
+#define NQ 4
+#define NX 8
+#define NU 4
+#define NZ 12
 
 /* ------------------------------------------------------------------------------------------ */
 /* model                                                                                       */
 /* ------------------------------------------------------------------------------------------ */
 
 typedef struct {
-  int nq, nx, nu, chain;
+  int nq, nx, nu, chain, ur5;
   double g, mu[NQ], l[NQ], a[NQ][NQ];
   double pm, pd, pb; /* damped pendulum: mass, rod length, damping */
 } model_t;
@@ -61,12 +63,16 @@ static void model_init(model_t* m, int nq) {
   memset(m, 0, sizeof(*m));
   m->nq = nq; m->nx = 2 * nq; m->nu = nq;
   m->g = 9.81;
+  if (nq == 4) {                 /* UR5 arm, VBOC/UR5/ur5reduced_class_fixedveldir.py:20-45 */
+    m->chain = 0; m->ur5 = 1;
+    return;
+  }
   if (nq == 1) {
     m->chain = 0; m->pm = 0.5; m->pd = 0.3; m->pb = 0.01;
     return;
   }
   m->chain = 1;
-  double mass[NQ] = {0.4, 0.4, 0.4};
+  double mass[NQ] = {0.4, 0.4, 0.4, 0.0};
   for (int j = 0; j < nq; ++j) m->l[j] = 0.8;
   for (int j = 0; j < nq; ++j) {
     m->mu[j] = 0.0;
@@ -107,6 +113,136 @@ static void chol_solve(int n, const double* L, double* b) {
   }
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* UR5 arm (nq = 4): rigid-body chain of VBOC/UR5/ur5reduced_class_fixedveldir.py:20-45, whose  */
+/* f_expl = [qdot; ABA(q, qdot, u)] comes from urdf2casadi (un-vendored, unpinned).  Parameters  */
+/* (joint tree transforms, merged body inertias) are generated from VBOC/UR5/ur5.urdf by         */
+/* tools/gen_ur5_model.py.  The oracle solves M(q) acc = u - RNEA(q, qdot, 0) with M from RNEA   */
+/* columns and differentiates RNEA by the complex step (Im f(x + i h) / h, h = 1e-30: exact to   */
+/* rounding, independent of the GPU's dual-number JVPs).                                        */
+/* ------------------------------------------------------------------------------------------ */
+#include "../vboc_amd/csrc/ur5_params.h"
+
+typedef double complex cplx;
+
+static void c_cross(const cplx* a, const cplx* b, cplx* o) {
+  cplx t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  o[0] = t0; o[1] = t1; o[2] = t2;
+}
+
+/* tau = RNEA(q, qd, qdd) in body coordinates; grav = 0 drops gravity (mass-matrix columns).
+ * Joint i: child frame = joint frame (UR5_R, UR5_P in the parent body) rotated by Rz(q_i);
+ * motion transform E = Rz(q)^T R^T, r = P:  X(w, v) = (E w, E (v - r x w)). */
+static void ur5_rnea(const cplx* q, const cplx* qd, const cplx* qdd, int grav, cplx* tau) {
+  cplx E[4][9], w[4][3], v[4][3], aw[4][3], av[4][3], fn[4][3], ff[4][3];
+  cplx wp[3] = {0, 0, 0}, vp[3] = {0, 0, 0}, awp[3] = {0, 0, 0}, avp[3] = {0, 0, grav ? 9.81 : 0.0};
+  for (int i = 0; i < 4; ++i) {
+    const double* R = UR5_R + 9 * i;
+    const double* P = UR5_P + 3 * i;
+    cplx c = ccos(q[i]), s = csin(q[i]);
+    /* E = Rz(q)^T R^T: row a of Rz^T = (c, s, 0), (-s, c, 0), (0, 0, 1); R^T[b][k] = R[k][b] */
+    for (int k = 0; k < 3; ++k) {
+      E[i][0 * 3 + k] = c * R[k * 3 + 0] + s * R[k * 3 + 1];
+      E[i][1 * 3 + k] = -s * R[k * 3 + 0] + c * R[k * 3 + 1];
+      E[i][2 * 3 + k] = R[k * 3 + 2];
+    }
+    cplx r[3] = {P[0], P[1], P[2]}, t[3], t2[3], ew[3], ev[3], eaw[3], eav[3];
+    c_cross(r, wp, t);
+    for (int a = 0; a < 3; ++a) t[a] = vp[a] - t[a];
+    c_cross(r, awp, t2);
+    for (int a = 0; a < 3; ++a) t2[a] = avp[a] - t2[a];
+    for (int a = 0; a < 3; ++a) {
+      ew[a] = E[i][a * 3] * wp[0] + E[i][a * 3 + 1] * wp[1] + E[i][a * 3 + 2] * wp[2];
+      ev[a] = E[i][a * 3] * t[0] + E[i][a * 3 + 1] * t[1] + E[i][a * 3 + 2] * t[2];
+      eaw[a] = E[i][a * 3] * awp[0] + E[i][a * 3 + 1] * awp[1] + E[i][a * 3 + 2] * awp[2];
+      eav[a] = E[i][a * 3] * t2[0] + E[i][a * 3 + 1] * t2[1] + E[i][a * 3 + 2] * t2[2];
+    }
+    /* v_i = X v_p + z qd ; a_i = X a_p + z qdd + v_i x_m (z qd) */
+    for (int a = 0; a < 3; ++a) { w[i][a] = ew[a]; v[i][a] = ev[a]; }
+    w[i][2] += qd[i];
+    cplx zq[3] = {0, 0, qd[i]}, cw[3], cv[3];
+    c_cross(w[i], zq, cw);
+    c_cross(v[i], zq, cv);
+    for (int a = 0; a < 3; ++a) { aw[i][a] = eaw[a] + cw[a]; av[i][a] = eav[a] + cv[a]; }
+    aw[i][2] += qdd[i];
+    /* f_i = I a_i + v_i x_f (I v_i);  I (w, v) = (Io w + mc x v, m v - mc x w) */
+    const double* Io = UR5_IO + 9 * i;
+    const double m = UR5_M[i];
+    cplx mc[3] = {UR5_MC[3 * i], UR5_MC[3 * i + 1], UR5_MC[3 * i + 2]};
+    cplx hA[3], hL[3], iaA[3], iaL[3], x1[3], x2[3];
+    c_cross(mc, v[i], x1);
+    c_cross(mc, w[i], x2);
+    for (int a = 0; a < 3; ++a) {
+      hA[a] = Io[a * 3] * w[i][0] + Io[a * 3 + 1] * w[i][1] + Io[a * 3 + 2] * w[i][2] + x1[a];
+      hL[a] = m * v[i][a] - x2[a];
+    }
+    c_cross(mc, av[i], x1);
+    c_cross(mc, aw[i], x2);
+    for (int a = 0; a < 3; ++a) {
+      iaA[a] = Io[a * 3] * aw[i][0] + Io[a * 3 + 1] * aw[i][1] + Io[a * 3 + 2] * aw[i][2] + x1[a];
+      iaL[a] = m * av[i][a] - x2[a];
+    }
+    cplx y1[3], y2[3], y3[3];
+    c_cross(w[i], hA, y1);
+    c_cross(v[i], hL, y2);
+    c_cross(w[i], hL, y3);
+    for (int a = 0; a < 3; ++a) { fn[i][a] = iaA[a] + y1[a] + y2[a]; ff[i][a] = iaL[a] + y3[a]; }
+    for (int a = 0; a < 3; ++a) { wp[a] = w[i][a]; vp[a] = v[i][a]; awp[a] = aw[i][a]; avp[a] = av[i][a]; }
+  }
+  /* backward: tau_i = z . n_i ; f_{i-1} += X_i^T f_i = (E^T n + r x E^T f, E^T f) */
+  for (int i = 3; i >= 0; --i) {
+    tau[i] = fn[i][2];
+    if (i == 0) break;
+    const double* P = UR5_P + 3 * i;
+    cplx r[3] = {P[0], P[1], P[2]}, en[3], ef[3], x[3];
+    for (int a = 0; a < 3; ++a) {
+      en[a] = E[i][a] * fn[i][0] + E[i][3 + a] * fn[i][1] + E[i][6 + a] * fn[i][2];
+      ef[a] = E[i][a] * ff[i][0] + E[i][3 + a] * ff[i][1] + E[i][6 + a] * ff[i][2];
+    }
+    c_cross(r, ef, x);
+    for (int a = 0; a < 3; ++a) { fn[i - 1][a] += en[a] + x[a]; ff[i - 1][a] += ef[a]; }
+  }
+}
+
+static void ur5_eval(const double* th, const double* om, const double* u, double* acc, double* Jth,
+                     double* Jom, double* Ju) {
+  cplx q[4], qd[4], qdd[4], tau[4];
+  double M[16], L[16];
+  for (int j = 0; j < 4; ++j) { q[j] = th[j]; qd[j] = om[j]; qdd[j] = 0.0; }
+  /* M e_c = RNEA(q, 0, e_c) without gravity */
+  cplx z4[4] = {0, 0, 0, 0};
+  for (int c = 0; c < 4; ++c) {
+    for (int j = 0; j < 4; ++j) qdd[j] = (j == c) ? 1.0 : 0.0;
+    ur5_rnea(q, z4, qdd, 0, tau);
+    for (int j = 0; j < 4; ++j) M[j * 4 + c] = creal(tau[j]);
+  }
+  for (int j = 0; j < 4; ++j) qdd[j] = 0.0;
+  ur5_rnea(q, qd, qdd, 1, tau);
+  for (int j = 0; j < 4; ++j) acc[j] = u[j] - creal(tau[j]);
+  memcpy(L, M, sizeof(M));
+  chol(4, L);
+  chol_solve(4, L, acc);
+  if (!Jth) return;
+  const double hs = 1e-30;
+  double col[4];
+  for (int j = 0; j < 4; ++j) qdd[j] = acc[j];
+  for (int c = 0; c < 8; ++c) {
+    cplx qq[4], qv[4];
+    for (int j = 0; j < 4; ++j) { qq[j] = th[j]; qv[j] = om[j]; }
+    if (c < 4) qq[c] += I * hs; else qv[c - 4] += I * hs;
+    ur5_rnea(qq, qv, qdd, 1, tau);
+    for (int j = 0; j < 4; ++j) col[j] = -cimag(tau[j]) / hs;   /* d acc = -M^-1 d RNEA|acc */
+    chol_solve(4, L, col);
+    double* J = (c < 4) ? Jth : Jom;
+    for (int j = 0; j < 4; ++j) J[j * 4 + (c & 3)] = col[j];
+  }
+  for (int c = 0; c < 4; ++c) {
+    for (int j = 0; j < 4; ++j) col[j] = (j == c) ? 1.0 : 0.0;
+    chol_solve(4, L, col);
+    for (int j = 0; j < 4; ++j) Ju[j * 4 + c] = col[j];
+  }
+}
+
 /* Accelerations and their Jacobians.  Point-mass chain (mass m_i at the tip of massless link
  * l_i, absolute angles from the downward vertical, generalised forces = C_i):
  *   M(th) acc = u - cor(th, om) - grav(th),   M_jk = a_jk cos(th_j - th_k),
@@ -117,6 +253,10 @@ static void chol_solve(int n, const double* L, double* b) {
 static void model_eval(const model_t* m, const double* th, const double* om, const double* u,
                        double* acc, double* Jth, double* Jom, double* Ju) {
   const int n = m->nq;
+  if (m->ur5) {
+    ur5_eval(th, om, u, acc, Jth, Jom, Ju);
+    return;
+  }
   if (!m->chain) {
     double inv = 1.0 / (m->pd * m->pd * m->pm);
     acc[0] = (m->pm * m->g * m->pd * sin(th[0]) + u[0] - m->pb * om[0]) * inv;

@@ -25,8 +25,13 @@ The pendulum's data generation (VBOC/pendulum_vboc.py:52-205) lives in the scrip
 function: its `for v_sel in [v_min, v_max]:` loop is taken by AST and run against the drop-in
 OCPpendulum (free-time OCP_solve) with the oracle's free-time solver injected; the fixture is X_save.
 
-Usage: python tests/golden/make_driver_golden.py [dg|test|pend]
-  ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json, tests/golden/driver_1.json
+The UR5's `testing_test` (VBOC/UR5/vboc_multiprocessing_ur5.py:369-466, what that script's main block fans
+out for its test and training sets) is extracted the same way and run against the drop-in OCPUR5INIT
+(vboc_amd.ur5) with the oracle injected; `random` serves the problem's ics.UR5_STREAM block.
+
+Usage: python tests/golden/make_driver_golden.py [dg|test|pend|ur5]
+  ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json, tests/golden/driver_1.json,
+      tests/golden/testing_ur5.json
 """
 import ast
 import json
@@ -229,6 +234,34 @@ def main_pendulum():
         json.dump({"nq": 1, "N_start": PEND_N_START, "eps": PEND_EPS, "X_save": X.tolist()}, f)
 
 
+UR5_IDS = list(range(0, 40))
+UR5_FAIL_MOD = 7   # a few forced failures exercise the None branch
+
+
+def main_ur5():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_backend import OracleOcpBackend
+    from vboc_amd import ocp as dropin
+    from vboc_amd.ics import UR5_DRAWS, UR5_STREAM
+    from vboc_amd.ur5 import OCPUR5INIT
+    dropin.use_backend(OracleOcpBackend(UR5_FAIL_MOD))
+    code = extract(os.path.join(REF, "UR5", "vboc_multiprocessing_ur5.py"), "testing_test")
+    ocp = OCPUR5INIT()
+    g = dict(np=np, norm=norm, ocp=ocp, x_min=ocp.xmin, x_max=ocp.xmax, N_start=100, dt_sym=1e-2,
+             tol=ocp.ocp.solver_options.nlp_solver_tol_stat)
+    exec(code, g)
+    U = uniforms(np.array(UR5_IDS), UR5_DRAWS, SEED, stream=UR5_STREAM)
+    out = []
+    for b, pid in enumerate(UR5_IDS):
+        # testing_test draws exactly UR5_DRAWS numbers; a further draw would come from stream 6 and break parity
+        g["random"] = FakeRandom(U[b], ProblemRNG(pid, SEED, stream=UR5_STREAM + 1))
+        out.append(tolist(g["testing_test"](pid)))
+        print("ur5", pid, out[-1], flush=True)
+    with open(os.path.join(HERE, "testing_ur5.json"), "w") as f:
+        json.dump({"nq": 4, "ids": UR5_IDS, "N_start": 100, "seed": SEED, "fail_mod": UR5_FAIL_MOD,
+                   "results": out}, f)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("dg", "all"):
@@ -237,3 +270,5 @@ if __name__ == "__main__":
         main_testing()
     if what in ("pend", "all"):
         main_pendulum()
+    if what in ("ur5", "all"):
+        main_ur5()

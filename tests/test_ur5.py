@@ -1,0 +1,337 @@
+"""UR5 arm (BASELINE config 5) on CPU: the dynamics restatement, the oracle, the
+drop-in classes and the batched `testing_test` driver.
+
+Dynamics parity with urdf2casadi itself is UNPINNED: it is an un-vendored, un-pinned dependency that is not
+installed, and the reference stores no output of it.  What pins the model here:
+  * two independent restatements agree to rounding - oracle/ur5_rbd.py (urdf2casadi's 6x6 spatial-algebra
+    ABA over the RAW URDF chain, tests/golden/ur5_urdf.json) and the C oracle's RNEA over the generated
+    parameters (vboc_amd/csrc/ur5_params.h, which the HIP kernels compile);
+  * physics: the energy of the unforced motion is conserved, with kinetic and potential energy computed from
+    independently composed link poses (a wrong inertia, Coriolis term or gravity direction breaks it);
+    M(q) is symmetric positive definite;
+  * the oracle's complex-step Jacobians equal central differences of the numpy ABA.
+The driver fixture tests/golden/testing_ur5.json is the reference's own `testing_test` (AST-extracted from
+VBOC/UR5/vboc_multiprocessing_ur5.py) run on the drop-in OCPUR5INIT with the oracle injected."""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+from oracle_backend import OracleBackend, OracleOcpBackend, _oracle_solve  # noqa: E402
+
+
+def _rbd():
+    import ur5_rbd
+    return ur5_rbd.UR5()
+
+
+def _states(n, seed):
+    rng = np.random.default_rng(seed)
+    return rng.uniform(-3, 3, (n, 4)), rng.uniform(-3, 3, (n, 4)), rng.uniform(-60, 60, (n, 4))
+
+
+def test_chain_is_the_reference_model():
+    m = _rbd()
+    assert m.nq == 4                                    # wrist_2 / wrist_3 are fixed joints (ur5.urdf:266-279)
+    names = [it["name"] for it in m.chain if it["kind"] == "joint" and it["type"] == "revolute"]
+    assert names == ["shoulder_pan_joint", "shoulder_lift_joint", "elbow_joint", "wrist_1_joint"]
+    assert m.chain[0]["name"] == "base_link" and m.chain[-1]["name"] == "tool0"
+
+
+def test_generated_params_equal_the_urdf2casadi_model():
+    """csrc/ur5_params.h / ur5_params.json (compact body-frame parameters) against the 6x6 model the
+    urdf2casadi restatement builds from the raw chain: transforms at random q and merged inertias."""
+    import ur5_rbd
+    from vboc_amd.ur5 import params
+    P = params()
+    m = _rbd()
+    for q in np.random.default_rng(1).uniform(-3, 3, (4, 4)):
+        Xs, S, Is = m.model(q)
+        for i in range(4):
+            c, s = np.cos(q[i]), np.sin(q[i])
+            Rz = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+            E = (np.asarray(P["joints"][i]["R"]) @ Rz).T
+            np.testing.assert_allclose(Xs[i], ur5_rbd.spatial_transform(E, np.asarray(P["joints"][i]["p"])),
+                                       atol=1e-12)
+            b = P["bodies"][i]
+            cx = ur5_rbd.skew(b["m"] * np.asarray(b["com"]))
+            I6 = np.block([[np.asarray(b["Io"]), cx], [cx.T, b["m"] * np.eye(3)]])
+            np.testing.assert_allclose(Is[i], I6, atol=1e-12)
+    # the header carries the same numbers
+    txt = open(os.path.join(ROOT, "vboc_amd", "csrc", "ur5_params.h")).read()
+    mass = [float(v) for v in txt.split("#define UR5_M_INIT {")[1].split("}")[0].split(",")]
+    np.testing.assert_array_equal(mass, [b["m"] for b in P["bodies"]])
+
+
+def test_oracle_rnea_matches_aba_restatement():
+    import oracle
+    m = _rbd()
+    Q, V, U = _states(24, 0)
+    for q, qd, u in zip(Q, V, U):
+        acc, Jth, Jom, Ju = oracle.model(4, q, qd, u)
+        np.testing.assert_allclose(acc, m.aba(q, qd, u), rtol=1e-11, atol=1e-9)
+        e = 1e-6
+        fd_q = np.stack([(m.aba(q + e * d, qd, u) - m.aba(q - e * d, qd, u)) / (2 * e) for d in np.eye(4)], 1)
+        fd_v = np.stack([(m.aba(q, qd + e * d, u) - m.aba(q, qd - e * d, u)) / (2 * e) for d in np.eye(4)], 1)
+        scale = 1.0 + np.abs(fd_q).max()
+        assert np.abs(fd_q - Jth).max() < 1e-6 * scale
+        assert np.abs(fd_v - Jom).max() < 1e-6 * scale
+        Minv = Ju
+        np.testing.assert_allclose(Minv, Minv.T, atol=1e-10 * np.abs(Minv).max())
+        assert np.all(np.linalg.eigvalsh(0.5 * (Minv + Minv.T)) > 0)
+
+
+def test_energy_is_conserved():
+    """Unforced motion under gravity: T + V from the independent link poses stays constant along the
+    oracle's RK4 trajectory (h = 1e-4, 0.2 s, large motion)."""
+    import oracle
+    m = _rbd()
+    rng = np.random.default_rng(2)
+    for _ in range(2):
+        x = np.concatenate([rng.uniform(-1.5, 1.5, 4), rng.uniform(-1.5, 1.5, 4)])
+        E0 = m.energy(x[:4], x[4:])
+        for _ in range(2000):
+            x = oracle.rk4(4, 1e-4, x, np.zeros(4))
+        assert abs(m.energy(x[:4], x[4:]) - E0) < 1e-7 * max(1.0, abs(E0)), (E0, m.energy(x[:4], x[4:]))
+
+
+def test_inverse_dynamics_helper():
+    """OCPUR5.get_inverse_dynamics (host numpy) = oracle RNEA bias: u = RNEA(q, qd, 0) gives acc = 0."""
+    import oracle
+    from vboc_amd.ur5 import OCPUR5
+    o = OCPUR5()
+    Q, V, _ = _states(6, 3)
+    for q, qd in zip(Q, V):
+        acc = oracle.model(4, q, qd, o.get_inverse_dynamics(q, qd))[0]
+        assert np.abs(acc).max() < 1e-9
+
+
+def test_class_surface():
+    from vboc_amd.ur5 import OCPUR5, SYMUR5INIT
+    o = OCPUR5()
+    assert (o.ocp.dims.nx, o.ocp.dims.nu, o.N, o.n_joints) == (8, 4, 100, 4)
+    np.testing.assert_array_equal(o.Cmax, [100., 80., 60., 1.])
+    np.testing.assert_array_equal(o.xmax, [3., 0., 3., 3., 3., 3., 3., 3.])
+    np.testing.assert_array_equal(o.xmin, -np.full(8, 3.))
+    assert o.ocp.solver_options.levenberg_marquardt == 1e-2
+    assert SYMUR5INIT().acados_integrator.T == 1e-2
+
+
+@pytest.fixture
+def oracle_dropin():
+    from vboc_amd import ocp
+    ocp.use_backend(OracleOcpBackend())
+    yield ocp
+    ocp.use_backend(None)
+
+
+def test_ocp_solve_is_the_batched_problem(oracle_dropin):
+    """OCPUR5INIT.OCP_solve (8-column arrays, as the reference calls it) = the 9-column batch of ics.ur5_ics."""
+    from vboc_amd.ics import ur5_ics
+    from vboc_amd.ur5 import OCPUR5INIT
+    b = ur5_ics(np.arange(3))
+    ref = _oracle_solve(4, b)
+    ocp = OCPUR5INIT()
+    N = ocp.N
+    for i in range(3):
+        a = lambda k: b[k][i, :8]
+        st = ocp.OCP_solve(b["x_guess"][i, :N, :8], b["u_guess"][i, :N], b["p"][i, :4], a("lbx"), a("ubx"),
+                           b["lbu"][i], b["ubu"][i], a("lbx0"), a("ubx0"), a("lbxe"), a("ubxe"))
+        assert st == ref["status"][i]
+        assert ocp.ocp_solver.get_cost() == ref["cost"][i]
+        np.testing.assert_array_equal(ocp.ocp_solver.get(0, "x"), ref["x"][i, 0, :8])
+
+
+def _fixture():
+    return json.load(open(os.path.join(HERE, "golden", "testing_ur5.json")))
+
+
+def test_ur5_driver_matches_reference_state_machine():
+    """The batched driver on the oracle returns the reference's `testing_test` results bit for bit."""
+    from vboc_amd.drivers import ur5_set, ur5_testing_batch
+    g = _fixture()
+    res, stats = ur5_testing_batch(np.array(g["ids"]), OracleBackend(4, g["fail_mod"]), N_start=g["N_start"])
+    assert stats["solves"] > len(g["ids"]) and stats["rk4"] == 0
+    assert sum(r is None for r in g["results"]) > 0
+    for pid, got, ref in zip(g["ids"], res, g["results"]):
+        assert (got is None) == (ref is None), pid
+        if ref is not None:
+            np.testing.assert_array_equal(np.asarray(got), np.asarray(ref), err_msg=f"problem {pid}")
+    assert ur5_set(res).shape == (sum(r is not None for r in g["results"]), 8)
+
+
+def test_first_solve_equals_ics():
+    from vboc_amd.drivers import ur5_problem
+    from vboc_amd.ics import UR5_DRAWS, UR5_STREAM, uniforms, ur5_ics
+    ids = np.arange(50, 58)
+    b = ur5_ics(ids)
+    U = uniforms(ids, UR5_DRAWS, stream=UR5_STREAM)
+    for k, pid in enumerate(ids):
+        r = next(ur5_problem(int(pid), U[k]))
+        np.testing.assert_array_equal(r.p, b["p"][k])
+        np.testing.assert_array_equal(r.q_init_lb, b["lbx0"][k])
+        np.testing.assert_array_equal(r.q_init_ub, b["ubx0"][k])
+        np.testing.assert_array_equal(r.x_guess, b["x_guess"][k, :100])
+        for f, kk in (("q_lb", "lbx"), ("q_ub", "ubx"), ("u_lb", "lbu"), ("u_ub", "ubu"), ("q_fin_lb", "lbxe"),
+                      ("q_fin_ub", "ubxe")):
+            np.testing.assert_array_equal(getattr(r, f), b[kk][k])
+
+
+# ---- GPU (lane-per-problem HIP kernels for nq = 4, RNEA sensitivities) ------------------------------------
+def _gpu_solve(b, **opts):
+    from vboc_amd import lib
+    s = lib.Solver(4, int(np.max(b["N"])), slots=max(256, len(b["N"])))
+    for k, v in opts.items():
+        s.set_option(k, v)
+    try:
+        return s.solve_host(b)
+    finally:
+        s.close()
+
+
+@pytest.mark.gpu
+def test_ur5_parity_with_oracle():
+    """Same bars as the pendulum chains (tests/test_gpu.py): status >= 98 %, SQP iterations >= 95 %, cost and
+    x_0 of problems converged on both: median <= 1e-9, max <= 2e-3."""
+    import oracle
+    from vboc_amd.ics import ur5_ics
+    b = ur5_ics(np.arange(64))
+    g = _gpu_solve(b, nlp_solver_max_iter=300)
+    xo, uo, r = oracle.solve_batch(4, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                                   b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"],
+                                   opts=oracle.default_opts(max_iter=300, lm=1e-2))
+    assert np.mean(g["status"] == r["status"]) >= 0.98, (g["status"], r["status"])
+    assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= 0.95, (g["sqp_iter"], r["sqp_iter"])
+    both = (g["status"] == 0) & (r["status"] == 0)
+    assert both.mean() >= 0.5
+    dc = np.abs(g["cost"] - r["cost"])[both]
+    dx = np.abs(g["x"][:, 0, :8] - xo[:, 0, :8]).max(axis=1)[both]
+    assert np.median(dc) <= 1e-9 and dc.max() <= 2e-3, (np.median(dc), dc.max())
+    assert np.median(dx) <= 1e-9 and dx.max() <= 2e-3, (np.median(dx), dx.max())
+    for i in np.where(both)[0][:8]:
+        np.testing.assert_array_equal(g["x"][i, :101, 8], 1e-2)
+
+
+@pytest.mark.gpu
+def test_ur5_twin_integrator_and_sensitivities():
+    """GPU RK4 step and its forward sensitivities (model.h: RNEA, dual-number JVPs) = the oracle's
+    (complex-step RNEA) to rounding; the wave solver is not offered for the arm and says so."""
+    import oracle
+    from vboc_amd import lib
+    Q, V, U = _states(256, 4)
+    X = np.concatenate([Q, V], axis=1)
+    x1 = lib.rk4_host(4, 1e-2, X, U)
+    ref = np.stack([oracle.rk4(4, 1e-2, X[i], U[i]) for i in range(len(X))])
+    np.testing.assert_allclose(x1, ref, rtol=1e-12, atol=1e-12)
+    x1, A, Bm = lib.rk4_sens_host(4, 1e-2, X[:64], U[:64])
+    for i in range(0, 64, 8):
+        r1, rA, rB = oracle.rk4_sens(4, 1e-2, X[i], U[i])
+        np.testing.assert_allclose(A[i], rA, rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(Bm[i], rB, rtol=1e-12, atol=1e-12)
+    s = lib.Solver(4, 100, slots=256)
+    assert s.get_option("wave_all") == 0.0
+    with pytest.raises(lib.VbocError, match="UR5"):
+        s.set_option("wave_all", 1)
+    s.close()
+
+
+@pytest.mark.gpu
+def test_ur5_dropin_class_on_gpu():
+    import oracle
+    from vboc_amd.ics import ur5_ics
+    from vboc_amd.ur5 import OCPUR5INIT
+    b = ur5_ics(np.arange(4))
+    xo, uo, r = oracle.solve_batch(4, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                                   b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"])
+    ocp = OCPUR5INIT()
+    N = ocp.N
+    for i in range(4):
+        a = lambda k: b[k][i, :8]
+        st = ocp.OCP_solve(b["x_guess"][i, :N, :8], b["u_guess"][i, :N], b["p"][i, :4], a("lbx"), a("ubx"),
+                           b["lbu"][i], b["ubu"][i], a("lbx0"), a("ubx0"), a("lbxe"), a("ubxe"))
+        assert st == r["status"][i]
+        if st == 0:
+            assert abs(ocp.ocp_solver.get_cost() - r["cost"][i]) < 2e-3
+            np.testing.assert_allclose(ocp.ocp_solver.get(0, "x"), xo[i, 0, :8], atol=2e-3)
+
+
+@pytest.mark.gpu
+def test_ur5_driver_on_gpu_matches_reference():
+    """The reference's `testing_test` fixture reproduced by the batched driver on the GPU (with the fixture's
+    failure injection): >= 90 % of the problems agree to 1e-5 (rounding-level differences may flip the
+    cost-decrease stop rule)."""
+    from vboc_amd.drivers import GpuBackend, ur5_testing_batch
+    from oracle_backend import forced_failure
+
+    class Failing:
+        def __init__(self, fail_mod):
+            self.gpu, self.fail_mod = GpuBackend(4), fail_mod
+            self.nmax = self.gpu.nmax
+
+        def solve(self, b):
+            r = self.gpu.solve(b)
+            st = np.array(r["status"], copy=True)
+            for i in range(st.shape[0]):
+                if forced_failure(b["lbx0"][i, 0], self.fail_mod):
+                    st[i] = 4
+            return dict(r, status=st)
+
+    g = _fixture()
+    n = 16   # the first 16 fixture problems (lane mode: a 1000-iteration problem costs ~2 min of rounds)
+    res, _ = ur5_testing_batch(np.array(g["ids"][:n]), Failing(g["fail_mod"]), N_start=g["N_start"])
+    same = 0
+    for got, ref in zip(res, g["results"][:n]):
+        if got is None or ref is None:
+            same += (got is None) == (ref is None)
+        elif np.abs(np.asarray(got) - np.asarray(ref)).max() < 1e-5:
+            same += 1
+    assert same >= 0.9 * n, (same, n)
+
+
+@pytest.mark.gpu
+def test_ur5_full_batch_properties():
+    """1024 first solves: converged solutions are dynamically feasible (re-simulated with the ORACLE's RK4 on
+    a sample, the GPU twin on all), inside the boxes, at rest at N, start along p, cost = p . qdot_0."""
+    import oracle
+    from vboc_amd import lib
+    from vboc_amd.ics import ur5_ics
+    from vboc_amd.ur5 import U_LIMITS, XMAX, XMIN
+    b = ur5_ics(np.arange(10**6, 10**6 + 1024))
+    g = _gpu_solve(b, nlp_solver_max_iter=60)
+    ok = g["status"] == 0
+    assert ok.mean() > 0.5
+    X, U = g["x"][ok, :, :8], g["u"][ok]
+    N = 100
+    x1 = lib.rk4_host(4, 1e-2, X[:, :N].reshape(-1, 8), U[:, :N].reshape(-1, 4)).reshape(-1, N, 8)
+    assert np.abs(x1 - X[:, 1:N + 1]).max() < 1e-6
+    for i in range(0, X.shape[0], max(1, X.shape[0] // 16)):
+        for k in (0, 37, 99):
+            np.testing.assert_allclose(oracle.rk4(4, 1e-2, X[i, k], U[i, k]), X[i, k + 1], atol=1e-6)
+    assert np.abs(X[:, N, 4:]).max() < 1e-6
+    assert np.all(np.abs(U) <= U_LIMITS + 1e-6)
+    assert np.all(X[:, 1:N] >= XMIN - 1e-6) and np.all(X[:, 1:N] <= XMAX + 1e-6)
+    d = b["p"][ok, :4]
+    v0 = X[:, 0, 4:]
+    assert np.abs(v0 - d * np.sum(d * v0, 1, keepdims=True)).max() < 1e-9
+    np.testing.assert_allclose(g["cost"][ok], np.sum(d * v0, 1), atol=1e-9)
+
+
+def test_ur5_run_on_oracle(tmp_path):
+    """The UR5 main block end to end on CPU (oracle solver, small sets, small minibatch): artefacts in the
+    reference's names and formats, loadable with weights_only=True."""
+    import torch
+    from vboc_amd.pipeline import ur5_run
+    r = ur5_run(OracleBackend(4), num_test=8, num_train=24, out_dir=str(tmp_path), device="cpu", minibatch=8,
+                hidden=32)
+    assert r["X_train"].shape[1] == 8 and r["X_train"].shape[0] >= 12
+    assert np.isfinite(r["rmse_train"]) and np.isfinite(r["rmse_test"])
+    sd = torch.load(tmp_path / "model_4dof_vboc", weights_only=True)
+    assert sd["linear_relu_stack.0.weight"].shape == (32, 8)
+    assert np.load(tmp_path / "data_4dof_vboc_test.npy").shape == r["X_test"].shape

@@ -10,10 +10,22 @@
 //    (VBOC/doublependulum_class_vboc.py:14-91, VBOC/triplependulum_class_vboc.py:15-58).
 //  * nq = 1: damped pendulum acc = (m g d sin th + F - b om) / (d^2 m), m=0.5, d=0.3, b=0.01
 //    (VBOC/pendulum_class_vboc.py:14-39).
+//  * nq = 4: the UR5 arm of VBOC/UR5/ur5reduced_class_fixedveldir.py:20-45 (4 revolute joints of
+//    VBOC/UR5/ur5.urdf between base_link and tool0; urdf2casadi's ABA in the reference).  Here
+//    M(q) acc = u - RNEA(q, qd, 0): a body-frame recursive Newton-Euler pass over the generated
+//    parameters of ur5_params.h (tools/gen_ur5_model.py), M from RNEA columns, and Jacobian-vector
+//    products by ONE forward-mode (dual-number) RNEA pass per direction:
+//      d acc = M^-1 (du - d RNEA(q, qd, acc)|acc fixed).
 // The dt state of the reference (f = dt * f_phys, RK4 with h = 1, tf = N) is folded into the
-// step length h = dt (exact: the dt state has zero derivative and is pinned by the bounds).
+// step length h = dt (exact: the dt state has zero derivative and is pinned by the bounds).  The UR5
+// OCP has no dt state (tf = 1 s over N = 100 intervals, set_new_time_steps(dt_sym = 1e-2)); its time
+// step travels in the same dt column of the C ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#define UR5_CONST static constexpr
+#include "ur5_params.h"
+
 
 #ifndef VBOC_SENS_GROUP
 #define VBOC_SENS_GROUP 1
@@ -76,11 +88,210 @@ __device__ __forceinline__ void chol_solve(const double (&L)[n * n], double (&b)
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// UR5 (nq = 4) rigid-body dynamics: generic over double and a forward-mode dual number
+// ---------------------------------------------------------------------------------------------
+struct Dl {
+  double v, d;
+};
+__device__ __forceinline__ Dl operator+(Dl a, Dl b) { return {a.v + b.v, a.d + b.d}; }
+__device__ __forceinline__ Dl operator-(Dl a, Dl b) { return {a.v - b.v, a.d - b.d}; }
+__device__ __forceinline__ Dl operator-(Dl a) { return {-a.v, -a.d}; }
+__device__ __forceinline__ Dl operator*(Dl a, Dl b) { return {a.v * b.v, a.v * b.d + a.d * b.v}; }
+__device__ __forceinline__ Dl operator*(double a, Dl b) { return {a * b.v, a * b.d}; }
+__device__ __forceinline__ Dl operator*(Dl a, double b) { return {a.v * b, a.d * b}; }
+__device__ __forceinline__ Dl operator+(Dl a, double b) { return {a.v + b, a.d}; }
+__device__ __forceinline__ void tsincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ void tsincos(Dl x, Dl* s, Dl* c) {
+  double sv, cv;
+  sincos(x.v, &sv, &cv);
+  *s = {sv, cv * x.d};
+  *c = {cv, -sv * x.d};
+}
+template <class T>
+__device__ __forceinline__ T tzero() { return T{}; }
+template <>
+__device__ __forceinline__ double tzero<double>() { return 0.0; }
+template <>
+__device__ __forceinline__ Dl tzero<Dl>() { return Dl{0.0, 0.0}; }
+
+template <class T, class U>
+__device__ __forceinline__ void cross3(const T* a, const U* b, T* o) {
+  const T t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  o[0] = t0; o[1] = t1; o[2] = t2;
+}
+template <class T>
+__device__ __forceinline__ void cross3c(const double* a, const T* b, T* o) {   // constant x T
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// tau = RNEA(q, qd, qdd) in body coordinates (VEL: velocity terms, GRAV: gravity (0, 0, -9.81)).
+// Joint i: child frame = joint frame (UR5_R, UR5_P in the parent body) rotated by Rz(q_i); motion
+// transform E = Rz(q)^T R^T, r = P:  X (w, v) = (E w, E (v - r x w));  X^T (n, f) = (E^T n + r x E^T f, E^T f).
+template <class T, bool VEL, bool GRAV>
+__device__ __forceinline__ void ur5_rnea(const T* q, const T* qd, const double* qdd, T* tau) {
+  T cs[4], sn[4], fn[4][3], ff[4][3];
+  T w[3], v[3], aw[3], av[3];
+  const T z = tzero<T>();
+#pragma unroll
+  for (int a = 0; a < 3; ++a) { w[a] = z; v[a] = z; aw[a] = z; av[a] = z; }
+  if constexpr (GRAV) av[2] = av[2] + 9.81;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    tsincos(q[i], &sn[i], &cs[i]);
+    T E[9];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      E[0 * 3 + k] = cs[i] * UR5_R[9 * i + k * 3 + 0] + sn[i] * UR5_R[9 * i + k * 3 + 1];
+      E[1 * 3 + k] = cs[i] * UR5_R[9 * i + k * 3 + 1] - sn[i] * UR5_R[9 * i + k * 3 + 0];
+      E[2 * 3 + k] = z + UR5_R[9 * i + k * 3 + 2];
+    }
+    const double r[3] = {UR5_P[3 * i], UR5_P[3 * i + 1], UR5_P[3 * i + 2]};
+    T t[3], t2[3], nw[3], nv[3], naw[3], nav[3];
+    if constexpr (VEL) {
+      cross3c(r, w, t);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) t[a] = v[a] - t[a];
+    }
+    cross3c(r, aw, t2);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) t2[a] = av[a] - t2[a];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if constexpr (VEL) {
+        nw[a] = E[a * 3] * w[0] + E[a * 3 + 1] * w[1] + E[a * 3 + 2] * w[2];
+        nv[a] = E[a * 3] * t[0] + E[a * 3 + 1] * t[1] + E[a * 3 + 2] * t[2];
+      }
+      naw[a] = E[a * 3] * aw[0] + E[a * 3 + 1] * aw[1] + E[a * 3 + 2] * aw[2];
+      nav[a] = E[a * 3] * t2[0] + E[a * 3 + 1] * t2[1] + E[a * 3 + 2] * t2[2];
+    }
+    if constexpr (VEL) {
+      // v_i = X v_p + z qd_i ; a_i = X a_p + z qdd_i + v_i x_m (z qd_i)
+      nw[2] = nw[2] + qd[i];
+      // (w x z qd, v x z qd) with z = e_3
+      naw[0] = naw[0] + nw[1] * qd[i];
+      naw[1] = naw[1] - nw[0] * qd[i];
+      nav[0] = nav[0] + nv[1] * qd[i];
+      nav[1] = nav[1] - nv[0] * qd[i];
+    }
+    naw[2] = naw[2] + qdd[i];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      if constexpr (VEL) { w[a] = nw[a]; v[a] = nv[a]; }
+      aw[a] = naw[a]; av[a] = nav[a];
+    }
+    // f_i = I a_i + v_i x_f (I v_i);  I (w, v) = (Io w + mc x v, m v - mc x w)
+    const double m = UR5_M[i];
+    const double mc[3] = {UR5_MC[3 * i], UR5_MC[3 * i + 1], UR5_MC[3 * i + 2]};
+    T x1[3], x2[3];
+    cross3c(mc, av, x1);
+    cross3c(mc, aw, x2);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      fn[i][a] = UR5_IO[9 * i + a * 3] * aw[0] + UR5_IO[9 * i + a * 3 + 1] * aw[1] + UR5_IO[9 * i + a * 3 + 2] * aw[2] +
+                 x1[a];
+      ff[i][a] = m * av[a] - x2[a];
+    }
+    if constexpr (VEL) {
+      T hA[3], hL[3], y1[3], y2[3], y3[3];
+      cross3c(mc, v, x1);
+      cross3c(mc, w, x2);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        hA[a] = UR5_IO[9 * i + a * 3] * w[0] + UR5_IO[9 * i + a * 3 + 1] * w[1] + UR5_IO[9 * i + a * 3 + 2] * w[2] + x1[a];
+        hL[a] = m * v[a] - x2[a];
+      }
+      cross3(w, hA, y1);
+      cross3(v, hL, y2);
+      cross3(w, hL, y3);
+#pragma unroll
+      for (int a = 0; a < 3; ++a) { fn[i][a] = fn[i][a] + y1[a] + y2[a]; ff[i][a] = ff[i][a] + y3[a]; }
+    }
+  }
+#pragma unroll
+  for (int i = 3; i >= 0; --i) {
+    tau[i] = fn[i][2];
+    if (i == 0) break;
+    T E[9];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      E[0 * 3 + k] = cs[i] * UR5_R[9 * i + k * 3 + 0] + sn[i] * UR5_R[9 * i + k * 3 + 1];
+      E[1 * 3 + k] = cs[i] * UR5_R[9 * i + k * 3 + 1] - sn[i] * UR5_R[9 * i + k * 3 + 0];
+      E[2 * 3 + k] = z + UR5_R[9 * i + k * 3 + 2];
+    }
+    const double r[3] = {UR5_P[3 * i], UR5_P[3 * i + 1], UR5_P[3 * i + 2]};
+    T en[3], ef[3], x[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      en[a] = E[a] * fn[i][0] + E[3 + a] * fn[i][1] + E[6 + a] * fn[i][2];
+      ef[a] = E[a] * ff[i][0] + E[3 + a] * ff[i][1] + E[6 + a] * ff[i][2];
+    }
+    cross3c(r, ef, x);
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { fn[i - 1][a] = fn[i - 1][a] + en[a] + x[a]; ff[i - 1][a] = ff[i - 1][a] + ef[a]; }
+  }
+}
+
+// Cholesky factor of M(q) (columns M e_c = RNEA(q, 0, e_c) without gravity) and acc = M^-1 (u - RNEA(q, qd, 0))
+__device__ __forceinline__ void ur5_point(const double* q, const double* qd, const double* u, double (&L)[16],
+                                          double (&acc)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    double e[4] = {0.0, 0.0, 0.0, 0.0}, col[4];
+    e[c] = 1.0;
+    ur5_rnea<double, false, false>(q, q, e, col);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L[j * 4 + c] = col[j];
+  }
+  const double zq[4] = {0.0, 0.0, 0.0, 0.0};
+  double b[4];
+  ur5_rnea<double, true, true>(q, qd, zq, b);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = u[j] - b[j];
+  chol<4>(L);
+  chol_solve<4>(L, acc);
+}
+
+// d acc along (dq, dqd, du) at a point with factor L and accelerations acc
+__device__ __forceinline__ void ur5_jvp(const double* q, const double* qd, const double (&L)[16], const double* acc,
+                                        const double* dq, const double* dqd, const double* du, double* dacc) {
+  Dl Q[4], V[4], tau[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { Q[j] = Dl{q[j], dq[j]}; V[j] = Dl{qd[j], dqd[j]}; }
+  ur5_rnea<Dl, true, true>(Q, V, acc, tau);
+  double r[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) r[j] = du[j] - tau[j].d;
+  chol_solve<4>(L, r);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) dacc[j] = r[j];
+}
+
 // acc = f(th, om, u); if JAC also Jth, Jom, Ju (row-major NQ x NQ).
 template <int NQ, bool JAC>
 __device__ __forceinline__ void model_eval(const double* th, const double* om, const double* u, double* acc,
                                            double* Jth, double* Jom, double* Ju) {
-  if constexpr (NQ == 1) {
+  if constexpr (NQ == 4) {
+    double L[16], a[4];
+    ur5_point(th, om, u, L, a);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = a[j];
+    if constexpr (JAC) {
+#pragma unroll
+      for (int c = 0; c < 12; ++c) {
+        double dq[4], dv[4], du[4], da[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { dq[j] = (c == j) ? 1.0 : 0.0; dv[j] = (c == 4 + j) ? 1.0 : 0.0; du[j] = (c == 8 + j) ? 1.0 : 0.0; }
+        ur5_jvp(th, om, L, a, dq, dv, du, da);
+        double* J = c < 4 ? Jth : (c < 8 ? Jom : Ju);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) J[j * 4 + (c & 3)] = da[j];
+      }
+    }
+  } else if constexpr (NQ == 1) {
     constexpr double pm = 0.5, pd = 0.3, pb = 0.01, g = 9.81;
     constexpr double inv = 1.0 / (pd * pd * pm);
     double sn, cs;
@@ -194,11 +405,16 @@ struct ModelPoint {
   double cd[NQ][NQ];       // cos(th_j - th_k)
   double cth[NQ];          // cos th_j
   double acc[NQ], om[NQ];
+  double th[NQ];           // angles (UR5: the JVP re-runs RNEA at the point)
 };
 
 template <int NQ>
 __device__ __forceinline__ void model_point(const double* th, const double* om, const double* u, ModelPoint<NQ>& mp) {
-  if constexpr (NQ == 1) {
+  if constexpr (NQ == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { mp.th[j] = th[j]; mp.om[j] = om[j]; }
+    ur5_point(th, om, u, mp.L, mp.acc);
+  } else if constexpr (NQ == 1) {
     constexpr double pm = 0.5, pd = 0.3, pb = 0.01, g = 9.81;
     constexpr double inv = 1.0 / (pd * pd * pm);
     double sn, cs;
@@ -246,7 +462,9 @@ __device__ __forceinline__ void model_point(const double* th, const double* om, 
 template <int NQ>
 __device__ __forceinline__ void model_jvp(const ModelPoint<NQ>& mp, const double* dth, const double* dom,
                                           const double* du, double* dacc) {
-  if constexpr (NQ == 1) {
+  if constexpr (NQ == 4) {
+    ur5_jvp(mp.th, mp.om, mp.L, mp.acc, dth, dom, du, dacc);
+  } else if constexpr (NQ == 1) {
     constexpr double pm = 0.5, pd = 0.3, pb = 0.01, g = 9.81;
     constexpr double inv = 1.0 / (pd * pd * pm);
     dacc[0] = (pm * g * pd * mp.cth[0] * dth[0] + du[0] - pb * dom[0]) * inv;

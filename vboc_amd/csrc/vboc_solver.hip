@@ -189,7 +189,7 @@ struct Lane {
   // Reads problem `pid` into this slot.  Returns false (nothing loaded) if its structure is
   // outside what the boundary-OCP solver implements: dt not pinned by the bounds, stage-0
   // positions not fixed, terminal velocities not fixed, horizon out of range.
-  __device__ bool supported(const Inputs& in, int pid) const {
+  __device__ __forceinline__ bool supported(const Inputs& in, int pid) const {
     constexpr int NXR = NX + 1;
     const int n = in.N[pid];
     if (n < 1 || n > in.nmax) return false;
@@ -1263,6 +1263,24 @@ __global__ __launch_bounds__(256) void rk4_kernel(int B, double T, const double*
   UNR for (int i = 0; i < NX; ++i) xo[(long long)b * NX + i] = x1[i];
 }
 
+// one ERK4 step with forward sensitivities per thread (the linearisation of the solvers, standalone)
+template <int NQ>
+__global__ __launch_bounds__(256) void rk4_sens_kernel(int B, double T, const double* __restrict__ x,
+                                                       const double* __restrict__ u, double* __restrict__ xo,
+                                                       double* __restrict__ A, double* __restrict__ Bm) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  constexpr int NX = 2 * NQ;
+  double xi[NX], ui[NQ], x1[NX];
+  UNR for (int i = 0; i < NX; ++i) xi[i] = x[(long long)b * NX + i];
+  UNR for (int a = 0; a < NQ; ++a) ui[a] = u[(long long)b * NQ + a];
+  rk4_sens<NQ>(T, xi, ui, x1, [&](int i, int c, double v) {
+    if (c < NX) A[(long long)b * NX * NX + i * NX + c] = v;
+    else Bm[(long long)b * NX * NQ + i * NQ + (c - NX)] = v;
+  });
+  UNR for (int i = 0; i < NX; ++i) xo[(long long)b * NX + i] = x1[i];
+}
+
 }  // namespace vboc
 
 #include "coop.h"
@@ -1331,7 +1349,7 @@ static void default_opts(Opts& o) {
 }
 
 static int par_count(int nq) {
-  return nq == 1 ? Par<1>::COUNT : (nq == 2 ? Par<2>::COUNT : Par<3>::COUNT);
+  return nq == 1 ? Par<1>::COUNT : (nq == 2 ? Par<2>::COUNT : (nq == 3 ? Par<3>::COUNT : Par<4>::COUNT));
 }
 
 static inline size_t ev(size_t f) { return (f + 1) & ~(size_t)1; }  // fields rounded up to pairs
@@ -1447,7 +1465,8 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
   switch (h->nq) {
     case 1: hipLaunchKernelGGL(k_wave<1>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
     case 2: hipLaunchKernelGGL(k_wave<2>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
-    default: hipLaunchKernelGGL(k_wave<3>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
+    case 3: hipLaunchKernelGGL(k_wave<3>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
+    default: return hipErrorInvalidValue;   // the UR5 arm runs in lane mode (vboc_create)
   }
   return hipGetLastError();
 }
@@ -1459,12 +1478,13 @@ const char* vboc_last_error(void) { return g_err.c_str(); }
 int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   if (!out) return fail(VBOC_ERR_ARG, "vboc_create: out is NULL");
   *out = nullptr;
-  if (nq < 1 || nq > 3) return fail(VBOC_ERR_ARG, "vboc_create: nq must be 1, 2 or 3");
+  if (nq < 1 || nq > 4) return fail(VBOC_ERR_ARG, "vboc_create: nq must be 1, 2, 3 (pendulum chains) or 4 (UR5)");
   if (nmax < 1) return fail(VBOC_ERR_ARG, "vboc_create: nmax must be >= 1");
   HIPCHK(hipSetDevice(device));
   vboc_solver* h = new vboc_solver();
   h->nq = nq; h->nmax = nmax; h->device = device;
   default_opts(h->o);
+  if (nq == 4) h->o.lm = 1e-2;   // UR5 OCP: levenberg_marquardt = 1e-2 (VBOC/UR5/ur5reduced_class_fixedveldir.py:135)
   if (slots <= 0) slots = 64 * 1024;
   if (slots > (1 << 30)) return fail(VBOC_ERR_ARG, "vboc_create: too many slots");
   slots = ((slots + 255) / 256) * 256;
@@ -1486,8 +1506,14 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   }
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);
-  // wave solver: one region of stage records per resident workgroup (occupancy x CUs)
-  {
+  // wave solver: one region of stage records per resident workgroup (occupancy x CUs).  The UR5 arm
+  // (nq = 4) is solved by the lane-per-problem kernels only: the wave solver's one-output-per-lane
+  // recursion steps and LDS ring slots are laid out for the pendulum chains.
+  if (nq == 4) {
+    h->wave_all = false;
+    h->coop_threshold = 0;
+    h->coop_ok = false;
+  } else {
     const void* fn = nq == 1 ? (const void*)k_wave<1> : (nq == 2 ? (const void*)k_wave<2> : (const void*)k_wave<3>);
     h->wave_lds = nq == 1 ? WaveLayout<1>::lds_bytes(nmax)
                           : (nq == 2 ? WaveLayout<2>::lds_bytes(nmax) : WaveLayout<3>::lds_bytes(nmax));
@@ -1572,7 +1598,11 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "ipm_push") o.push = v;
   else if (s == "ipm_tau") o.tau = v;
   else if (s == "coop_threshold") h->coop_threshold = v;
-  else if (s == "wave_all") h->wave_all = v != 0.0;
+  else if (s == "wave_all") {
+    if (h->nq == 4 && v != 0.0)
+      return fail(VBOC_ERR_UNSUPPORTED, "vboc_set_option: the UR5 arm (nq = 4) is solved in lane mode only");
+    h->wave_all = v != 0.0;
+  }
   else if (s == "wave_groups") h->group_cap = (long long)v;
   else if (s == "mall_mib") h->mall_mib = v;
   else if (s == "profile_kernels") {
@@ -1675,7 +1705,8 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
       switch (h->nq) {
         case 1: le = launch_round<1>(h, grid, block, st, w, h->o, in, ss); break;
         case 2: le = launch_round<2>(h, grid, block, st, w, h->o, in, ss); break;
-        default: le = launch_round<3>(h, grid, block, st, w, h->o, in, ss); break;
+        case 3: le = launch_round<3>(h, grid, block, st, w, h->o, in, ss); break;
+        default: le = launch_round<4>(h, grid, block, st, w, h->o, in, ss); break;
       }
       if (le != hipSuccess) return fail(VBOC_ERR_HIP, std::string("vboc_solve_batch: ") + hipGetErrorString(le));
     }
@@ -1781,7 +1812,8 @@ int vboc_solve_batch_ft(vboc_handle h, const vboc_batch_t* b, void* stream) {
   switch (h->nq) {
     case 1: rc = launch_ft<1>(h, in, st); break;
     case 2: rc = launch_ft<2>(h, in, st); break;
-    default: rc = launch_ft<3>(h, in, st); break;
+    case 3: rc = launch_ft<3>(h, in, st); break;
+    default: return fail(VBOC_ERR_UNSUPPORTED, "vboc_solve_batch_ft: the free-time OCP is defined for the pendulum chains only");
   }
   if (rc == -1) return fail(VBOC_ERR_NOMEM, "vboc_solve_batch_ft: hipMalloc of the stage regions");
   if (rc) return fail(VBOC_ERR_HIP, std::string("vboc_solve_batch_ft: ") + hipGetErrorString(hipGetLastError()));
@@ -1850,7 +1882,7 @@ int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) { return solve_h
 int vboc_solve_batch_ft_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, true); }
 
 int vboc_rk4_batch(int nq, int B, double T, const double* x, const double* u, double* x_out, void* stream) {
-  if (nq < 1 || nq > 3 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_batch: bad nq/B");
+  if (nq < 1 || nq > 4 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_batch: bad nq/B");
   if (B == 0) return VBOC_OK;
   if (!x || !u || !x_out) return fail(VBOC_ERR_ARG, "vboc_rk4_batch: NULL array");
   hipStream_t st = (hipStream_t)stream;
@@ -1858,14 +1890,43 @@ int vboc_rk4_batch(int nq, int B, double T, const double* x, const double* u, do
   switch (nq) {
     case 1: hipLaunchKernelGGL(rk4_kernel<1>, grid, block, 0, st, B, T, x, u, x_out); break;
     case 2: hipLaunchKernelGGL(rk4_kernel<2>, grid, block, 0, st, B, T, x, u, x_out); break;
-    default: hipLaunchKernelGGL(rk4_kernel<3>, grid, block, 0, st, B, T, x, u, x_out); break;
+    case 3: hipLaunchKernelGGL(rk4_kernel<3>, grid, block, 0, st, B, T, x, u, x_out); break;
+    default: hipLaunchKernelGGL(rk4_kernel<4>, grid, block, 0, st, B, T, x, u, x_out); break;
   }
   HIPCHK(hipGetLastError());
   return VBOC_OK;
 }
 
+int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const double* u, double* x_out, double* A,
+                             double* Bm) {
+  if (nq < 1 || nq > 4 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_sens_batch_host: bad nq/B");
+  if (B == 0) return VBOC_OK;
+  const size_t nx = 2 * nq;
+  double *dx, *du, *dxo, *dA, *dB;
+  HIPCHK(hipMalloc(&dx, B * nx * sizeof(double)));
+  HIPCHK(hipMalloc(&du, B * nq * sizeof(double)));
+  HIPCHK(hipMalloc(&dxo, B * nx * sizeof(double)));
+  HIPCHK(hipMalloc(&dA, B * nx * nx * sizeof(double)));
+  HIPCHK(hipMalloc(&dB, B * nx * nq * sizeof(double)));
+  HIPCHK(hipMemcpy(dx, x, B * nx * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(du, u, B * nq * sizeof(double), hipMemcpyHostToDevice));
+  const dim3 grid((B + 255) / 256), block(256);
+  switch (nq) {
+    case 1: hipLaunchKernelGGL(rk4_sens_kernel<1>, grid, block, 0, nullptr, B, T, dx, du, dxo, dA, dB); break;
+    case 2: hipLaunchKernelGGL(rk4_sens_kernel<2>, grid, block, 0, nullptr, B, T, dx, du, dxo, dA, dB); break;
+    case 3: hipLaunchKernelGGL(rk4_sens_kernel<3>, grid, block, 0, nullptr, B, T, dx, du, dxo, dA, dB); break;
+    default: hipLaunchKernelGGL(rk4_sens_kernel<4>, grid, block, 0, nullptr, B, T, dx, du, dxo, dA, dB); break;
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpy(x_out, dxo, B * nx * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(A, dA, B * nx * nx * sizeof(double), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(Bm, dB, B * nx * nq * sizeof(double), hipMemcpyDeviceToHost));
+  (void)hipFree(dx); (void)hipFree(du); (void)hipFree(dxo); (void)hipFree(dA); (void)hipFree(dB);
+  return VBOC_OK;
+}
+
 int vboc_rk4_batch_host(int nq, int B, double T, const double* x, const double* u, double* x_out) {
-  if (nq < 1 || nq > 3 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_batch_host: bad nq/B");
+  if (nq < 1 || nq > 4 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_batch_host: bad nq/B");
   if (B == 0) return VBOC_OK;
   const size_t nx = 2 * nq;
   double *dx = nullptr, *du = nullptr, *dxo = nullptr;

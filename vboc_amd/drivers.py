@@ -553,6 +553,71 @@ def testing_batch(nq, ids, backend, N_start=None, seed=SEED, max_restarts=MAX_TE
 
 
 # ------------------------------------------------------------------------------------------------
+# UR5 arm (BASELINE config 5): the main block of VBOC/UR5/vboc_multiprocessing_ur5.py fans
+# `testing_test` (:369-466) out over Pool(30) for the 10k test set (:487-498) and the 1M training set
+# (:506-528).  Each call extends the horizon while the cost still drops by more than tol and returns
+# [x_0]; a failed solve returns None (no restarts).
+# ------------------------------------------------------------------------------------------------
+def ur5_problem(pid, U, N_start=100):
+    """Generator for one `testing_test` problem; U: the problem's uniform block (ics.UR5_STREAM), drawn
+    in the reference's order (random() before choice() in `random.random() * random.choice([-1, 1])`).
+    Requests use the 9-column C-ABI layout (time step pinned in the dt column, p padded with 0)."""
+    from .ics import UR5_DRAWS
+    from .ur5 import DT, NQ, U_LIMITS, XMAX, XMIN
+    tol = 1e-3                                   # nlp_solver_tol_stat (:483)
+    draw = iter(float(v) for v in U[:UR5_DRAWS])
+    pick = lambda seq: seq[min(int(next(draw) * len(seq)), len(seq) - 1)]
+    p = np.empty(NQ)
+    for j in range(NQ):
+        r = next(draw)
+        p[j] = r * pick([-1, 1])
+    p = p / norm(p)
+    q0 = np.empty(NQ)
+    for j in range(NQ):
+        q0[j] = XMIN[j] + next(draw) * (XMAX[j] - XMIN[j])
+    col = lambda a: np.r_[a, DT]
+    q_lb, q_ub = col(XMIN), col(XMAX)
+    u_lb, u_ub = -U_LIMITS, U_LIMITS.copy()
+    q_init_lb, q_init_ub = col(np.r_[q0, XMIN[NQ:]]), col(np.r_[q0, XMAX[NQ:]])
+    q_fin_lb, q_fin_ub = col(np.r_[XMIN[:NQ], np.zeros(NQ)]), col(np.r_[XMAX[:NQ], np.zeros(NQ)])
+    pp = np.r_[p, 0.0]
+    N = N_start
+    xg = np.tile(col(np.r_[q0, np.zeros(NQ)]), (N, 1))
+    ug = np.zeros((N, NQ))
+    cost_old = 1e6
+    while True:
+        res = yield Solve(N, xg, ug, pp, q_lb, q_ub, u_lb, u_ub, q_init_lb, q_init_ub, q_fin_lb, q_fin_ub)
+        if res.status != 0:
+            return None
+        if res.cost > cost_old - tol:
+            return [res.x[0][:2 * NQ].copy()]
+        cost_old = res.cost
+        xg = np.empty((N + 1, 2 * NQ + 1))
+        ug = np.empty((N + 1, NQ))
+        xg[:N] = res.x[:N]
+        ug[:N] = res.u[:N]
+        xg[N] = res.x[N]
+        ug[N] = 0.0
+        N = N + 1
+
+
+def ur5_testing_batch(ids, backend, N_start=100, seed=SEED):
+    """`testing_test(v)` for every problem id in `ids`, batched.  Returns (results, stats): results[i] is
+    [x_0] (8 floats) or None, as the reference's call returns."""
+    from .ics import UR5_DRAWS, UR5_STREAM
+    ids = np.asarray(ids)
+    U = uniforms(ids, UR5_DRAWS, seed, stream=UR5_STREAM)
+    gens = [ur5_problem(int(pid), U[b], N_start) for b, pid in enumerate(ids)]
+    return run_problems(4, gens, backend, nmax=getattr(backend, "nmax", 200))
+
+
+def ur5_set(results):
+    """X = np.array([i for f in X_temp for i in f]) over the non-None results (:493-495)."""
+    rows = [row for t in results if t is not None for row in t]
+    return np.array(rows, dtype=np.float64).reshape(len(rows), 8)
+
+
+# ------------------------------------------------------------------------------------------------
 # pendulum VBOC data generation (free-time OCPs)
 # ------------------------------------------------------------------------------------------------
 PEND_N_START, PEND_EPS = 50, 1e-3   # VBOC/pendulum_vboc.py:21, :47

@@ -181,6 +181,36 @@ def _bounds(sysd, B, N, xg, ug, p, lbx0, ubx0, extra=None):
     return b
 
 
+UR5_DRAWS = 12   # testing_test: (random, choice) per joint for p, one random per joint for q_init
+UR5_STREAM = 5
+
+
+def ur5_ics(ids, N=100, seed=SEED):
+    """First OCP of the UR5's `testing_test` (VBOC/UR5/vboc_multiprocessing_ur5.py:369-426), what its main
+    block fans out for the test and training sets (:487-511): p[l] = random() * choice([-1, 1]),
+    normalised; q_init ~ U(x_min, x_max) per joint (x_max[1] = 0); constant guess [q_init, 0]; u = 0.
+    9-column C-ABI layout (the UR5 time step 1e-2 pinned in the dt column, p padded with 0)."""
+    from .ur5 import DT, NQ, U_LIMITS, XMAX, XMIN
+    ids = np.asarray(ids)
+    B = ids.shape[0]
+    U = uniforms(ids, UR5_DRAWS, seed, stream=UR5_STREAM)
+    r = np.stack([U[:, 2 * j] * _choice(U[:, 2 * j + 1], [-1.0, 1.0]) for j in range(NQ)], axis=1)
+    p = np.zeros((B, NQ + 1))
+    p[:, :NQ] = r / _row_norms(r)
+    qi = XMIN[:NQ] + U[:, 2 * NQ:3 * NQ] * (XMAX[:NQ] - XMIN[:NQ])
+    col = lambda a: np.concatenate([a, np.full(a.shape[:-1] + (1,), DT)], axis=-1)
+    xg = np.zeros((B, N + 1, 2 * NQ + 1))
+    xg[:, :, :NQ] = qi[:, None, :]
+    xg[:, :, 2 * NQ] = DT
+    return Batch(N=np.full(B, N, dtype=np.int32), x_guess=xg, u_guess=np.zeros((B, N, NQ)), p=p,
+                 lbx=np.tile(col(XMIN), (B, 1)), ubx=np.tile(col(XMAX), (B, 1)),
+                 lbu=np.tile(-U_LIMITS, (B, 1)), ubu=np.tile(U_LIMITS, (B, 1)),
+                 lbx0=col(np.concatenate([qi, np.tile(XMIN[NQ:], (B, 1))], axis=1)),
+                 ubx0=col(np.concatenate([qi, np.tile(XMAX[NQ:], (B, 1))], axis=1)),
+                 lbxe=np.tile(col(np.r_[XMIN[:NQ], np.zeros(NQ)]), (B, 1)),
+                 ubxe=np.tile(col(np.r_[XMAX[:NQ], np.zeros(NQ)]), (B, 1)))
+
+
 def pendulum_free_time_ics(ids, N_range=(20, 60), seed=SEED):
     """Free-time pendulum OCPs shaped like VBOC/pendulum_vboc.py's solves (OCPpendulum.OCP_solve,
     VBOC/pendulum_class_vboc.py:107-130): sweep direction v_sel = +-v_max (:55-77), a fixed initial

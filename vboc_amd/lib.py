@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("VBOC_LIB") or os.path.join(HERE, "libvboc_amd.so")
 SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
-           "vboc_solve_batch_host", "vboc_solve_batch_ft", "vboc_solve_batch_ft_host", "vboc_rk4_batch", "vboc_rk4_batch_host", "vboc_last_kernel_ms",
+           "vboc_solve_batch_host", "vboc_solve_batch_ft", "vboc_solve_batch_ft_host", "vboc_rk4_batch", "vboc_rk4_batch_host",
+           "vboc_rk4_sens_batch_host", "vboc_last_kernel_ms",
            "vboc_kernel_stats", "vboc_debug_counters", "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
@@ -74,6 +75,7 @@ def load():
                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.vboc_rk4_batch_host.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p]
+    lib.vboc_rk4_sens_batch_host.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double] + [ctypes.c_void_p] * 5
     lib.vboc_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int)]
     lib.vboc_debug_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
@@ -205,6 +207,18 @@ def rk4_host(nq, T, x, u):
     xo = np.zeros_like(x)
     _check(lib.vboc_rk4_batch_host(int(nq), B, float(T), x.ctypes.data, u.ctypes.data, xo.ctypes.data))
     return xo
+
+
+def rk4_sens_host(nq, T, x, u):
+    """One ERK4 step with forward sensitivities per state (the solvers' linearisation): (x1, A, B)."""
+    lib = load()
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    u = np.ascontiguousarray(u, dtype=np.float64)
+    B, nx = x.shape
+    xo, A, Bm = np.zeros_like(x), np.zeros((B, nx, nx)), np.zeros((B, nx, nq))
+    _check(lib.vboc_rk4_sens_batch_host(int(nq), B, float(T), x.ctypes.data, u.ctypes.data, xo.ctypes.data,
+                                        A.ctypes.data, Bm.ctypes.data))
+    return xo, A, Bm
 
 
 def rk4_device(nq, T, x, u, stream=None):

@@ -178,3 +178,49 @@ def pendulum_vboc_run(out_dir=None, device="cuda", seed=0, backend=None, it_max=
         torch.save(mean, os.path.join(out_dir, "mean_1dof_vboc_10"))
         torch.save(std, os.path.join(out_dir, "std_1dof_vboc_10"))
     return dict(X=X, rmse=rmse, fit=fit, stats=stats, mean=mean, std=std)
+
+
+def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device="cuda", seed=0,
+            minibatch=1 << 15, hidden=1000, log=None):
+    """VBOC/UR5/vboc_multiprocessing_ur5.py's main block (config 5) on one GPU:
+      test set      `testing_test` over ids [0, num_test) (:487-498)      -> data_4dof_vboc_test.npy
+      training set  `testing_test` over ids [num_test, + num_train) (:506-528) -> data_4dof_vboc_train.npy
+      features      [(q - mean) / std, qdot / |qdot|, |qdot|] with the position mean / std of the training set
+                    (the reference's commented-out computation, :546-548; it loads them from files)
+      fit           NeuralNetDIR(8, 1000, 1), Adam lr 1e-3, minibatch 2^15, EMA beta 0.95, stop at val <= 1e-3
+                    or it_max = 20 * int(n * 100 / 2^15) steps (:530-595), on the HIP-graph trainer
+      RMSE          on the training and the test data (:597-625); artefacts model_/mean_/std_4dof_vboc.
+    Difference: the reference appends the new rows to a training set loaded from a previous run (X_old,
+    :501, :530); here the run starts from an empty one.  Returns dict(X_test, X_train, fit, rmse_train,
+    rmse_test, stats)."""
+    import torch
+    from .drivers import GpuBackend, ur5_set, ur5_testing_batch
+    log = log or (lambda *a: None)
+    backend = backend or GpuBackend(4, nmax=200)
+    t0 = time.time()
+    res, st_test = ur5_testing_batch(np.arange(num_test), backend)
+    X_test = ur5_set(res)
+    log(f"test set: {X_test.shape[0]} rows of {num_test} in {time.time() - t0:.1f} s")
+    t1 = time.time()
+    res, st_train = ur5_testing_batch(np.arange(num_test, num_test + num_train), backend)
+    X_train = ur5_set(res)
+    log(f"training set: {X_train.shape[0]} rows of {num_train} in {time.time() - t1:.1f} s")
+    mean, std = position_stats(X_train, 4)
+    F = dir_features(X_train, mean, std, 4)
+    F_test = dir_features(X_test, mean, std, 4)
+    k = min(minibatch, F.shape[0])
+    tr = DirTrainer(4, device=device, hidden=hidden, minibatch=k, beta=0.95, stop_val=1e-3, seed=seed)
+    B = int(F.shape[0] * 100 / k)
+    fit = tr.fit(F, it_max=max(1, B * 20))
+    rmse_train, rmse_test = tr.rmse(F), tr.rmse(F_test)
+    log(f"fit {fit}  RMSE train {rmse_train:.4g} test {rmse_test:.4g}")
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        np.save(os.path.join(out_dir, "data_4dof_vboc_test.npy"), X_test)
+        np.save(os.path.join(out_dir, "data_4dof_vboc_train.npy"), X_train)
+        torch.save({kk: v.detach().cpu() for kk, v in tr.model.state_dict().items()},
+                   os.path.join(out_dir, "model_4dof_vboc"))
+        torch.save(mean, os.path.join(out_dir, "mean_4dof_vboc"))
+        torch.save(std, os.path.join(out_dir, "std_4dof_vboc"))
+    return dict(X_test=X_test, X_train=X_train, fit=fit, rmse_train=rmse_train, rmse_test=rmse_test,
+                stats=(st_test, st_train), mean=mean, std=std)
