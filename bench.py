@@ -133,11 +133,8 @@ def main():
 
     from vboc_amd import lib
     nq, B = args.nq, args.batch
-    if nq == 4:
-        args.mode = "lane"   # the UR5 arm is solved by the lane-per-problem kernels
     solver = lib.Solver(nq, 100, slots=args.slots, device=local)
-    if nq != 4:
-        solver.set_option("wave_all", 1 if args.mode == "wave" else 0)
+    solver.set_option("wave_all", 1 if args.mode == "wave" else 0)
     solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
     stream = torch.cuda.current_stream(device)
 
@@ -222,7 +219,7 @@ def main():
                     "kernel": f"k_qp_factor<{nq}>", "avg_launch_ms": round(avg_launch_ms, 4),
                     "launches": fact_launch}
     else:
-        traffic_gb, traffic_src = pmc_traffic("k_wave")
+        traffic_gb, traffic_src = pmc_traffic("k_wave" if nq != 4 else "k_wave_ur5")
         avg_ms = wave_ms / max(1, wave_launch)
         per_launch = local_flops / max(1, args.steps)
         wave_tf = per_launch / (avg_ms * 1e-3) / 1e12 if wave_ms else None
@@ -232,7 +229,7 @@ def main():
                     "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
                     "traffic_source": traffic_src,
                     "algorithmic": "FP64 flops per launch, SURVEY.md 8(d): N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp)",
-                    "flops_per_launch": round(per_launch), "kernel": f"k_wave<{nq}>",
+                    "flops_per_launch": round(per_launch), "kernel": f"k_wave<{nq}>" if nq != 4 else "k_wave_ur5",
                     "avg_launch_ms": round(avg_ms, 3), "launches": wave_launch}
     if rank == 0:
         line = {

@@ -1239,6 +1239,7 @@ __global__ __launch_bounds__(256) VBOC_WPE void k_ls(Work w, Opts o, Inputs in, 
   else ss(IS_PH, L.slot) = 1;
 }
 
+#ifndef VBOC_ARM_TU
 __global__ void k_slots_init(int* ist, long long S) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= S) return;
@@ -1246,6 +1247,7 @@ __global__ void k_slots_init(int* ist, long long S) {
   ist[IS_PH * S + i] = 0;
   ist[IS_N * S + i] = 0;
 }
+#endif
 
 // -------------------------------------------------------------------------------------------------
 // twin integrator (SYM<sys>INIT.acados_integrator): one RK4 step of length T per problem
@@ -1281,8 +1283,45 @@ __global__ __launch_bounds__(256) void rk4_sens_kernel(int B, double T, const do
   UNR for (int i = 0; i < NX; ++i) xo[(long long)b * NX + i] = x1[i];
 }
 
+// Jobs of the persistent wave kernel: either the slots still iterating in lane mode (hand-off,
+// list != nullptr) or problems [0, count) straight from the inputs.
+struct WaveJobs {
+  const int* list;
+  int count;
+  unsigned* next;          // job counter
+  double* regions;         // one stage-record region per workgroup
+  long long region_doubles;
+};
+
+// The UR5 arm's wave solver lives in its own translation unit (wave_arm.hip, coop_arm.h, built at -O1):
+// its layout and launch, for the handle code below.
+namespace arm_api {
+size_t lds_bytes(int nmax);
+long long region_doubles(int nmax);
+long long hot_doubles();
+const void* kernel();
+hipError_t launch(dim3 grid, size_t lds, hipStream_t st, const Work& w, const Opts& o, const Inputs& in,
+                  const SlotState& ss, const WaveJobs& jb);
+}  // namespace arm_api
+
 }  // namespace vboc
 
+#ifdef VBOC_ARM_TU
+#include "coop_arm.h"
+namespace vboc {
+namespace arm_api {
+size_t lds_bytes(int nmax) { return arm::WaveLayout<4>::lds_bytes(nmax); }
+long long region_doubles(int nmax) { return (long long)arm::WaveLayout<4>::region_doubles(nmax); }
+long long hot_doubles() { return arm::WaveLayout<4>::OX; }
+const void* kernel() { return (const void*)arm::k_wave_ur5; }
+hipError_t launch(dim3 grid, size_t lds, hipStream_t st, const Work& w, const Opts& o, const Inputs& in,
+                  const SlotState& ss, const WaveJobs& jb) {
+  hipLaunchKernelGGL(arm::k_wave_ur5, grid, dim3(64), lds, st, w, o, in, ss, jb);
+  return hipGetLastError();
+}
+}  // namespace arm_api
+}  // namespace vboc
+#else
 #include "coop.h"
 #include "ft.h"
 
@@ -1449,7 +1488,8 @@ static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st) {
 // batch (profiles/r01_wave_groups_sweep.log): 1024 groups 5434, 1408 groups 6212, 2048 groups 5504
 // solves/s.  `wave_groups` overrides; `mall_mib` changes the budget.
 static long long wave_group_budget(const vboc_solver* h, int nmax) {
-  const long long hot = (long long)(h->nq == 1 ? WaveLayout<1>::OX : (h->nq == 2 ? WaveLayout<2>::OX : WaveLayout<3>::OX)) *
+  const long long hot = (long long)(h->nq == 1 ? WaveLayout<1>::OX
+                                    : (h->nq == 2 ? WaveLayout<2>::OX : (h->nq == 3 ? WaveLayout<3>::OX : arm_api::hot_doubles()))) *
                         (long long)(nmax + 1) * (long long)sizeof(double);
   const long long g = (long long)(0.92 * h->mall_mib * 1024.0 * 1024.0) / (hot > 0 ? hot : 1);
   return g < 256 ? 256 : g;
@@ -1466,7 +1506,7 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
     case 1: hipLaunchKernelGGL(k_wave<1>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
     case 2: hipLaunchKernelGGL(k_wave<2>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
     case 3: hipLaunchKernelGGL(k_wave<3>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
-    default: return hipErrorInvalidValue;   // the UR5 arm runs in lane mode (vboc_create)
+    default: return arm_api::launch(grid, h->wave_lds, st, w, h->o, in, ss, jb);
   }
   return hipGetLastError();
 }
@@ -1484,7 +1524,10 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   vboc_solver* h = new vboc_solver();
   h->nq = nq; h->nmax = nmax; h->device = device;
   default_opts(h->o);
-  if (nq == 4) h->o.lm = 1e-2;   // UR5 OCP: levenberg_marquardt = 1e-2 (VBOC/UR5/ur5reduced_class_fixedveldir.py:135)
+  if (nq == 4) {
+    h->o.lm = 1e-2;          // UR5 OCP: levenberg_marquardt = 1e-2 (VBOC/UR5/ur5reduced_class_fixedveldir.py:135)
+    h->coop_threshold = 0;   // lane mode (wave_all = 0) for the arm runs without the wave tail
+  }
   if (slots <= 0) slots = 64 * 1024;
   if (slots > (1 << 30)) return fail(VBOC_ERR_ARG, "vboc_create: too many slots");
   slots = ((slots + 255) / 256) * 256;
@@ -1506,19 +1549,18 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   }
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);
-  // wave solver: one region of stage records per resident workgroup (occupancy x CUs).  The UR5 arm
-  // (nq = 4) is solved by the lane-per-problem kernels only: the wave solver's one-output-per-lane
-  // recursion steps and LDS ring slots are laid out for the pendulum chains.
-  if (nq == 4) {
-    h->wave_all = false;
-    h->coop_threshold = 0;
-    h->coop_ok = false;
-  } else {
-    const void* fn = nq == 1 ? (const void*)k_wave<1> : (nq == 2 ? (const void*)k_wave<2> : (const void*)k_wave<3>);
+  // wave solver: one region of stage records per resident workgroup (occupancy x CUs); the UR5 arm's
+  // (nq = 4) comes from its own -O1 translation unit (wave_arm.hip)
+  {
+    const void* fn = nq == 1 ? (const void*)k_wave<1>
+                             : (nq == 2 ? (const void*)k_wave<2> : (nq == 3 ? (const void*)k_wave<3> : arm_api::kernel()));
     h->wave_lds = nq == 1 ? WaveLayout<1>::lds_bytes(nmax)
-                          : (nq == 2 ? WaveLayout<2>::lds_bytes(nmax) : WaveLayout<3>::lds_bytes(nmax));
-    h->region_doubles = (long long)(nq == 1 ? WaveLayout<1>::region_doubles(nmax)
-                                            : (nq == 2 ? WaveLayout<2>::region_doubles(nmax) : WaveLayout<3>::region_doubles(nmax)));
+                          : (nq == 2 ? WaveLayout<2>::lds_bytes(nmax)
+                                     : (nq == 3 ? WaveLayout<3>::lds_bytes(nmax) : arm_api::lds_bytes(nmax)));
+    h->region_doubles = nq == 1 ? (long long)WaveLayout<1>::region_doubles(nmax)
+                                : (nq == 2 ? (long long)WaveLayout<2>::region_doubles(nmax)
+                                           : (nq == 3 ? (long long)WaveLayout<3>::region_doubles(nmax)
+                                                      : arm_api::region_doubles(nmax)));
     int per_cu = 0, cus = 0;
     hipDeviceProp_t prop;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, h->wave_lds) == hipSuccess &&
@@ -1599,8 +1641,6 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "ipm_tau") o.tau = v;
   else if (s == "coop_threshold") h->coop_threshold = v;
   else if (s == "wave_all") {
-    if (h->nq == 4 && v != 0.0)
-      return fail(VBOC_ERR_UNSUPPORTED, "vboc_set_option: the UR5 arm (nq = 4) is solved in lane mode only");
     h->wave_all = v != 0.0;
   }
   else if (s == "wave_groups") h->group_cap = (long long)v;
@@ -1947,3 +1987,4 @@ int vboc_rk4_batch_host(int nq, int B, double T, const double* x, const double* 
 }
 
 }  // extern "C"
+#endif  // VBOC_ARM_TU

@@ -39,13 +39,22 @@ class Batch(ctypes.Structure):
                 ("sqp_iter", ctypes.c_void_p), ("qp_iter", ctypes.c_void_p)]
 
 
+SRC_ARM = os.path.join(HERE, "csrc", "wave_arm.hip")
+
+
 def build(verbose=False):
-    """hipcc the solver for gfx950 into vboc_amd/libvboc_amd.so (in-tree)."""
-    cmd = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-o", LIB_PATH, SRC]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.check_call(cmd)
+    """hipcc the solver for gfx950 into vboc_amd/libvboc_amd.so (in-tree): vboc_solver.hip at -O3 and the
+    UR5 arm's wave solver (wave_arm.hip) at -O1 as a second translation unit."""
+    import tempfile
+    base = ["hipcc", "--offload-arch=gfx950", "-std=c++17", "-fPIC"]
+    with tempfile.TemporaryDirectory() as tmp:
+        o_main, o_arm = os.path.join(tmp, "solver.o"), os.path.join(tmp, "wave_arm.o")
+        cmds = [base + ["-O3", "-c", SRC, "-o", o_main], base + ["-O1", "-c", SRC_ARM, "-o", o_arm],
+                base + ["-shared", o_main, o_arm, "-o", LIB_PATH]]
+        for cmd in cmds:
+            if verbose:
+                print(" ".join(cmd))
+            subprocess.check_call(cmd)
     return LIB_PATH
 
 
