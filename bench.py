@@ -219,7 +219,9 @@ def main():
                     "kernel": f"k_qp_factor<{nq}>", "avg_launch_ms": round(avg_launch_ms, 4),
                     "launches": fact_launch}
     else:
-        traffic_gb, traffic_src = pmc_traffic("k_wave" if nq != 4 else "k_wave_ur5")
+        # the committed PMC passes are of the triple's k_wave<3> (and k_wave_ur5 once profiled): no other
+        # instantiation borrows them
+        traffic_gb, traffic_src = pmc_traffic("k_wave" if nq == 3 else ("k_wave_ur5" if nq == 4 else f"k_wave_nq{nq}"))
         avg_ms = wave_ms / max(1, wave_launch)
         per_launch = local_flops / max(1, args.steps)
         wave_tf = per_launch / (avg_ms * 1e-3) / 1e12 if wave_ms else None
