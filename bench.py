@@ -219,9 +219,8 @@ def main():
                     "kernel": f"k_qp_factor<{nq}>", "avg_launch_ms": round(avg_launch_ms, 4),
                     "launches": fact_launch}
     else:
-        # the committed PMC passes are of the triple's k_wave<3> (and k_wave_ur5 once profiled): no other
-        # instantiation borrows them
-        traffic_gb, traffic_src = pmc_traffic("k_wave" if nq == 3 else ("k_wave_ur5" if nq == 4 else f"k_wave_nq{nq}"))
+        # PMC passes are per instantiation (profiles/*_pmc_k_wave.json is the triple's k_wave<3>)
+        traffic_gb, traffic_src = pmc_traffic("k_wave" if nq == 3 else f"k_wave_nq{nq}")
         avg_ms = wave_ms / max(1, wave_launch)
         per_launch = local_flops / max(1, args.steps)
         wave_tf = per_launch / (avg_ms * 1e-3) / 1e12 if wave_ms else None
@@ -231,7 +230,7 @@ def main():
                     "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
                     "traffic_source": traffic_src,
                     "algorithmic": "FP64 flops per launch, SURVEY.md 8(d): N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp)",
-                    "flops_per_launch": round(per_launch), "kernel": f"k_wave<{nq}>" if nq != 4 else "k_wave_ur5",
+                    "flops_per_launch": round(per_launch), "kernel": f"k_wave<{nq}>",
                     "avg_launch_ms": round(avg_ms, 3), "launches": wave_launch}
     if rank == 0:
         line = {

@@ -31,7 +31,7 @@
  *   The UR5 OCP has no dt state (x = [q, qdot], p = w, tf = 1 over N = 100 intervals): its shooting
  *   interval (set_new_time_steps, dt_sym = 1e-2) travels in the dt column, and p[nq] = 0.  Its
  *   OCPUR5INIT.OCP_solve (:145-192) is otherwise the same boundary problem; levenberg_marquardt defaults
- *   to 1e-2 on an nq = 4 handle (:131).  nq = 4 runs on its own wave-solver instantiation (k_wave_ur5,
+ *   to 1e-2 on an nq = 4 handle (:131).  nq = 4 runs on the wave solver (k_wave<4>,
  *   the default) or the lane-per-problem kernels (wave_all = 0); it has no free-time variant.
  *   N[b]                 horizon of problem b (<= nmax of the handle)
  *   x_guess[b][nmax+1][nx]  stage guesses; row N[b] is the stage-N guess (OCP_solve sets it from

@@ -184,7 +184,7 @@ def test_first_solve_equals_ics():
             np.testing.assert_array_equal(getattr(r, f), b[kk][k])
 
 
-# ---- GPU (wave solver k_wave_ur5 by default, lane-per-problem kernels on request; RNEA sensitivities) ----
+# ---- GPU (wave solver k_wave<4> by default, lane-per-problem kernels on request; RNEA sensitivities) ----
 def _gpu_solve(b, **opts):
     from vboc_amd import lib
     s = lib.Solver(4, int(np.max(b["N"])), slots=max(256, len(b["N"])))
@@ -199,11 +199,9 @@ def _gpu_solve(b, **opts):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,B", [("wave", 96), ("lane", 32)])
 def test_ur5_parity_with_oracle(mode, B):
-    """Bars of the pendulum chains (tests/test_gpu.py): status >= 98 %, cost and x_0 of problems converged on
-    both: median <= 1e-9, max <= 2e-3; SQP-iteration agreement >= 95 % in lane mode.  The arm's wave solver
-    (k_wave_ur5, the -O1 unit) has an open defect: it follows a different iteration sequence on ~20 % of the
-    problems (same converged points: |dcost| <= 1e-4 measured, profiles/r01h_ur5_wave_vs_lane.log), so its
-    iteration bar is 75 %."""
+    """The bars of the pendulum chains (tests/test_gpu.py) in both modes: status >= 98 %, SQP-iteration
+    agreement >= 95 %, cost and x_0 of problems converged on both: median <= 1e-9, max <= 2e-3.  The wave
+    solver is k_wave<4> at -O3, one wave per SIMD (no scratch spills)."""
     import oracle
     from vboc_amd.ics import ur5_ics
     b = ur5_ics(np.arange(B))
@@ -212,7 +210,7 @@ def test_ur5_parity_with_oracle(mode, B):
                                    b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"],
                                    opts=oracle.default_opts(max_iter=300, lm=1e-2))
     assert np.mean(g["status"] == r["status"]) >= 0.98, (g["status"], r["status"])
-    assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= (0.95 if mode == "lane" else 0.75), (g["sqp_iter"], r["sqp_iter"])
+    assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= 0.95, (g["sqp_iter"], r["sqp_iter"])
     both = (g["status"] == 0) & (r["status"] == 0)
     assert both.mean() >= 0.5
     dc = np.abs(g["cost"] - r["cost"])[both]

@@ -21,6 +21,8 @@
 // LDS per problem is ~8 KB, so several problems share a CU (occupancy is set by registers).
 // The arithmetic is the algorithm of Lane<NQ> / oracle/vboc_oracle.c (same formulas, same
 // decisions); only summation orders differ (rounding-level).
+// Sizes: NQ = 1-3 are the pendulum chains (one output per lane per recursion step, stage windows of
+// one or two LDS-DMAs); NQ = 4 is the UR5 arm (NX = 8: two outputs per lane, windows of up to three DMAs).
 #pragma once
 
 namespace vboc {
@@ -50,7 +52,13 @@ struct WaveLayout {
   // LDS-DMA rings (global_load_lds_dwordx4: one wave-instruction lands 64 lanes x 16 B = 128 doubles):
   // the factorisation streams its window two stages ahead through 4 slots of 2 KiB (two DMAs per
   // stage), the vector / forward / costate recursions six stages ahead through 8 slots of 1 KiB
-  static constexpr int RSF = 256, NSF = 4, DF = 2, RSV = 128, NSV = 8, DV = 6;
+  // DMAs per stage window (one DMA = 128 doubles); the slot sizes of the pendulum chains (NQ <= 3) are
+  // kept as tuned, the UR5 arm (NQ = 4) gets slots of whole DMAs
+  static constexpr int P_FAC = (W_FAC + 127) / 128, P_VEC = (W_VEC + 127) / 128, P_FWD = (W_FWD + 127) / 128,
+                       P_COS = (W_COS + 127) / 128;
+  static constexpr int P_VMAX = P_VEC > P_FWD ? (P_VEC > P_COS ? P_VEC : P_COS) : (P_FWD > P_COS ? P_FWD : P_COS);
+  static constexpr int RSF = NQ <= 3 ? 256 : 128 * P_FAC, NSF = 4, DF = 2, RSV = NQ <= 3 ? 128 : 128 * P_VMAX,
+                       NSV = 8, DV = 6;
   static constexpr int RING_D = NSF * RSF > NSV * RSV ? NSF * RSF : NSV * RSV;
   static_assert(OB % 2 == 0 && OZ % 2 == 0 && OD % 2 == 0 && OK % 2 == 0 && OPE % 2 == 0 && OC % 2 == 0 &&
                     OACL % 2 == 0 && OX % 2 == 0,
@@ -162,6 +170,7 @@ __device__ __forceinline__ void tri(int u, int& i, int& j) {
 // vboc_debug_counters().  Scalar counters (no arrays, no printf) keep the instrumented build's
 // register allocation and schedule close to the product build.
 __device__ unsigned long long g_wave_prof[16];
+__device__ unsigned g_dbg_cnt;
 #ifdef VBOC_COOP_PROF
 #define CPROF_DECL unsigned long long cp0 = 0, cp1 = 0, cp2 = 0, cp3 = 0, cp4 = 0, cp5 = 0, cp6 = 0, cp7 = 0, cp8 = 0; \
   unsigned long long cp_t = __builtin_amdgcn_s_memtime();
@@ -244,7 +253,9 @@ struct Coop {
   // wait until at most N VMEM ops of this wave are outstanding (LDS-DMA landings are ordered for this
   // wave's own ds_reads by this wait alone)
   template <int N>
-  __device__ __forceinline__ static void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+  __device__ __forceinline__ static void vmwait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+  }
   // retire every ordinary VMEM op in a way the compiler's waitcnt pass sees (the builtin, vmcnt(0)):
   // called before a ring's first DMA, so no loop-carried register is still "pending" in the pass's
   // bookkeeping - otherwise it re-waits vmcnt(0) inside the loop and drains the ring every stage
@@ -256,6 +267,24 @@ struct Coop {
     const dbl2* src = (const dbl2*)(s + fslot(slot));
     gdbl2* dst = (gdbl2*)(g + (long long)k * REC);
     if (t < (HI - LO) / 2) dst[LO / 2 + t] = src[LO / 2 + t];
+  }
+
+  // debug (-DVBOC_DBG_CHECK): compare a landed ring window with a direct global read of the same fields
+  __device__ __forceinline__ void dbg_check(int kb, int k, int lo, int W, int tag) const {
+#ifdef VBOC_DBG_CHECK
+    int bad = -1;
+    double a0 = 0.0, b0 = 0.0;
+    for (int e = t; e < W; e += 64) {
+      const double a = s[kb + e], b = st(k, lo + e);
+      if (__double_as_longlong(a) != __double_as_longlong(b) && bad < 0) { bad = e; a0 = a; b0 = b; }
+    }
+    if (bad >= 0) {
+      const unsigned c = atomicAdd(&g_dbg_cnt, 1u);
+      if (c < 40) printf("tag %d lane %d k %d N %d off %d lds %.17g glob %.17g\n", tag, t, k, N, bad, a0, b0);
+    }
+#else
+    (void)kb; (void)k; (void)lo; (void)W; (void)tag;
+#endif
   }
 
   // box of component i of stage k (the Lane::stage_box pattern)
@@ -335,23 +364,40 @@ struct Coop {
     d.rel = 0;
     d.sg = 1.0;
   }
-  template <int L1, int L2>
-  __device__ __forceinline__ void dstep(const Dsc& d, int kb) const {
-    auto ad = [&](int a, unsigned bit) { return a + ((d.rel & bit) ? kb : 0); };
-    const int x1 = ad(d.x1, RX1), y1 = ad(d.y1, RY1), x2 = ad(d.x2, RX2), y2 = ad(d.y2, RY2);
-    // every operand load issued before any arithmetic: one LDS round trip per step
-    double a1[L1 > 0 ? L1 : 1], b1[L1 > 0 ? L1 : 1], a2[L2 > 0 ? L2 : 1], b2[L2 > 0 ? L2 : 1];
-    UNR for (int q = 0; q < L1; ++q) { a1[q] = s[x1 + q * d.sx1]; b1[q] = s[y1 + q * d.sy1]; }
-    UNR for (int q = 0; q < L2; ++q) { a2[q] = s[x2 + q * d.sx2]; b2[q] = s[y2 + q * d.sy2]; }
-    const double r0 = s[ad(d.ini, RINI)];
-    __builtin_amdgcn_sched_barrier(0);
-    double s1 = 0.0, s2 = 0.0;
-    UNR for (int q = 0; q < L1; ++q) s1 += a1[q] * b1[q];
-    UNR for (int q = 0; q < L2; ++q) s2 += a2[q] * b2[q];
-    const double r = r0 + d.sg * s1 + s2;
+  // outputs per lane of one recursion step: 1 for the pendulum chains, 2 for the UR5 arm (NX = 8)
+  static constexpr int TXC = NX * (NX + 1) / 2, TUC = NU * (NU + 1) / 2, TMC = M0 * (M0 + 1) / 2;
+  static constexpr int imax(int a, int b) { return a > b ? a : b; }
+  static constexpr int OUTMAX =
+      imax(imax(imax(NX * NX + NX * NU + NX + NQ, TXC + TUC + NU * NX + NU * NQ), imax(TXC + NX * NQ + NQ * NQ,
+                                                                                      M0 * NX + M0 * NQ + NX + NQ)),
+           imax(TMC, NQ * NQ));
+  static constexpr int RD = (OUTMAX + 63) / 64;
+
+  template <int L1, int L2, int R>
+  __device__ __forceinline__ void dstep(const Dsc (&dd)[R], int kb) const {
+    double res[R];
+    UNR for (int rr = 0; rr < R; ++rr) {
+      const Dsc& d = dd[rr];
+      auto ad = [&](int a, unsigned bit) { return a + ((d.rel & bit) ? kb : 0); };
+      const int x1 = ad(d.x1, RX1), y1 = ad(d.y1, RY1), x2 = ad(d.x2, RX2), y2 = ad(d.y2, RY2);
+      // every operand load issued before any arithmetic: one LDS round trip per step
+      double a1[L1 > 0 ? L1 : 1], b1[L1 > 0 ? L1 : 1], a2[L2 > 0 ? L2 : 1], b2[L2 > 0 ? L2 : 1];
+      UNR for (int q = 0; q < L1; ++q) { a1[q] = s[x1 + q * d.sx1]; b1[q] = s[y1 + q * d.sy1]; }
+      UNR for (int q = 0; q < L2; ++q) { a2[q] = s[x2 + q * d.sx2]; b2[q] = s[y2 + q * d.sy2]; }
+      const double r0 = s[ad(d.ini, RINI)];
+      __builtin_amdgcn_sched_barrier(0);
+      double s1 = 0.0, s2 = 0.0;
+      UNR for (int q = 0; q < L1; ++q) s1 += a1[q] * b1[q];
+      UNR for (int q = 0; q < L2; ++q) s2 += a2[q] * b2[q];
+      res[rr] = r0 + d.sg * s1 + s2;
+    }
     lsync();
-    s[ad(d.d1, RD1)] = r;
-    s[ad(d.d2, RD2)] = r;
+    UNR for (int rr = 0; rr < R; ++rr) {
+      const Dsc& d = dd[rr];
+      auto ad = [&](int a, unsigned bit) { return a + ((d.rel & bit) ? kb : 0); };
+      s[ad(d.d1, RD1)] = res[rr];
+      s[ad(d.d2, RD2)] = res[rr];
+    }
     lsync();
   }
   // all lanes: L = chol(s[ru..]); lane-specific column solve rhs -> sgn * Ru^-1 rhs; lane 0 stores L
@@ -372,13 +418,16 @@ struct Coop {
   }
 
   // descriptors of the middle-stage factorisation steps (rs enters through sg)
-  __device__ void desc_mid(Dsc& d1, Dsc& d2, Dsc& d4) const {
+  __device__ __forceinline__ void desc_mid(Dsc (&dd1)[RD], Dsc (&dd2)[RD], Dsc (&dd4)[RD]) const {
+    UNR for (int rr = 0; rr < RD; ++rr) desc_mid1(dd1[rr], dd2[rr], dd4[rr], t + 64 * rr);
+  }
+  __device__ __forceinline__ void desc_mid1(Dsc& d1, Dsc& d2, Dsc& d4, const int lane) const {
     constexpr int P = L::P, PA = L::PA, PB = L::PB, APA = L::APA, RU = L::RU, S = L::S, PI = L::PI, SC = L::SC,
                   LINE = L::LINE;
     constexpr int TX = NX * (NX + 1) / 2, TU = NU * (NU + 1) / 2;
     dnull(d1); dnull(d2); dnull(d4);
     // step 1: PA = P A, PB = P B, P e (-> stage PE), lin_e += Pi' e
-    int u = t;
+    int u = lane;
     if (u < NX * NX) {
       const int i = u / NX, j = u % NX;
       d1.x1 = P + i * NX; d1.sx1 = 1; d1.y1 = OA + j; d1.sy1 = NX; d1.rel = RY1; d1.d1 = d1.d2 = PA + u;
@@ -392,7 +441,7 @@ struct Coop {
       d1.x1 = PI + u; d1.sx1 = NQ; d1.y1 = OE; d1.sy1 = 1; d1.sg = rs; d1.ini = d1.d1 = d1.d2 = LINE + u; d1.rel = RY1;
     }
     // step 2: A'PA + diag(Hx), B'PB + diag(Hu), S = B'PA, Y = B'Pi
-    u = t;
+    u = lane;
     if (u < TX) {
       int i, j;
       tri(u, i, j);
@@ -413,7 +462,7 @@ struct Coop {
       d2.x1 = OB + a; d2.sx1 = NU; d2.y1 = PI + j; d2.sy1 = NQ; d2.rel = RX1 | RD1 | RD2; d2.d1 = d2.d2 = OY + u;
     }
     // step 4: P <- A'PA + Hx + S'K, Pi <- A'Pi + K'Y, Sc += Y'M
-    u = t;
+    u = lane;
     if (u < TX) {
       int i, j;
       tri(u, i, j);
@@ -431,12 +480,15 @@ struct Coop {
     }
   }
   // stage 0 (controls s, u_0; F0 = [A0 g, B0]): e and H of stage 0 come from its ring slot
-  __device__ void desc_s0(Dsc& z1, Dsc& z2, Dsc& z4) const {
+  __device__ __forceinline__ void desc_s0(Dsc (&zz1)[RD], Dsc (&zz2)[RD], Dsc (&zz4)[RD]) const {
+    UNR for (int rr = 0; rr < RD; ++rr) desc_s01(zz1[rr], zz2[rr], zz4[rr], t + 64 * rr);
+  }
+  __device__ __forceinline__ void desc_s01(Dsc& z1, Dsc& z2, Dsc& z4, const int lane) const {
     constexpr int P = L::P, BP = L::PA, PI = L::PI, F0 = L::F0, Y0 = L::Y0, PE0 = L::PE0, LINE = L::LINE,
                   LR0 = L::LR0, MM0 = L::MM0, SC = L::SC;
     constexpr int TM = M0 * (M0 + 1) / 2;
     dnull(z1); dnull(z2); dnull(z4);
-    int u = t;
+    int u = lane;
     if (u < M0 * NX) {
       const int a = u / NX, j = u % NX;
       z1.x1 = F0 + a; z1.sx1 = M0; z1.y1 = P + j; z1.sy1 = NX; z1.d1 = z1.d2 = BP + u;
@@ -448,7 +500,7 @@ struct Coop {
     } else if ((u -= NX) < NQ) {
       z1.x1 = PI + u; z1.sx1 = NQ; z1.y1 = OE; z1.sy1 = 1; z1.sg = rs; z1.ini = z1.d1 = z1.d2 = LINE + u; z1.rel = RY1;
     }
-    u = t;
+    u = lane;
     if (u < TM) {
       int a, c;
       tri(u, a, c);
@@ -456,7 +508,7 @@ struct Coop {
       if (a == c) { z2.ini = OD + a; z2.rel = RINI; }
       z2.d1 = LR0 + a * M0 + c; z2.d2 = LR0 + c * M0 + a;
     }
-    u = t;
+    u = lane;
     if (u < NQ * NQ) {
       const int i = u / NQ, j = u % NQ;
       z4.x2 = Y0 + i; z4.sx2 = NQ; z4.y2 = MM0 + j; z4.sy2 = NQ; z4.ini = z4.d1 = z4.d2 = SC + u;
@@ -466,7 +518,7 @@ struct Coop {
   // ---------------------------------------------------------------------------------------------
   // problem set-up: from the inputs (wave mode) or from a lane-mode slot (hand-off)
   // ---------------------------------------------------------------------------------------------
-  __device__ void from_inputs(const Inputs& in, int pid) {
+  __device__ __forceinline__ void from_inputs(const Inputs& in, int pid) {
     fresh();
     constexpr int NXR = NX + 1, NP = NQ + 1;
     N = in.N[pid];
@@ -520,7 +572,7 @@ struct Coop {
     }
     __syncthreads();
   }
-  __device__ void from_slot(const SlotState& ss, unsigned slot) {
+  __device__ __forceinline__ void from_slot(const SlotState& ss, unsigned slot) {
     fresh();
     Lane<NQ> G(w, o, slot);
     N = ss(IS_N, slot);
@@ -539,7 +591,7 @@ struct Coop {
   // ---------------------------------------------------------------------------------------------
   // linearisation (stage-parallel): ERK4 + sensitivities, defects, current z, NLP residuals
   // ---------------------------------------------------------------------------------------------
-  __device__ void linearize(double& rstat, double& req, double& rineq, double& rcomp) {
+  __device__ __forceinline__ void linearize(double& rstat, double& req, double& rineq, double& rcomp) {
     fresh();
     const double h = par(PF::H), sv = par(PF::S);
     double stt = 0.0, eq = 0.0, inq = 0.0, cp = 0.0;
@@ -634,7 +686,7 @@ struct Coop {
   // ---------------------------------------------------------------------------------------------
   // interior-point QP
   // ---------------------------------------------------------------------------------------------
-  __device__ void qp_init() {
+  __device__ __forceinline__ void qp_init() {
     fresh();
     double musum = 0.0, nb = 0.0, rd = 0.0, e0 = 0.0;
     for (int k = t; k <= N; k += 64) {
@@ -686,14 +738,14 @@ struct Coop {
     __syncthreads();
   }
 
-  __device__ int qp_check() const {
+  __device__ __forceinline__ int qp_check() const {
     if (!isfinite(mu)) return -1;
     if (mu < o.qp_tol_comp && rs * rd0 < o.qp_tol_stat && rs * e00 < o.qp_tol_eq) return 0;
     return 1;
   }
 
   // H -> D slot, predictor gradient -> DA slot
-  __device__ void prep_pred() {
+  __device__ __forceinline__ void prep_pred() {
     fresh();
     for (int k = t; k <= N; k += 64) {
       IP r;
@@ -709,7 +761,7 @@ struct Coop {
     __syncthreads();
   }
   // corrector gradient (uses the affine direction in DA) -> D slot
-  __device__ void prep_corr(double smu) {
+  __device__ __forceinline__ void prep_corr(double smu) {
     fresh();
     for (int k = t; k <= N; k += 64) {
       IP r;
@@ -733,7 +785,7 @@ struct Coop {
   }
 
   // Riccati factorisation (matrix part) of stages N-1..0 through the LDS ring; the vector part is vec()
-  __device__ bool factor() {
+  __device__ __forceinline__ bool factor() {
     fresh();
     for (int e = t; e < NX * NX; e += 64) {
       const int i = e / NX, j = e % NX;
@@ -747,18 +799,17 @@ struct Coop {
     if (t < NQ) s[L::LINE + t] = 0.0;
     // stage windows through the 4-slot LDS-DMA ring, landing two stages ahead (sweep index j <-> stage
     // N-1-j, clamped at 0); P = DMAs per stage
-    constexpr int P = L::W_FAC > 128 ? 2 : 1;
+    constexpr int P = L::P_FAC;
     auto fdma = [&](int j) {
       const int kk = N - 1 - j >= 0 ? N - 1 - j : 0;
-      dma(kk, 0, L::W_FAC, fslot(j % L::NSF), 0);
-      if (P == 2) dma(kk, 0, L::W_FAC, fslot(j % L::NSF), 1);
+      UNR for (int part = 0; part < P; ++part) dma(kk, 0, L::W_FAC, fslot(j % L::NSF), part);
     };
     __syncthreads();   // before any DMA is in flight: this barrier's fence would drain them
     settle();
     fdma(0);
     fdma(1);
     bool ok = true;
-    Dsc d1, d2, d4;
+    Dsc d1[RD], d2[RD], d4[RD];
     desc_mid(d1, d2, d4);
     SPROF_DECL(1)
     for (int j = 0; j < N; ++j) {
@@ -771,6 +822,7 @@ struct Coop {
       if (j == 0) vmwait<2 * P>();
       else if (j == 1) vmwait<2 * P + 1>();
       else vmwait<2 * P + 2>();
+      dbg_check(kb, k, 0, L::W_FAC, 1);
       SPROF(3)
       if (k >= 1) {
         dstep<NX, 0>(d1, kb);
@@ -786,7 +838,7 @@ struct Coop {
         dstep<NX, NU>(d4, kb);
         SPROF(2)
       } else {
-        Dsc z1, z2, z4;
+        Dsc z1[RD], z2[RD], z4[RD];
         desc_s0(z1, z2, z4);
         dstep<NX, 0>(z1, kb);
         dstep<NX, 0>(z2, kb);
@@ -807,7 +859,7 @@ struct Coop {
   // closed-loop matrices A_cl = A + B K of stages 1..N-1 (row-major, OACL): formed once per
   // factorisation, stage-parallel, and shared by both vector passes (columns) and both forward
   // sweeps (rows) of the interior-point iteration
-  __device__ void acl_pass() {
+  __device__ __forceinline__ void acl_pass() {
     fresh();
     constexpr int NAB = (NX * NX + NX * NU) / 2, NKK = (NU * NX) / 2;
     for (int k = 1 + t; k < N; k += 64) {
@@ -835,7 +887,7 @@ struct Coop {
 
   // vector pass with the gradient in slot OG; leaves the stage-0 open-loop step w0 and the
   // terminal multiplier nu (wave-uniform).  False if S = sum Y'M is not positive definite.
-  __device__ bool vec(int OG, double (&w0)[M0], double (&nun)[NQ]) {
+  __device__ __forceinline__ bool vec(int OG, double (&w0)[M0], double (&nun)[NQ]) {
     fresh();
     // p_k = c'_k + A_cl,k' p_{k+1},  c'_k = g_x + K'g_u + A_cl' PE_k  (lane i: row i of p);
     // v_k = PE_k + p_{k+1} is kept for k_f.  c' is formed stage-parallel first (-> OC).
@@ -874,9 +926,10 @@ struct Coop {
     __syncthreads();
     // stage windows [PE | C | ACL] through the 8-slot LDS-DMA ring, DV stages ahead (sweep index j <->
     // stage N-1-j, clamped at 1): one DMA per stage, so DV - 1 are younger than the one waited for
+    constexpr int PV = L::P_VEC;
     auto vdma = [&](int j) {
       const int kk = N - 1 - j >= 1 ? N - 1 - j : 1;
-      dma(kk, L::LO_VEC, L::W_VEC, vslot(j % L::NSV), 0);
+      UNR for (int part = 0; part < PV; ++part) dma(kk, L::LO_VEC, L::W_VEC, vslot(j % L::NSV), part);
     };
     auto vld = [&](int kb, double (&acl)[NX], double& cc, double& pe) {
       const int i = t < NX ? t : NX - 1;
@@ -888,14 +941,15 @@ struct Coop {
     settle();
     if (cnt >= 1) {
       UNR for (int d = 0; d < L::DV; ++d) vdma(d);
-      vmwait<L::DV - 1>();
+      vmwait<(L::DV - 1) * PV>();
       vld(vslot(0), acl, cc, pe);
     }
     for (int j = 0; j < cnt; ++j) {
       const int k = N - 1 - j;
       const int rb = L::PV + (j & 1) * NX, wb = L::PV + ((j + 1) & 1) * NX;
       vdma(j + L::DV);
-      vmwait<L::DV - 1>();   // stage of sweep index j + 1 has landed
+      vmwait<(L::DV - 1) * PV>();   // stage of sweep index j + 1 has landed
+      dbg_check(vslot((j + 1) % L::NSV), N - 2 - j >= 1 ? N - 2 - j : 1, L::LO_VEC, L::W_VEC, 2);
       double pv[NX], an[NX], cn, pn;
       UNR for (int q = 0; q < NX; ++q) pv[q] = s[rb + q];
       vld(vslot((j + 1) % L::NSV), an, cn, pn);
@@ -972,7 +1026,7 @@ struct Coop {
   // forward sweep.  CORR == false: affine direction -> DA, returns the affine step and the mu_aff
   // polynomial; CORR == true: combined direction -> D, returns alpha_max.
   template <bool CORR>
-  __device__ void fwd(const double (&w0in)[M0], const double (&nun)[NQ], double smu, double& amax, double& c0,
+  __device__ __forceinline__ void fwd(const double (&w0in)[M0], const double (&nun)[NQ], double smu, double& amax, double& c0,
                       double& c1, double& c2) {
     fresh();
     constexpr int OT = CORR ? OD : ODA;
@@ -1032,9 +1086,10 @@ struct Coop {
     __syncthreads();
     // stage windows [C | ACL] through the 8-slot LDS-DMA ring, DV stages ahead (sweep index j <-> stage
     // 1 + j, clamped at N - 1)
+    constexpr int PW = L::P_FWD;
     auto wdma = [&](int j) {
       const int kk = 1 + j < N ? 1 + j : N - 1;
-      dma(kk, L::LO_FWD, L::W_FWD, vslot(j % L::NSV), 0);
+      UNR for (int part = 0; part < PW; ++part) dma(kk, L::LO_FWD, L::W_FWD, vslot(j % L::NSV), part);
     };
     auto fld = [&](int kb, double (&acl)[NX], double& cc) {
       const int i = t < NX ? t : NX - 1;
@@ -1046,14 +1101,15 @@ struct Coop {
       settle();
       if (cnt >= 1) {
         UNR for (int d = 0; d < L::DV; ++d) wdma(d);
-        vmwait<L::DV - 1>();
+        vmwait<(L::DV - 1) * PW>();
         fld(vslot(0), acl, cc);
       }
       for (int j = 0; j < cnt; ++j) {
         const int k = 1 + j;
         const int rb = L::DXV + (j & 1) * NX, wb = L::DXV + ((j + 1) & 1) * NX;
         wdma(j + L::DV);
-        vmwait<L::DV - 1>();
+        vmwait<(L::DV - 1) * PW>();
+        dbg_check(vslot((j + 1) % L::NSV), 2 + j < N ? 2 + j : N - 1, L::LO_FWD, L::W_FWD, 3);
         double dx[NX], an[NX], cn;
         UNR for (int q = 0; q < NX; ++q) dx[q] = s[rb + q];
         fld(vslot((j + 1) % L::NSV), an, cn);
@@ -1131,7 +1187,7 @@ struct Coop {
     SPROF_FLUSH
   }
 
-  __device__ void update(double alpha, double smu) {
+  __device__ __forceinline__ void update(double alpha, double smu) {
     fresh();
     double musum = 0.0;
     for (int k = t; k <= N; k += 64) {
@@ -1160,7 +1216,7 @@ struct Coop {
   }
 
   // costate recovery into the DA slot (x part) of stages 0..N-1
-  __device__ bool costate() {
+  __device__ __forceinline__ bool costate() {
     fresh();
     bool fin = true;
     if (t < NX) {
@@ -1176,9 +1232,10 @@ struct Coop {
     const int cnt = N - 1;   // stages N-1 .. 1
     __syncthreads();
     // stage windows [A, e) through the 8-slot LDS-DMA ring (sweep index j <-> stage N-1-j, clamped at 1)
+    constexpr int PC = L::P_COS;
     auto cdma = [&](int j) {
       const int kk = N - 1 - j >= 1 ? N - 1 - j : 1;
-      dma(kk, 0, L::W_COS, vslot(j % L::NSV), 0);
+      UNR for (int part = 0; part < PC; ++part) dma(kk, 0, L::W_COS, vslot(j % L::NSV), part);
     };
     auto cterms = [&](int kb, double (&ac)[NX], double& cc) {
       const int i = t < NX ? t : NX - 1;
@@ -1189,14 +1246,15 @@ struct Coop {
     settle();
     if (cnt >= 1) {
       UNR for (int d = 0; d < L::DV; ++d) cdma(d);
-      vmwait<L::DV - 1>();
+      vmwait<(L::DV - 1) * PC>();
       cterms(vslot(0), ac, cc);
     }
     for (int j = 0; j < cnt; ++j) {
       const int k = N - 1 - j;
       const int rb = L::DXV + (j & 1) * NX, wb = L::DXV + ((j + 1) & 1) * NX;
       cdma(j + L::DV);
-      vmwait<L::DV - 1>();
+      vmwait<(L::DV - 1) * PC>();
+      dbg_check(vslot((j + 1) % L::NSV), N - 2 - j >= 1 ? N - 2 - j : 1, 0, L::W_COS, 4);
       double lam[NX], an[NX], cn;
       UNR for (int q = 0; q < NX; ++q) lam[q] = s[rb + q];
       cterms(vslot((j + 1) % L::NSV), an, cn);
@@ -1224,7 +1282,7 @@ struct Coop {
   // ---------------------------------------------------------------------------------------------
   // merit line search + update (stage-parallel)
   // ---------------------------------------------------------------------------------------------
-  __device__ void update_weights() {
+  __device__ __forceinline__ void update_weights() {
     fresh();
     double lmax = 0.0;
     for (int k = t; k <= N; k += 64) {
@@ -1241,7 +1299,9 @@ struct Coop {
     __syncthreads();
   }
 
-  __device__ double merit(double alpha) {
+  // forced inline: as a call (the UR5 instantiation is large enough for the inliner to refuse), the
+  // kernel's arguments and the Coop state had to live in scratch behind flat pointers
+  __device__ __forceinline__ double merit(double alpha) {
     fresh();
     const double h = par(PF::H);
     const double sv = par(PF::S) + alpha * st(0, ODZ);
@@ -1278,7 +1338,7 @@ struct Coop {
     return par(PF::CS) * sv + par(PF::CCONST) + wsum(val) + par(PF::WBND) * wsum(viol);
   }
 
-  __device__ void apply(double alpha) {
+  __device__ __forceinline__ void apply(double alpha) {
     fresh();
     for (int k = t; k <= N; k += 64) {
       gdouble* rec = &g[(long long)k * REC];
@@ -1306,7 +1366,7 @@ struct Coop {
     __syncthreads();
   }
 
-  __device__ void store(const Inputs& in, int pid, int status, int it, int qit) {
+  __device__ __forceinline__ void store(const Inputs& in, int pid, int status, int it, int qit) {
     fresh();
     constexpr int NXR = NX + 1;
     double* xo = in.xo + (long long)pid * (in.nmax + 1) * NXR;
@@ -1332,7 +1392,7 @@ struct Coop {
   }
 
   // the remaining SQP of the loaded problem, to termination; returns the ACADOS status
-  __device__ int run(int& it, int& qit) {
+  __device__ __forceinline__ int run(int& it, int& qit) {
     for (int e = t; e < 16; e += 64) s[L::ZERO + e] = 0.0;
     __syncthreads();
     int status = -1;
@@ -1412,16 +1472,18 @@ struct Coop {
 };
 
 
-// Register budget of the wave kernel: two waves per SIMD (<= 256 VGPRs, eight problems per CU).  It
-// fits without spills only because every pass re-derives its lane-dependent values (Coop::fresh());
-// override with -DVBOC_WAVE_WPE= (empty) for the unconstrained one-wave build.
-#ifndef VBOC_WAVE_WPE
-#define VBOC_WAVE_WPE __attribute__((amdgpu_waves_per_eu(2, 2)))
-#endif
+// Register budget of the wave kernel.  The pendulum chains run two waves per SIMD (<= 256 registers,
+// eight problems per CU); they fit without spills only because every pass re-derives its lane-dependent
+// values (Coop::fresh()).  The UR5 arm's rigid-body model alone needs ~430 registers (rk4_kernel<4>), so
+// its instantiation runs one wave per SIMD (256 VGPRs + 256 AGPRs, no scratch): squeezed into 256 it spilled
+// ~2000 VGPRs to scratch and the -O2/-O3 builds then produced wrong QP steps.
+template <int NQ>
+struct WavesPerEu { static constexpr int v = NQ <= 3 ? 2 : 1; };
 
 // one workgroup = one wave = one problem at a time; workgroups pull jobs until none are left
 template <int NQ>
-__global__ __launch_bounds__(64) VBOC_WAVE_WPE void k_wave(Work w, Opts o, Inputs in, SlotState ss, WaveJobs jb) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WavesPerEu<NQ>::v, WavesPerEu<NQ>::v)))
+void k_wave(Work w, Opts o, Inputs in, SlotState ss, WaveJobs jb) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int t = (int)threadIdx.x;
   Coop<NQ> C(smem, gptr(jb.regions) + (long long)blockIdx.x * jb.region_doubles, w, o, t);

@@ -1239,7 +1239,6 @@ __global__ __launch_bounds__(256) VBOC_WPE void k_ls(Work w, Opts o, Inputs in, 
   else ss(IS_PH, L.slot) = 1;
 }
 
-#ifndef VBOC_ARM_TU
 __global__ void k_slots_init(int* ist, long long S) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= S) return;
@@ -1247,7 +1246,6 @@ __global__ void k_slots_init(int* ist, long long S) {
   ist[IS_PH * S + i] = 0;
   ist[IS_N * S + i] = 0;
 }
-#endif
 
 // -------------------------------------------------------------------------------------------------
 // twin integrator (SYM<sys>INIT.acados_integrator): one RK4 step of length T per problem
@@ -1293,35 +1291,8 @@ struct WaveJobs {
   long long region_doubles;
 };
 
-// The UR5 arm's wave solver lives in its own translation unit (wave_arm.hip, coop_arm.h, built at -O1):
-// its layout and launch, for the handle code below.
-namespace arm_api {
-size_t lds_bytes(int nmax);
-long long region_doubles(int nmax);
-long long hot_doubles();
-const void* kernel();
-hipError_t launch(dim3 grid, size_t lds, hipStream_t st, const Work& w, const Opts& o, const Inputs& in,
-                  const SlotState& ss, const WaveJobs& jb);
-}  // namespace arm_api
-
 }  // namespace vboc
 
-#ifdef VBOC_ARM_TU
-#include "coop_arm.h"
-namespace vboc {
-namespace arm_api {
-size_t lds_bytes(int nmax) { return arm::WaveLayout<4>::lds_bytes(nmax); }
-long long region_doubles(int nmax) { return (long long)arm::WaveLayout<4>::region_doubles(nmax); }
-long long hot_doubles() { return arm::WaveLayout<4>::OX; }
-const void* kernel() { return (const void*)arm::k_wave_ur5; }
-hipError_t launch(dim3 grid, size_t lds, hipStream_t st, const Work& w, const Opts& o, const Inputs& in,
-                  const SlotState& ss, const WaveJobs& jb) {
-  hipLaunchKernelGGL(arm::k_wave_ur5, grid, dim3(64), lds, st, w, o, in, ss, jb);
-  return hipGetLastError();
-}
-}  // namespace arm_api
-}  // namespace vboc
-#else
 #include "coop.h"
 #include "ft.h"
 
@@ -1489,7 +1460,7 @@ static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st) {
 // solves/s.  `wave_groups` overrides; `mall_mib` changes the budget.
 static long long wave_group_budget(const vboc_solver* h, int nmax) {
   const long long hot = (long long)(h->nq == 1 ? WaveLayout<1>::OX
-                                    : (h->nq == 2 ? WaveLayout<2>::OX : (h->nq == 3 ? WaveLayout<3>::OX : arm_api::hot_doubles()))) *
+                                    : (h->nq == 2 ? WaveLayout<2>::OX : (h->nq == 3 ? WaveLayout<3>::OX : WaveLayout<4>::OX))) *
                         (long long)(nmax + 1) * (long long)sizeof(double);
   const long long g = (long long)(0.92 * h->mall_mib * 1024.0 * 1024.0) / (hot > 0 ? hot : 1);
   return g < 256 ? 256 : g;
@@ -1506,7 +1477,7 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
     case 1: hipLaunchKernelGGL(k_wave<1>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
     case 2: hipLaunchKernelGGL(k_wave<2>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
     case 3: hipLaunchKernelGGL(k_wave<3>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
-    default: return arm_api::launch(grid, h->wave_lds, st, w, h->o, in, ss, jb);
+    default: hipLaunchKernelGGL(k_wave<4>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
   }
   return hipGetLastError();
 }
@@ -1549,18 +1520,17 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   }
   (void)hipEventCreate(&h->ev0);
   (void)hipEventCreate(&h->ev1);
-  // wave solver: one region of stage records per resident workgroup (occupancy x CUs); the UR5 arm's
-  // (nq = 4) comes from its own -O1 translation unit (wave_arm.hip)
+  // wave solver: one region of stage records per resident workgroup (occupancy x CUs)
   {
     const void* fn = nq == 1 ? (const void*)k_wave<1>
-                             : (nq == 2 ? (const void*)k_wave<2> : (nq == 3 ? (const void*)k_wave<3> : arm_api::kernel()));
+                             : (nq == 2 ? (const void*)k_wave<2> : (nq == 3 ? (const void*)k_wave<3> : (const void*)k_wave<4>));
     h->wave_lds = nq == 1 ? WaveLayout<1>::lds_bytes(nmax)
                           : (nq == 2 ? WaveLayout<2>::lds_bytes(nmax)
-                                     : (nq == 3 ? WaveLayout<3>::lds_bytes(nmax) : arm_api::lds_bytes(nmax)));
+                                     : (nq == 3 ? WaveLayout<3>::lds_bytes(nmax) : WaveLayout<4>::lds_bytes(nmax)));
     h->region_doubles = nq == 1 ? (long long)WaveLayout<1>::region_doubles(nmax)
                                 : (nq == 2 ? (long long)WaveLayout<2>::region_doubles(nmax)
                                            : (nq == 3 ? (long long)WaveLayout<3>::region_doubles(nmax)
-                                                      : arm_api::region_doubles(nmax)));
+                                                      : (long long)WaveLayout<4>::region_doubles(nmax)));
     int per_cu = 0, cus = 0;
     hipDeviceProp_t prop;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 64, h->wave_lds) == hipSuccess &&
@@ -1987,4 +1957,3 @@ int vboc_rk4_batch_host(int nq, int B, double T, const double* x, const double* 
 }
 
 }  // extern "C"
-#endif  // VBOC_ARM_TU

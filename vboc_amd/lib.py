@@ -39,23 +39,15 @@ class Batch(ctypes.Structure):
                 ("sqp_iter", ctypes.c_void_p), ("qp_iter", ctypes.c_void_p)]
 
 
-SRC_ARM = os.path.join(HERE, "csrc", "wave_arm.hip")
-
-
-def build(verbose=False):
-    """hipcc the solver for gfx950 into vboc_amd/libvboc_amd.so (in-tree): vboc_solver.hip at -O3 and the
-    UR5 arm's wave solver (wave_arm.hip) at -O1 as a second translation unit."""
-    import tempfile
-    base = ["hipcc", "--offload-arch=gfx950", "-std=c++17", "-fPIC"]
-    with tempfile.TemporaryDirectory() as tmp:
-        o_main, o_arm = os.path.join(tmp, "solver.o"), os.path.join(tmp, "wave_arm.o")
-        cmds = [base + ["-O3", "-c", SRC, "-o", o_main], base + ["-O1", "-c", SRC_ARM, "-o", o_arm],
-                base + ["-shared", o_main, o_arm, "-o", LIB_PATH]]
-        for cmd in cmds:
-            if verbose:
-                print(" ".join(cmd))
-            subprocess.check_call(cmd)
-    return LIB_PATH
+def build(verbose=False, extra_flags=(), out=None):
+    """hipcc the solver for gfx950 into vboc_amd/libvboc_amd.so (in-tree, -O3, one translation unit).
+    `extra_flags` / `out` build an instrumented variant next to it (e.g. -DVBOC_COOP_PROF)."""
+    out = out or LIB_PATH
+    cmd = ["hipcc", "--offload-arch=gfx950", "-std=c++17", "-fPIC", "-O3", "-shared", *extra_flags, SRC, "-o", out]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return out
 
 
 _lib = None
