@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--slots", type=int, default=65536)
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--factor", choices=("mfma", "valu"), default="mfma",
+                    help="wave solver's Riccati factorisation: FP64 MFMA (default, nq <= 3) or VALU dot-product steps")
     ap.add_argument("--mode", choices=("wave", "lane"), default="wave",
                     help="wave: one problem per wave (default); lane: lane-per-problem kernels + wave tail")
     args = ap.parse_args()
@@ -135,6 +137,7 @@ def main():
     nq, B = args.nq, args.batch
     solver = lib.Solver(nq, 100, slots=args.slots, device=local)
     solver.set_option("wave_all", 1 if args.mode == "wave" else 0)
+    solver.set_option("factor_mfma", 1 if args.factor == "mfma" else 0)
     solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
     stream = torch.cuda.current_stream(device)
 

@@ -28,6 +28,7 @@
 namespace vboc {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
+typedef double dbl4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) dbl2 gdbl2;
 typedef __attribute__((address_space(1))) void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
@@ -92,6 +93,15 @@ __device__ __forceinline__ double uni(double v) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b);
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// keep v in a VGPR (MFMA operands must not be folded to SGPRs / constants)
+__device__ __forceinline__ void vreg(double& v) { asm volatile("" : "+v"(v)); }
+// lane `lane` (wave-uniform constant) of v, as a uniform value
+__device__ __forceinline__ double rdlane(double v, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, lane);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), lane);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 __device__ __forceinline__ double wsum(double v) {
@@ -199,7 +209,7 @@ __device__ unsigned g_dbg_cnt;
 #define SPROF_FLUSH
 #endif
 
-template <int NQ>
+template <int NQ, bool FM = false>
 struct Coop {
   using L = WaveLayout<NQ>;
   using PF = Par<NQ>;
@@ -218,8 +228,11 @@ struct Coop {
   int N;
   double rs, rd0, e00, mu, nbox;   // interior-point scalars (wave-uniform)
 
+  unsigned lds0;    // LDS byte address of s[0] (wave-uniform), for the LDS-DMA's M0
+
   __device__ Coop(double* s_, gdouble* g_, const Work& w_, const Opts& o_, int t_)
-      : s(s_), g(g_), w(w_), o(o_), t(t_), N(0) {}
+      : s(s_), g(g_), w(w_), o(o_), t(t_), N(0),
+        lds0((unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(size_t)(lvoid*)s_)) {}
 
   // The lane index as a fresh opaque value: lane-derived addresses and descriptors are then recomputed
   // in each pass instead of being hoisted to the kernel prologue and held live across the whole job
@@ -242,8 +255,7 @@ struct Coop {
     const int nc = W / 2;
     const int c = part * 64 + t < nc ? part * 64 + t : nc - 1;
     const gdouble* src = g + (long long)k * REC + lo + 2 * c;
-    const unsigned lds = (unsigned)__builtin_amdgcn_readfirstlane(
-        (int)(unsigned)(size_t)(lvoid*)(s + dst + part * 128));
+    const unsigned lds = lds0 + 8u * (unsigned)(dst + part * 128);
     unsigned keep;
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
@@ -856,6 +868,190 @@ struct Coop {
     return ok;
   }
 
+  // The same factorisation of stages N-1..1 on FP64 MFMA (v_mfma_f64_16x16x4f64), pendulum chains only.
+  // With G_k = [A_k | B_k | rs e_k] (NX x (NX + NU + 1), padded to 16 columns), every stage is
+  //   PG = P G                                   (2 MFMAs: k = 0..7)
+  //   H  = G' [PG | Pi] + diag(Hx, Hu) + carry   (2 MFMAs)   = [A'PA+Hx A'PB A'Pe A'Pi; B'PA B'PB+Hu . B'Pi; ..]
+  //   Z  = L^-1 H_u, L = chol(Ru = H_uu)         (uniform 3x3 Cholesky, one column of Z per lane)
+  //   D  = H - Z' Z                              (1 MFMA, k = 0..3)
+  // so D holds P_k = A'PA + Hx - S'Ru^-1 S, Pi_k = A'Pi + K'Y, -Sc (Sc += Y'Ru^-1 Y) and LINE (+= rs e'Pi)
+  // in the accumulator layout (lane l, reg r <-> row (l >> 4) + 4r, column l & 15).  Because P is
+  // symmetric, accumulator register s of D is already the A operand of the next stage's P G for k-step s,
+  // and the Pi columns are already its B operand: the recursion stays in registers, one LDS read of the
+  // stage window per k-step, no LDS round trip between products.  K, M, chol(Ru), Y and P e go to the
+  // ring slot (written back by ring_wb as in factor()).  Stage 0 (controls s, u_0) runs factor()'s
+  // dot-product steps on P, Pi, Sc, LINE flushed to LDS.  Same algebra as factor(); the summation order
+  // inside an MFMA differs (rounding-level).
+  static constexpr int CE = NX + NU, CP = CE + 1;   // H row / G column of rs e; first Pi column
+  static constexpr bool MFMA_OK = (NX <= 8) && (CP + NQ <= 16) && (L::W_FAC + 2 * NX + 2 <= L::RSF);
+  // H_u rows NX .. NX+NU-1 live in accumulator registers HR0, HR0 + 1; the LDS image keeps those two
+  // registers of every lane group: image row (row & 3) + 4 * ((row >> 2) - HR0)
+  static constexpr int HR0 = NX >> 2;
+  static_assert(((NX + NU - 1) >> 2) <= HR0 + 1, "H_u spans two accumulator registers");
+  __device__ __forceinline__ static constexpr int hrow(int row) { return (row & 3) + 4 * ((row >> 2) - HR0); }
+  // The loop body is written for a low VALU count (the wave solver is VALU-issue bound): loop-invariant
+  // per-lane masks are FP64 0/1 multipliers (no lane-mask SGPRs to spill), H_u goes through an LDS image
+  // (no readlane / bpermute), and outputs a lane does not own land in the slot's junk tail [W_FAC, RSF)
+  // (never written back) instead of behind an exec mask.
+  __device__ __forceinline__ bool factor_mfma() {
+    static_assert(MFMA_OK, "stage blocks fit one 16x16 FP64 MFMA tile");
+    fresh();
+    const int c = t & 15, g = t >> 4;
+    constexpr int HS = L::XS;   // H_u image [8][16] (rows g and 4 + g of every lane group); XS is free here
+    // initial state: P_N = diag(D_N), Pi = E' (velocity selection), Sc = 0, LINE = 0
+    dbl4 Dm;
+    UNR for (int r = 0; r < 4; ++r) {
+      const int row = g + 4 * r;
+      double v = 0.0;
+      if (row < NX && c == row) v = st(N, OD + row);
+      if (row < NX && c >= CP && c < CP + NQ && row == NQ + (c - CP)) v = 1.0;
+      Dm[r] = v;
+    }
+    constexpr int P = L::P_FAC;
+    auto fdma = [&](int j) {
+      const int kk = N - 1 - j >= 0 ? N - 1 - j : 0;
+      UNR for (int part = 0; part < P; ++part) dma(kk, 0, L::W_FAC, fslot(j % L::NSF), part);
+    };
+    // loop-invariant per-lane constants
+    int goff[2];
+    double gm[2];
+    UNR for (int q = 0; q < 2; ++q) {
+      const int row = 4 * q + g;
+      int off = L::W_FAC;
+      double m = 0.0;
+      if (row < NX) {
+        if (c < NX) { off = OA + row * NX + c; m = 1.0; }
+        else if (c < CE) { off = OB + row * NU + (c - NX); m = 1.0; }
+        else if (c == CE) { off = OE + row; m = rs; }
+      }
+      goff[q] = off;
+      gm[q] = m;
+    }
+    const int hoff = c < CE ? OD + c : L::W_FAC;
+    double hm[4], cm[4];
+    UNR for (int r = 0; r < 4; ++r) {
+      const int row = g + 4 * r;
+      hm[r] = (c < CE && row == c) ? 1.0 : 0.0;
+      cm[r] = (c >= CP && c < CP + NQ && (row == CE || (row >= CP && row < CP + NQ))) ? 1.0 : 0.0;
+    }
+    const double pim = (c >= CP && c < CP + NQ) ? 1.0 : 0.0;
+    const bool zc = c < NX || (c >= CP && c < CP + NQ);
+    double zm[NU];
+    UNR for (int a = 0; a < NU; ++a) zm[a] = (zc && g == a) ? 1.0 : 0.0;
+    // output addresses (slot-relative; lanes without that output write the junk tail)
+    const int kofs = (g == 0 && c < NX) ? OK + c : L::W_FAC;
+    const int mofs = (g == 0 && c >= CP && c < CP + NQ) ? OM + (c - CP) : L::W_FAC;
+    const int pofs = (c == CE) ? OPE + g : L::W_FAC;
+    int yofs = L::W_FAC, ysrc = HS;
+    if (t < NU * NQ) {
+      const int a = t / NQ, jj = t % NQ, row = NX + a;
+      yofs = OY + t;
+      ysrc = HS + hrow(row) * 16 + CP + jj;
+    }
+    __syncthreads();   // before any DMA is in flight: this barrier's fence would drain them
+    settle();
+    fdma(0);
+    fdma(1);
+    bool ok = true;
+    for (int j = 0; j < N - 1; ++j) {
+      const int k = N - 1 - j, kb = fslot(j % L::NSF);
+      if (j >= 1) ring_wb<OK, OC>((j - 1) % L::NSF, k + 1);
+      fdma(j + 2);
+      if (j == 0) vmwait<2 * P>();
+      else if (j == 1) vmwait<2 * P + 1>();
+      else vmwait<2 * P + 2>();
+      dbg_check(kb, k, 0, L::W_FAC, 1);
+      double g0 = s[kb + goff[0]] * gm[0], g1 = s[kb + goff[1]] * gm[1];
+      const double hv = s[kb + hoff];
+      vreg(g0);
+      vreg(g1);
+      // P G (rows / columns of D beyond the stage blocks only meet zero rows of G)
+      double p0 = Dm[0], p1 = Dm[1];
+      vreg(p0);
+      vreg(p1);
+      dbl4 pg = {0.0, 0.0, 0.0, 0.0};
+      pg = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, g0, pg, 0, 0, 0);
+      pg = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, g1, pg, 0, 0, 0);
+      // H = G' [PG | Pi] + diag(Hx, Hu) + carried LINE / -Sc
+      dbl4 h;
+      UNR for (int r = 0; r < 4; ++r) h[r] = fma(Dm[r], cm[r], hv * hm[r]);
+      double b0 = fma(Dm[0], pim, pg[0]), b1 = fma(Dm[1], pim, pg[1]);
+      vreg(b0);
+      vreg(b1);
+      h = __builtin_amdgcn_mfma_f64_16x16x4f64(g0, b0, h, 0, 0, 0);
+      h = __builtin_amdgcn_mfma_f64_16x16x4f64(g1, b1, h, 0, 0, 0);
+      // H rows 4..11 -> LDS image; Ru (uniform) and this lane's column of H_u back
+      s[HS + g * 16 + c] = h[HR0];
+      if (HR0 + 1 < 4) s[HS + (4 + g) * 16 + c] = h[HR0 + 1 < 4 ? HR0 + 1 : 3];
+      double Lm[NU * NU], id[NU], hu[NU];
+      UNR for (int a = 0; a < NU; ++a) {
+        const int ia = hrow(NX + a);
+        UNR for (int b = 0; b <= a; ++b) {
+          const double v = s[HS + ia * 16 + NX + b];
+          Lm[a * NU + b] = v;
+          Lm[b * NU + a] = v;
+        }
+        hu[a] = s[HS + ia * 16 + c];
+      }
+      const bool okk = chol_inv<NU>(Lm, id);
+      ok = ok && okk;
+      double z[NU], zs = 0.0;
+      UNR for (int a = 0; a < NU; ++a) {
+        double tt = hu[a];
+        UNR for (int b = 0; b < a; ++b) tt -= Lm[a * NU + b] * z[b];
+        z[a] = tt * id[a];
+        zs = fma(z[a], zm[a], zs);
+      }
+      double nz = -zs;
+      vreg(zs);
+      vreg(nz);
+      Dm = __builtin_amdgcn_mfma_f64_16x16x4f64(nz, zs, h, 0, 0, 0);
+      // outputs of stage k into its ring slot: K = -Ru^-1 S, M = Ru^-1 Y, chol(Ru), Y, P e
+      double w[NU];
+      UNR for (int a = NU - 1; a >= 0; --a) {
+        double tt = z[a];
+        UNR for (int b = a + 1; b < NU; ++b) tt -= Lm[b * NU + a] * w[b];
+        w[a] = tt * id[a];
+      }
+      UNR for (int a = 0; a < NU; ++a) {
+        s[kb + kofs + a * NX] = -w[a];
+        s[kb + mofs + a * NQ] = w[a];
+      }
+      UNR for (int e = 0; e < NU * NU; ++e) s[kb + OLR + e] = Lm[e];
+      s[kb + yofs] = s[ysrc];
+      s[kb + pofs] = pg[0];
+      s[kb + pofs + 4] = pg[1];
+      lsync();
+    }
+    // flush P, Pi, Sc, LINE for stage 0 (factor()'s dot-product steps)
+    UNR for (int r = 0; r < 4; ++r) {
+      const int row = g + 4 * r;
+      if (row < NX && c < NX) s[L::P + row * NX + c] = Dm[r];
+      if (row < NX && c >= CP && c < CP + NQ) s[L::PI + row * NQ + (c - CP)] = Dm[r];
+      if (row >= CP && row < CP + NQ && c >= CP && c < CP + NQ) s[L::SC + (row - CP) * NQ + (c - CP)] = -Dm[r];
+      if (row == CE && c >= CP && c < CP + NQ) s[L::LINE + (c - CP)] = Dm[r];
+    }
+    lsync();
+    {
+      const int j = N - 1, kb = fslot(j % L::NSF);
+      if (j >= 1) ring_wb<OK, OC>((j - 1) % L::NSF, 1);
+      // stage 0's window was issued two sweeps ago (and the clamped repeats after it): retire all
+      vmwait<0>();
+      Dsc z1[RD], z2[RD], z4[RD];
+      desc_s0(z1, z2, z4);
+      dstep<NX, 0>(z1, kb);
+      dstep<NX, 0>(z2, kb);
+      int rb = L::ZERO, rstr = 0, db = L::TRASH + t, dstr = 0;
+      if (t < NQ) { rb = L::Y0 + t; rstr = NQ; db = L::MM0 + t; dstr = NQ; }
+      const bool ok0 = sstep<M0>(L::LR0, L::LR0, rb, rstr, db, dstr, 1.0);
+      ok = ok && ok0;
+      dstep<0, M0>(z4, kb);
+      lsync();
+    }
+    __syncthreads();   // write-back visible to the next sweep's ring loads
+    return ok;
+  }
+
   // closed-loop matrices A_cl = A + B K of stages 1..N-1 (row-major, OACL): formed once per
   // factorisation, stage-parallel, and shared by both vector passes (columns) and both forward
   // sweeps (rows) of the interior-point iteration
@@ -1417,7 +1613,9 @@ struct Coop {
         if (q != 1) { qst = q; break; }
         prep_pred();
         CPROF(2)
-        const bool okf = factor();
+        bool okf;
+        if constexpr (FM) okf = factor_mfma();
+        else okf = factor();
         acl_pass();
         CPROF(3)
         const bool okv = vec(ODA, w0, nun);
@@ -1481,12 +1679,13 @@ template <int NQ>
 struct WavesPerEu { static constexpr int v = NQ <= 3 ? 2 : 1; };
 
 // one workgroup = one wave = one problem at a time; workgroups pull jobs until none are left
-template <int NQ>
+// FM: the Riccati factorisation on FP64 MFMA (factor_mfma, NQ <= 3) instead of VALU dot-product steps
+template <int NQ, bool FM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WavesPerEu<NQ>::v, WavesPerEu<NQ>::v)))
 void k_wave(Work w, Opts o, Inputs in, SlotState ss, WaveJobs jb) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int t = (int)threadIdx.x;
-  Coop<NQ> C(smem, gptr(jb.regions) + (long long)blockIdx.x * jb.region_doubles, w, o, t);
+  Coop<NQ, FM> C(smem, gptr(jb.regions) + (long long)blockIdx.x * jb.region_doubles, w, o, t);
   for (;;) {
     unsigned idx = 0;
     if (t == 0) idx = atomicAdd(jb.next, 1u);

@@ -1339,6 +1339,7 @@ struct vboc_solver {
   int* list = nullptr;
   double coop_threshold = 8192;
   bool wave_all = true;
+  bool factor_mfma = true;          // wave solver's Riccati factorisation on FP64 MFMA (nq <= 3)
   double* regions = nullptr;
   long long n_regions = 0, region_doubles = 0, group_cap = 0;
   double mall_mib = 256.0;          // MALL budget for the resident problems' hot stage fields (0: off)
@@ -1474,10 +1475,19 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
   if (groups < 1) return hipSuccess;
   const dim3 grid((unsigned)groups), block(64);
   switch (h->nq) {
-    case 1: hipLaunchKernelGGL(k_wave<1>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
-    case 2: hipLaunchKernelGGL(k_wave<2>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
-    case 3: hipLaunchKernelGGL(k_wave<3>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
-    default: hipLaunchKernelGGL(k_wave<4>, grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
+    case 1:
+      if (h->factor_mfma) hipLaunchKernelGGL((k_wave<1, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      else hipLaunchKernelGGL((k_wave<1, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      break;
+    case 2:
+      if (h->factor_mfma) hipLaunchKernelGGL((k_wave<2, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      else hipLaunchKernelGGL((k_wave<2, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      break;
+    case 3:
+      if (h->factor_mfma) hipLaunchKernelGGL((k_wave<3, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      else hipLaunchKernelGGL((k_wave<3, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      break;
+    default: hipLaunchKernelGGL((k_wave<4, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
   }
   return hipGetLastError();
 }
@@ -1494,6 +1504,7 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   HIPCHK(hipSetDevice(device));
   vboc_solver* h = new vboc_solver();
   h->nq = nq; h->nmax = nmax; h->device = device;
+  h->factor_mfma = nq <= 3;
   default_opts(h->o);
   if (nq == 4) {
     h->o.lm = 1e-2;          // UR5 OCP: levenberg_marquardt = 1e-2 (VBOC/UR5/ur5reduced_class_fixedveldir.py:135)
@@ -1522,8 +1533,10 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   (void)hipEventCreate(&h->ev1);
   // wave solver: one region of stage records per resident workgroup (occupancy x CUs)
   {
-    const void* fn = nq == 1 ? (const void*)k_wave<1>
-                             : (nq == 2 ? (const void*)k_wave<2> : (nq == 3 ? (const void*)k_wave<3> : (const void*)k_wave<4>));
+    // occupancy of the VALU-factorisation instantiation; the MFMA one is held to the same register budget
+    const void* fn = nq == 1 ? (const void*)k_wave<1, false>
+                             : (nq == 2 ? (const void*)k_wave<2, false>
+                                        : (nq == 3 ? (const void*)k_wave<3, false> : (const void*)k_wave<4, false>));
     h->wave_lds = nq == 1 ? WaveLayout<1>::lds_bytes(nmax)
                           : (nq == 2 ? WaveLayout<2>::lds_bytes(nmax)
                                      : (nq == 3 ? WaveLayout<3>::lds_bytes(nmax) : WaveLayout<4>::lds_bytes(nmax)));
@@ -1613,6 +1626,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "wave_all") {
     h->wave_all = v != 0.0;
   }
+  else if (s == "factor_mfma") h->factor_mfma = v != 0.0 && h->nq <= 3;
   else if (s == "wave_groups") h->group_cap = (long long)v;
   else if (s == "mall_mib") h->mall_mib = v;
   else if (s == "profile_kernels") {
@@ -1648,6 +1662,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "coop_threshold") *v = h->coop_threshold;
   else if (s == "coop_available") *v = h->coop_ok ? 1.0 : 0.0;
   else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
+  else if (s == "factor_mfma") *v = h->factor_mfma ? 1.0 : 0.0;
   else if (s == "wave_groups") *v = (double)h->n_regions;
   else if (s == "mall_mib") *v = h->mall_mib;
   else if (s == "coop_problems") *v = (double)h->coop_count;
