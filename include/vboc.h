@@ -21,6 +21,10 @@
  *                             VBOC/triplependulum_class_vboc.py:235-239, VBOC/triplependulum_vboc.py:346-353
  *   vboc_solve_batch_ft    <- one OCPpendulum.OCP_solve(...) per problem (free-time OCP, dt a state):
  *                             VBOC/pendulum_class_vboc.py:107-130, called from VBOC/pendulum_vboc.py:94,181
+ *   vboc_data_generation   <- Pool(30).map(data_generation, range(P)): the whole per-problem boundary-sampling
+ *                             state machine of VBOC/triplependulum_vboc.py:19-370 (fan-out :399-405) /
+ *                             VBOC/doublependulum_vboc.py:19-403, with its OCP_solve calls (:110,262) and
+ *                             twin-integrator steps (:346-353), run on the device
  *   vboc_destroy           <- solver object destruction (acados_template __del__ -> free)
  *   vboc_last_error        <- Python exceptions raised by acados_template on bad fields
  *
@@ -139,6 +143,38 @@ int vboc_rk4_batch_host(int nq, int B, double T, const double* x, const double* 
  * x[B][2nq], u[B][nq] -> x_out[B][2nq], A[B][2nq][2nq] = dx_out/dx, Bm[B][2nq][nq] = dx_out/du. */
 int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const double* u, double* x_out, double* A,
                              double* Bm);
+
+/* Batched data generation ON THE DEVICE (nq = 2 or 3): for every problem id, the reference's
+ * `data_generation(v)` - IC sampling (Philox4x32-10 keyed by (seed, id), streams 0 and 2 of
+ * vboc_amd/ics.py), horizon extension (<= 10 solves, perturbed restarts), the sweep along the optimal
+ * trajectory with the twin RK4 steps and the verification solves (<= 5 per exit of the state box),
+ * the save filter.  One wave runs one problem's whole state machine with the wave solver in between
+ * (dg.h).  Device pointers except rows_used; synchronous (returns when every problem finished).
+ *   ids[B]              problem ids (int64)
+ *   q_min .. m2         system constants (vboc_amd/systems.py; the double's gravity guess uses g, l, m)
+ *   rows[rows_cap][2nq] saved samples, one contiguous block per problem (blocks in completion order)
+ *   row_off[B], row_cnt[B]  block of problem b; row_cnt -1 = the reference returns None
+ *   ic[B][4], ic_slot[B]    double pendulum store_ic and its tuple position (1 success, 2 failure);
+ *                       may be NULL for the triple
+ *   stats[B][5]         OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter
+ *   rows_used           OUT: rows written
+ * Requires N_start + 12 <= nmax of the handle. */
+typedef struct {
+  int B;
+  const long long* ids;
+  unsigned long long seed;
+  int N_start;
+  double q_min, q_max, v_max, u_max, dt, tol, eps, g, l1, l2, m1, m2;
+  double* rows;
+  long long rows_cap;
+  long long* row_off;
+  int* row_cnt;
+  double* ic;
+  int* ic_slot;
+  double* stats;
+  long long rows_used;
+} vboc_dg_batch_t;
+int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* batch, void* stream);
 
 /* Device time of the last vboc_solve_batch* call's solver kernel in milliseconds (HIP events on
  * the call's stream) and the number of kernel launches it used. */

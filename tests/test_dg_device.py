@@ -1,0 +1,104 @@
+"""The data-generation loop on the device (vboc_data_generation, vboc_amd/csrc/dg.h) against the batched
+host driver (vboc_amd.drivers.data_generation_batch).
+
+The host driver is the restatement pinned bit for bit against the reference's own `data_generation`
+(VBOC/triplependulum_vboc.py:19-370, VBOC/doublependulum_vboc.py:19-403; tests/test_drivers.py).  Run on
+the GPU backend it issues exactly the OCP solves and twin steps the device state machine issues, on the
+same wave solver, so the device loop must reproduce it: bit for bit for the triple; for the double
+pendulum the gravity-compensation guesses use the device's sin (the host driver uses glibc's math.sin),
+so a last-bit difference in a guess may propagate to rounding-level differences in the solutions.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _samples(nq, r):
+    s = r if nq == 3 else r[0]
+    return None if s is None else np.asarray(s, dtype=float)
+
+
+def _compare(nq, a_res, b_res, tol):
+    same, worst = 0, 0.0
+    for a, b in zip(a_res, b_res):
+        sa, sb = _samples(nq, a), _samples(nq, b)
+        if sa is None or sb is None:
+            ok = (sa is None) == (sb is None)
+        else:
+            ok = sa.shape == sb.shape and (sa.size == 0 or np.abs(sa - sb).max() <= tol)
+            if sa.shape == sb.shape and sa.size:
+                worst = max(worst, float(np.abs(sa - sb).max()))
+        if nq == 2 and ok:
+            for k in (1, 2):
+                if (a[k] is None) != (b[k] is None):
+                    ok = False
+                elif a[k] is not None:
+                    ok = ok and np.abs(np.asarray(a[k], float) - np.asarray(b[k], float)).max() <= tol
+        same += ok
+    return same, worst
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq", [3, 2])
+def test_device_loop_matches_host_driver(nq):
+    from vboc_amd import lib
+    from vboc_amd.drivers import GpuBackend, data_generation_batch, data_generation_device
+    ids = np.arange(1000, 1000 + (48 if nq == 3 else 64))
+    host, hst = data_generation_batch(nq, ids, GpuBackend(nq, nmax=120), N_start=100)
+    dev, dst = data_generation_device(nq, ids, lib.Solver(nq, 120), N_start=100)
+    assert dst["solves"] == hst["solves"] and dst["rk4"] == hst["rk4"], (dst, hst)
+    same, worst = _compare(nq, dev, host, 0.0 if nq == 3 else 1e-9)
+    print(f"nq {nq}: {same}/{len(ids)} problems identical, worst |diff| {worst:.2e}, solves {dst['solves']}, "
+          f"twin steps {dst['rk4']}")
+    assert same == len(ids) if nq == 3 else same >= 0.95 * len(ids), (same, len(ids))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq", [3, 2])
+def test_device_loop_matches_reference_fixture(nq):
+    """tests/golden/driver_{nq}.json: the reference's own data_generation on the CPU oracle.  The GPU
+    solver differs from the oracle at rounding level, which can flip a tolerance decision on a few
+    problems - the same bar as the host driver on the GPU (tests/test_drivers.py)."""
+    from vboc_amd import lib
+    from vboc_amd.drivers import data_generation_device
+    g = json.load(open(os.path.join(HERE, "golden", f"driver_{nq}.json")))
+    res, _ = data_generation_device(nq, np.array(g["ids"]), lib.Solver(nq, g["N_start"] + 20),
+                                    N_start=g["N_start"], seed=g["seed"])
+    same, _ = _compare(nq, res, g["results"], 1e-5)
+    assert same >= 0.8 * len(g["ids"]), (same, len(g["ids"]))
+
+
+@pytest.mark.gpu
+def test_device_loop_properties_at_scale():
+    """4096 triple problems: every saved row satisfies the save filter (:362-365) or is a quirk-A.3
+    duplicate of a state at the velocity box; statistics are consistent; a second run is identical."""
+    import torch
+    from vboc_amd import lib
+    from vboc_amd.systems import system
+    sysd = system(3)
+    s = lib.Solver(3, 120)
+    ids = torch.arange(50_000, 54_096, dtype=torch.int64, device="cuda:0")
+    a = s.data_generation_device(ids)
+    b = s.data_generation_device(ids)
+    cnt = a["row_cnt"].cpu().numpy()
+    st = a["stats"].cpu().numpy()
+    assert (cnt >= -1).all() and (cnt > 0).mean() > 0.9
+    assert (st[:, 0] >= 1).all() and (st[:, 0] <= 10 + 5 * 110).all()
+    assert int(cnt[cnt > 0].sum()) == a["rows"].shape[0]
+    # same rows per problem in both runs (completion order may differ)
+    for k in ("row_cnt", "stats"):
+        assert torch.equal(a[k], b[k])
+    ra, rb = a["rows"].cpu().numpy(), b["rows"].cpu().numpy()
+    oa, ob = a["row_off"].cpu().numpy(), b["row_off"].cpu().numpy()
+    for i in np.flatnonzero(cnt > 0)[::97]:
+        np.testing.assert_array_equal(ra[oa[i]:oa[i] + cnt[i]], rb[ob[i]:ob[i] + cnt[i]])
+    rows = ra
+    q, v = rows[:, :3], rows[:, 3:]
+    inside = ((q > sysd.q_min + sysd.eps) & (q < sysd.q_max - sysd.eps)).all(1) & (np.abs(v) > sysd.tol).all(1)
+    dup = (np.abs(v) <= sysd.v_max + 1e-9).all(1)
+    assert (inside | dup).all()
+    assert (np.abs(v) <= sysd.v_max + 1e-6).all() and (q >= sysd.q_min - 1e-6).all() and (q <= sysd.q_max + 1e-6).all()

@@ -1,0 +1,662 @@
+// dg.h - the VBOC data-generation loop ON THE DEVICE, fused with the wave solver.
+//
+// The reference runs `data_generation(v)` once per problem in a process pool
+// (VBOC/triplependulum_vboc.py:19-370, fan-out :399-405; double pendulum VBOC/doublependulum_vboc.py:19-403).
+// Each call is a sequential state machine: IC sampling, up to 10 horizon-extension OCP solves (with
+// perturbed restarts), then a sweep f = 1..N-1 along the optimal trajectory that either advances the
+// "unviable twin" by one RK4 step or, where the trajectory leaves the state box, runs up to 5
+// verification OCPs.  Here ONE WAVE RUNS ONE PROBLEM'S WHOLE STATE MACHINE: k_dg pulls problem ids
+// from a queue, and between the state machine's steps the same wave runs the wave solver (coop.h) on
+// the request it just wrote.  No host round trip, no per-round batching and no per-round tail: a wave
+// that finishes a problem pulls the next one, so the launch is bound by throughput plus ONE tail.
+//
+// The state machine is a restatement of vboc_amd/drivers.py::data_generation_problem (itself pinned bit
+// for bit against the reference's own function, tests/test_drivers.py) with the same arithmetic:
+//  * random draws: Philox4x32-10 keyed by (seed, problem id) - ics.uniforms stream 0 for the IC
+//    sampling, stream 2 for the perturbations, drawn in the reference's call order;
+//  * numpy.linalg.norm of a 2- or 3-vector = sqrt(x0*x0 (+) fma chain) (OpenBLAS ddot), reproduced
+//    with explicit fma; np.linspace(0, 1, n) = i * (1 / (n - 1)) with the last point 1.0;
+//  * every other expression is the Python scalar expression, evaluated left to right WITHOUT
+//    contraction (`#pragma clang fp contract(off)` in every function here);
+//  * the twin integrator is the same rk4<NQ> (model.h) as vboc_rk4_batch.
+// The state lives in a per-workgroup scratch record in HBM (not in registers across the solve, which
+// would push the wave kernel past its 256-VGPR budget); every lane executes the scalar logic
+// redundantly (uniform control flow), row copies are lane-parallel.
+#pragma once
+
+namespace vboc {
+
+struct DgJobs {
+  const long long* ids;        // problem ids (Philox keys), one per job
+  int count;
+  int N_start, nmax;
+  unsigned long long seed;
+  // system constants (vboc_amd/systems.py; VBOC/triplependulum_vboc.py:381-393)
+  double q_min, q_max, v_max, u_max, dt, tol, eps, g, l1, l2, m1, m2;
+  // per-workgroup arrays (the solver's single-problem inputs / outputs are an Inputs batch of one
+  // problem per workgroup, indexed by the workgroup: the kernel receives them as a kernel argument like
+  // k_wave, so the solver's pointers stay rematerialisable kernarg loads)
+  double* xs;                  // [groups][nmax + 1][nx]  x_sol
+  double* us;                  // [groups][nmax + 1][nu]  u_sol
+  double* vr;                  // [groups][vr_cap][2nq]   saved rows of the running problem
+  double* st;                  // [groups][st_doubles]    DgState
+  int vr_cap, st_doubles;
+  double* rows;                // [rows_cap][2nq] saved samples, one block per problem
+  long long rows_cap;
+  long long* row_off;          // [count]
+  int* row_cnt;                // [count]: number of rows, -1 = None, -2 = row pool overflow
+  double* ic;                  // [count][4] double pendulum store_ic (nullptr for the triple)
+  int* ic_slot;                // [count] 0: none, 1: tuple element 1 (success), 2: element 2 (failure)
+  double* stats;               // [count][DG_NSTAT]
+  unsigned* next;              // job counter
+  unsigned long long* rows_next;
+  unsigned* err;               // [0] pool overflow, [1] horizon > nmax
+  unsigned* done;
+};
+
+// per-problem statistics: OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter
+enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_NSTAT };
+
+template <int NQ>
+struct DgState {
+  int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, pad0, pad1;
+  double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
+  double sqp, nsqp, nqp;
+  double ran[2], store_ic[4], xsym[2 * NQ];
+};
+
+// ------------------------------------------------------------------------------------------------
+// Philox4x32-10 (Random123) and the 53-bit uniforms of vboc_amd/ics.py::uniforms
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox4x32_10(unsigned (&c)[4], unsigned k0, unsigned k1) {
+  UNR for (int r = 0; r < 10; ++r) {
+    const unsigned long long p0 = 0xD2511F53ull * c[0];
+    const unsigned long long p1 = 0xCD9E8D57ull * c[2];
+    const unsigned n0 = (unsigned)(p1 >> 32) ^ c[1] ^ k0;
+    const unsigned n2 = (unsigned)(p0 >> 32) ^ c[3] ^ k1;
+    c[1] = (unsigned)p1;
+    c[3] = (unsigned)p0;
+    c[0] = n0;
+    c[2] = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+// draw i of problem `id`'s stream (ics.uniforms(ids, n, seed, stream)[., i])
+__device__ __forceinline__ double philox_uniform(long long id, int i, unsigned long long seed, unsigned stream) {
+  unsigned c[4] = {(unsigned)(unsigned long long)id, (unsigned)((unsigned long long)id >> 32), (unsigned)(i >> 1),
+                   stream};
+  philox4x32_10(c, (unsigned)seed, (unsigned)(seed >> 32) ^ 0x5BD1E995u);
+  const unsigned a = (i & 1) ? c[2] : c[0], b = (i & 1) ? c[3] : c[1];
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+}
+
+// numpy.linalg.norm of a short float64 vector: sqrt(dot(x, x)), OpenBLAS ddot's FMA chain
+template <int n>
+__device__ __forceinline__ double np_norm(const double* v) {
+  double s = v[0] * v[0];
+  UNR for (int i = 1; i < n; ++i) s = fma(v[i], v[i], s);
+  return sqrt(s);
+}
+
+template <int NQ>
+struct Dg {
+  static constexpr int NX = 2 * NQ, NXR = NX + 1, NU = NQ, NP = NQ + 1;
+  static constexpr bool GRAV = NQ == 2;   // double pendulum: gravity-compensation guesses, 3-tuple result
+  enum : int { START = 0, HEXT = 1, VERIF = 2, SWEEP = 3, DONE = 4 };
+
+  const DgJobs& J;
+  const Inputs& in;  // the solver's batch: one problem per workgroup, this one at index wg
+  const int wg, t;
+  DgState<NQ>* s;
+  long long pid;
+  int job;
+
+  __device__ Dg(const DgJobs& J_, const Inputs& in_, int wg_, int t_) : J(J_), in(in_), wg(wg_), t(t_), pid(0), job(0) {
+    s = (DgState<NQ>*)(J.st + (long long)wg * J.st_doubles);
+  }
+
+  __device__ __forceinline__ long long row(int r) const { return (long long)wg * (J.nmax + 1) + r; }
+  __device__ __forceinline__ double* xg(int r) const { return (double*)in.xg + row(r) * NXR; }
+  __device__ __forceinline__ double* ug(int r) const { return (double*)in.ug + ((long long)wg * J.nmax + r) * NU; }
+  __device__ __forceinline__ const double* xo(int r) const { return in.xo + row(r) * NXR; }
+  __device__ __forceinline__ const double* uo(int r) const { return in.uo + ((long long)wg * J.nmax + r) * NU; }
+  __device__ __forceinline__ double* xs(int r) const { return J.xs + row(r) * NXR; }
+  __device__ __forceinline__ double* us(int r) const { return J.us + row(r) * NU; }
+  __device__ __forceinline__ double* pp() const { return (double*)in.p + (long long)wg * NP; }
+  __device__ __forceinline__ double* qlb0() const { return (double*)in.lbx0 + (long long)wg * NXR; }
+  __device__ __forceinline__ double* qub0() const { return (double*)in.ubx0 + (long long)wg * NXR; }
+  __device__ __forceinline__ double* vr(int n) const { return J.vr + ((long long)wg * J.vr_cap + n) * NX; }
+  __device__ __forceinline__ int status() const { return in.status[wg]; }
+  __device__ __forceinline__ int nreq() const { return in.N[wg]; }
+
+  // random.random() / random.choice([-1, 1]) of the problem's perturbation stream (ProblemRNG, stream 2)
+  __device__ __forceinline__ double rng_random() {
+    const int i = s->rng_pos;
+    s->rng_pos = i + 1;
+    return philox_uniform(pid, i, J.seed, 2u);
+  }
+  __device__ __forceinline__ static int choice_idx(double u, int n) {
+#pragma clang fp contract(off)
+    const int v = (int)(u * (double)n);
+    return v < n - 1 ? v : n - 1;
+  }
+  __device__ __forceinline__ double rng_pm1() { return choice_idx(rng_random(), 2) == 0 ? -1.0 : 1.0; }
+
+  // VBOC/doublependulum_vboc.py:84: u = [g l1 (m1 + m2) sin q1, g l2 m2 sin q2]
+  __device__ __forceinline__ void grav_u(const double* x, double* u) const {
+#pragma clang fp contract(off)
+    if constexpr (GRAV) {
+      u[0] = J.g * J.l1 * (J.m1 + J.m2) * sin(x[0]);
+      u[1] = J.g * J.l2 * J.m2 * sin(x[1]);
+    } else {
+      UNR for (int a = 0; a < NU; ++a) u[a] = 0.0;
+    }
+  }
+  __device__ __forceinline__ bool vel_out(const double* x) const {
+    bool r = false;
+    UNR for (int j = 0; j < NQ; ++j) r = r || x[NQ + j] > J.v_max || x[NQ + j] < -J.v_max;
+    return r;
+  }
+  __device__ __forceinline__ bool pos_at_limit(const double* x) const {
+#pragma clang fp contract(off)
+    bool r = false;
+    UNR for (int j = 0; j < NQ; ++j) r = r || x[j] > J.q_max - J.eps || x[j] < J.q_min + J.eps;
+    return r;
+  }
+
+  // straight-line guess over Nc rows (VBOC/triplependulum_vboc.py:85-93; qpos: positions of the others)
+  __device__ __forceinline__ void straight_guess(int Nc, const double* qpos) {
+#pragma clang fp contract(off)
+    const int js = s->joint_sel;
+    const double qi = s->q_init_sel, qf = s->q_fin_sel;
+    const double step = 1.0 / (double)(Nc - 1);
+    double q[NQ];
+    UNR for (int j = 0; j < NQ; ++j) q[j] = qpos[j];
+    for (int r = t; r <= Nc; r += 64) {
+      const int i = r < Nc ? r : Nc - 1;        // row Nc: the stage-N guess = the last row
+      const double tau = (i == Nc - 1) ? 1.0 : (double)i * step;
+      double x[NXR];
+      UNR for (int j = 0; j < NQ; ++j) { x[j] = q[j]; x[NQ + j] = 0.0; }
+      x[NX] = J.dt;
+      UNR for (int j = 0; j < NQ; ++j)
+        if (j == js) {
+          x[j] = (1.0 - tau) * qi + tau * qf;
+          x[NQ + j] = 2.0 * (1.0 - tau) * (qf - qi);
+        }
+      UNR for (int c = 0; c < NXR; ++c) xg(r)[c] = x[c];
+      if (r < Nc) {
+        double u[NU];
+        grav_u(x, u);
+        UNR for (int a = 0; a < NU; ++a) ug(r)[a] = u[a];
+      }
+    }
+  }
+
+  // x_guess[:n+1] = src_x[:n+1], u_guess[:n] = src_u[:n], u_guess[n] = gravity(x_guess[n]) | 0; then the
+  // horizon grows by one and the stage-(n+1) guess is the last row (x_guess[n + 1] = x_guess[n])
+  __device__ __forceinline__ void guess_from(const double* sx, const double* su, int n) {
+#pragma clang fp contract(off)
+    for (int r = t; r <= n + 1; r += 64) {
+      const int rr = r <= n ? r : n;
+      UNR for (int c = 0; c < NXR; ++c) xg(r)[c] = sx[(long long)rr * NXR + c];
+      if (r < n) {
+        UNR for (int a = 0; a < NU; ++a) ug(r)[a] = su[(long long)r * NU + a];
+      } else if (r == n) {
+        double u[NU];
+        grav_u(sx + (long long)n * NXR, u);
+        UNR for (int a = 0; a < NU; ++a) ug(r)[a] = u[a];
+      }
+    }
+  }
+
+  __device__ __forceinline__ void request(int N) {
+    if (N > J.nmax) {   // cannot happen for N_start + 12 <= nmax (checked on the host)
+      if (t == 0) atomicOr(J.err + 1, 1u);
+      N = J.nmax;
+    }
+    ((int*)in.N)[wg] = N;
+    s->solves += 1;
+  }
+
+  __device__ __forceinline__ void append(const double* x) {
+    const int n = s->nrows;
+    if (n < J.vr_cap) {
+      double* d = vr(n);
+      UNR for (int c = 0; c < NX; ++c) d[c] = x[c];
+    }
+    s->nrows = n + 1;
+  }
+
+  // ---- phase START: IC sampling (:32-83) and the first solve ----
+  __device__ __forceinline__ bool start(int job_) {
+#pragma clang fp contract(off)
+    job = job_;
+    pid = J.ids[job];
+    const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max, eps = J.eps;
+    s->phase = HEXT; s->N = J.N_start; s->ext = 0; s->f = 0; s->at_limit = 0; s->N_test = 0; s->ver = 0;
+    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0;
+    s->sqp = 0.0; s->nsqp = 0.0; s->nqp = 0.0; s->cost = 1e6;
+    int di = 0;
+    auto draw = [&]() { return philox_uniform(pid, di++, J.seed, 0u); };
+    const int js = choice_idx(draw(), NQ);
+    const int vs = choice_idx(draw(), 2) == 0 ? -1 : 1;
+    s->joint_sel = js;
+    s->vel_sel = vs;
+    const double qis = vs == -1 ? q_min : q_max, qfs = vs == -1 ? q_max : q_min;
+    s->q_init_sel = qis;
+    s->q_fin_sel = qfs;
+    double r[NQ];
+    r[0] = (double)vs * draw();
+    UNR for (int k = 1; k < NQ; ++k) {
+      const double sg = choice_idx(draw(), 2) == 0 ? -1.0 : 1.0;
+      r[k] = sg * draw();
+    }
+    const double nw = np_norm<NQ>(r);
+    double p[NP];
+    {
+      int c = 1;
+      UNR for (int j = 0; j < NQ; ++j) {
+        if (j == js) p[j] = r[0] / nw;
+        else { p[j] = r[c] / nw; ++c; }
+      }
+      p[NQ] = 0.0;
+    }
+    auto clamp_eps = [&](double v) {
+      if (v > q_max - eps) v = v - eps;
+      if (v < q_min + eps) v = v + eps;
+      return v;
+    };
+    double qpos[NQ];
+    if constexpr (GRAV) {
+      const double qo = clamp_eps(q_min + draw() * (q_max - q_min));
+      s->ran[0] = r[0]; s->ran[1] = r[1];
+      s->q_init_oth = qo;
+      s->store_ic[0] = (double)(vs + 1 + js); s->store_ic[1] = r[0]; s->store_ic[2] = r[1]; s->store_ic[3] = qo;
+      UNR for (int j = 0; j < NQ; ++j) qpos[j] = qo;
+    } else {
+      UNR for (int j = 0; j < NQ; ++j) qpos[j] = clamp_eps(q_min + draw() * (q_max - q_min));
+    }
+    const double sel0 = qis == q_min ? q_min + eps : q_max - eps;
+    double* P = pp();
+    double *lb0 = qlb0(), *ub0 = qub0();
+    UNR for (int j = 0; j < NP; ++j) P[j] = p[j];
+    UNR for (int j = 0; j < NQ; ++j) {
+      lb0[j] = j == js ? sel0 : qpos[j];
+      ub0[j] = j == js ? sel0 : qpos[j];
+      lb0[NQ + j] = v_min;
+      ub0[NQ + j] = v_max;
+    }
+    lb0[NX] = J.dt; ub0[NX] = J.dt;
+    // the bounds every OCP_solve of data_generation passes (:381-393)
+    double* lbx = (double*)in.lbx + (long long)wg * NXR; double* ubx = (double*)in.ubx + (long long)wg * NXR;
+    double* lbxe = (double*)in.lbxe + (long long)wg * NXR; double* ubxe = (double*)in.ubxe + (long long)wg * NXR;
+    double* lbu = (double*)in.lbu + (long long)wg * NU; double* ubu = (double*)in.ubu + (long long)wg * NU;
+    UNR for (int j = 0; j < NQ; ++j) {
+      lbx[j] = q_min; ubx[j] = q_max; lbx[NQ + j] = v_min; ubx[NQ + j] = v_max;
+      lbxe[j] = q_min; ubxe[j] = q_max; lbxe[NQ + j] = 0.0; ubxe[NQ + j] = 0.0;
+      lbu[j] = -J.u_max; ubu[j] = J.u_max;
+    }
+    lbx[NX] = J.dt; ubx[NX] = J.dt; lbxe[NX] = J.dt; ubxe[NX] = J.dt;
+    straight_guess(J.N_start, qpos);
+    request(J.N_start);
+    return true;
+  }
+
+  // the solve just finished: account it and run the state machine to its next request
+  __device__ __forceinline__ bool feed(int job_) {
+    job = job_;
+    pid = J.ids[job];
+    const int N = nreq();
+    const int it = in.sqp_iter[wg], qit = in.qp_iter[wg];
+    s->sqp += (double)it;
+    s->nsqp += (double)N * (double)it;
+    s->nqp += (double)N * (double)qit;
+    const bool more = s->phase == HEXT ? on_hext() : on_verif();
+    if (more) return true;
+    return s->phase == SWEEP ? sweep() : false;   // one inlined copy of the sweep (with its RK4)
+  }
+
+  // ---- horizon extension (:105-174) ----
+  __device__ __forceinline__ bool on_hext() {
+#pragma clang fp contract(off)
+    const int status = this->status();
+    const double q_min = J.q_min, q_max = J.q_max, eps = J.eps;
+    int N = s->N;
+    s->ext += 1;
+    if (status == 0) {
+      const double cost_new = in.cost[wg];
+      if (cost_new > s->cost - J.tol) {
+        sweep_init();
+        return false;
+      }
+      s->cost = cost_new;
+      guess_from(xo(0), uo(0), N);
+      N = N + 1;
+      s->N = N;
+    } else {
+      double* P = pp();
+      double *lb0 = qlb0(), *ub0 = qub0();
+      const int js = s->joint_sel;
+      if constexpr (GRAV) {
+        double r0 = s->ran[0], r1 = s->ran[1];
+        { const double a = rng_random(); const double c = rng_pm1(); r0 = r0 + a * c * 0.01; }
+        { const double a = rng_random(); const double c = rng_pm1(); r1 = r1 + a * c * 0.01; }
+        double rr[2] = {r0, r1};
+        const double nw = np_norm<2>(rr);
+        if (js == 0) { P[0] = r0 / nw; P[1] = r1 / nw; }
+        else { P[0] = r1 / nw; P[1] = r0 / nw; }
+        P[2] = 0.0;
+        double qo = s->q_init_oth;
+        { const double a = rng_random(); const double c = rng_pm1(); qo = qo + a * c * 0.01; }
+        if (qo > q_max - eps) qo = qo - eps;
+        if (qo < q_min + eps) qo = qo + eps;
+        const int jo = 1 - js;
+        lb0[jo] = qo; ub0[jo] = qo;
+        s->ran[0] = r0; s->ran[1] = r1; s->q_init_oth = qo;
+        s->store_ic[0] = (double)(s->vel_sel + 1 + js); s->store_ic[1] = r0; s->store_ic[2] = r1; s->store_ic[3] = qo;
+      } else {
+        double rans[NQ];
+        UNR for (int k = 0; k < NQ; ++k) {
+          const double a = rng_random();
+          const double c = rng_pm1();
+          rans[k] = P[k] + a * c * 0.01;
+        }
+        const double nw = np_norm<NQ>(rans);
+        UNR for (int k = 0; k < NQ; ++k) P[k] = rans[k] / nw;
+        P[NQ] = 0.0;
+        const double a = rng_random();
+        const double c = rng_pm1();
+        const double dev = a * c * 0.01;
+        UNR for (int j = 0; j < NQ; ++j) {
+          if (j != js) {
+            double val = lb0[j] + dev;
+            if (val > q_max - eps) val = val - eps;
+            if (val < q_min + eps) val = val + eps;
+            lb0[j] = val;
+            ub0[j] = val;
+          }
+        }
+      }
+      double qpos[NQ];
+      UNR for (int j = 0; j < NQ; ++j) qpos[j] = lb0[j];
+      __syncthreads();
+      straight_guess(N, qpos);
+      s->cost = 1e6;
+    }
+    if (s->ext >= 10) {     // all 10 solves used without an accepted horizon: None
+      s->fail = 1;
+      s->phase = DONE;
+      return false;
+    }
+    request(N);
+    return true;
+  }
+
+  // ---- sweep along the optimal trajectory (:177-365) ----
+  __device__ __forceinline__ void sweep_init() {
+#pragma clang fp contract(off)
+    const int N = s->N;
+    for (int r = t; r <= N; r += 64) {
+      UNR for (int c = 0; c < NXR; ++c) xs(r)[c] = xo(r)[c];
+      if (r < N) UNR for (int a = 0; a < NU; ++a) us(r)[a] = uo(r)[a];
+    }
+    __syncthreads();
+    append(xs(0));
+    double x[NX];
+    const double* P = pp();
+    UNR for (int c = 0; c < NX; ++c) x[c] = xs(0)[c];
+    UNR for (int j = 0; j < NQ; ++j) x[NQ + j] = x[NQ + j] - J.eps * P[j];
+    const bool lim = vel_out(x);
+    s->at_limit = lim ? 1 : 0;
+    if (!lim) UNR for (int c = 0; c < NX; ++c) s->xsym[c] = x[c];
+    s->f = 1;
+    s->phase = SWEEP;
+  }
+
+  // save filter of the sweep's step f (:362-365)
+  __device__ __forceinline__ void save_filter(int f) {
+#pragma clang fp contract(off)
+    const double* x = xs(f);
+    bool ok = true;
+    UNR for (int j = 0; j < NQ; ++j) ok = ok && (J.q_min + J.eps < x[j] && x[j] < J.q_max - J.eps);
+    UNR for (int j = 0; j < NQ; ++j) ok = ok && fabs(x[NQ + j]) > J.tol;
+    if (ok) append(x);
+  }
+
+  __device__ __forceinline__ bool sweep() {
+#pragma clang fp contract(off)
+    const int N = s->N;
+    const double eps = J.eps;
+    for (int f = s->f; f < N; ++f) {
+      if (s->at_limit) {
+        double x[NX];
+        UNR for (int c = 0; c < NX; ++c) x[c] = xs(f)[c];
+        const double nv = np_norm<NQ>(x + NQ);
+        UNR for (int j = 0; j < NQ; ++j) x[NQ + j] = x[NQ + j] + eps * x[NQ + j] / nv;
+        if (pos_at_limit(xs(f)) || vel_out(x)) {
+          s->at_limit = 1;
+        } else {
+          s->at_limit = 0;
+          if (pos_at_limit(xs(f - 1))) break;
+          // verification OCP from x_sol[f] (:245-339)
+          const int Nt = N - f;
+          const double nw = np_norm<NQ>(xs(f) + NQ);
+          double* P = pp();
+          double *lb0 = qlb0(), *ub0 = qub0();
+          UNR for (int j = 0; j < NQ; ++j) {
+            P[j] = -xs(f)[NQ + j] / nw;
+            lb0[j] = xs(f)[j]; ub0[j] = xs(f)[j];
+          }
+          P[NQ] = 0.0;
+          for (int r = t; r <= Nt; r += 64) {
+            const int src = r < Nt ? r + f : N;
+            UNR for (int c = 0; c < NXR; ++c) xg(r)[c] = xs(src)[c];
+            if (r < Nt) {
+              UNR for (int a = 0; a < NU; ++a) ug(r)[a] = us(r + f)[a];
+            } else {
+              double u[NU];
+              grav_u(xs(N), u);
+              UNR for (int a = 0; a < NU; ++a) ug(r)[a] = u[a];
+            }
+          }
+          s->norm_old = nw;
+          s->norm_bef = 0.0;
+          s->ver = 0;
+          s->N_test = Nt;
+          s->f = f;
+          s->phase = VERIF;
+          request(Nt);
+          return true;
+        }
+      } else {
+        double x1[NX], x0[NX], u0[NU];
+        UNR for (int c = 0; c < NX; ++c) x0[c] = s->xsym[c];
+        UNR for (int a = 0; a < NU; ++a) u0[a] = us(f - 1)[a];
+        rk4<NQ>(J.dt, x0, u0, x1);
+        s->rk4s += 1;
+        UNR for (int c = 0; c < NX; ++c) s->xsym[c] = x1[c];
+        bool lim = vel_out(x1);
+        UNR for (int j = 0; j < NQ; ++j) lim = lim || x1[j] > J.q_max || x1[j] < J.q_min;
+        s->at_limit = lim ? 1 : 0;
+      }
+      save_filter(f);
+    }
+    s->phase = DONE;
+    return false;
+  }
+
+  // ---- a verification solve finished (:289-339) ----
+  __device__ __forceinline__ bool on_verif() {
+#pragma clang fp contract(off)
+    const int status = this->status();
+    const int N = s->N, f = s->f;
+    const double eps = J.eps;
+    s->ver += 1;
+    bool ok_v = false;
+    if (status == 0) {
+      const double norm_new = np_norm<NQ>(xo(0) + NQ);
+      s->norm_new = norm_new;
+      if (norm_new < s->norm_bef + J.tol) {
+        ok_v = true;
+      } else {
+        s->norm_bef = norm_new;
+        const int Nt = s->N_test;
+        guess_from(xo(0), uo(0), Nt);
+        s->N_test = Nt + 1;
+        if (s->ver < 5) {
+          request(Nt + 1);
+          return true;
+        }
+      }
+    }
+    if (!ok_v) {
+      // unresolved: x_sol[f] appended once per later state at a velocity limit (quirk A.3, :333-337)
+      for (int r = f; r < N; ++r) {
+        bool hit = false;
+        UNR for (int j = 0; j < NQ; ++j) hit = hit || fabs(xs(r)[NQ + j]) > J.v_max - eps;
+        if (hit) append(xs(f));
+      }
+      s->phase = DONE;
+      return false;
+    }
+    const double norm_new = s->norm_new;
+    if (norm_new > s->norm_old + J.tol) {    // the state is inside V
+      for (int r = t; r < N - f; r += 64) {
+        UNR for (int c = 0; c < NXR; ++c) xs(r + f)[c] = xo(r)[c];
+        UNR for (int a = 0; a < NU; ++a) us(r + f)[a] = uo(r)[a];
+      }
+      __syncthreads();
+      double x[NX];
+      UNR for (int c = 0; c < NX; ++c) x[c] = xs(f)[c];
+      UNR for (int j = 0; j < NQ; ++j) x[NQ + j] = x[NQ + j] + eps * x[NQ + j] / norm_new;
+      if (vel_out(x)) {
+        s->at_limit = 1;
+      } else {
+        s->at_limit = 0;
+        UNR for (int c = 0; c < NX; ++c) s->xsym[c] = x[c];
+      }
+    } else {                                  // the state is on dV
+      s->at_limit = 0;
+      double x[NX];
+      const double* P = pp();
+      UNR for (int c = 0; c < NX; ++c) x[c] = xs(f)[c];
+      UNR for (int j = 0; j < NQ; ++j) x[NQ + j] = x[NQ + j] - eps * P[j];
+      const int jv = s->joint_sel + NQ;
+      UNR for (int c = NQ; c < NX; ++c)
+        if (c == jv) {
+          if (x[c] > J.v_max) x[c] = J.v_max;
+          if (x[c] < -J.v_max) x[c] = -J.v_max;
+        }
+      UNR for (int c = 0; c < NX; ++c) s->xsym[c] = x[c];
+    }
+    save_filter(f);
+    s->f = f + 1;
+    s->phase = SWEEP;
+    return false;
+  }
+
+  // ---- results: the problem's rows into the pool (reference order restored on the host) ----
+  __device__ __forceinline__ void finish(int job_) {
+    job = job_;
+    __syncthreads();
+    const int n = s->fail ? -1 : s->nrows;
+    long long off = 0;
+    int cnt = n;
+    if (n > J.vr_cap) {
+      cnt = -2;
+      if (t == 0) atomicOr(J.err, 1u);
+    } else if (n > 0) {
+      unsigned long long o = 0;
+      if (t == 0) o = atomicAdd(J.rows_next, (unsigned long long)n);
+      o = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(o >> 32)) << 32) |
+          (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)o);
+      if ((long long)o + n > J.rows_cap) {
+        cnt = -2;
+        if (t == 0) atomicOr(J.err, 1u);
+      } else {
+        off = (long long)o;
+        const double* src = vr(0);
+        for (int e = t; e < n * NX; e += 64) J.rows[off * NX + e] = src[e];
+      }
+    }
+    if (t == 0) {
+      J.row_off[job] = off;
+      J.row_cnt[job] = cnt;
+      if (J.ic) {
+        UNR for (int c = 0; c < 4; ++c) J.ic[(long long)job * 4 + c] = GRAV ? s->store_ic[c] : 0.0;
+        J.ic_slot[job] = GRAV ? (s->fail ? 2 : 1) : 0;
+      }
+      double* st = J.stats + (long long)job * DG_NSTAT;
+      st[DG_SOLVES] = (double)s->solves;
+      st[DG_RK4] = (double)s->rk4s;
+      st[DG_SQP] = s->sqp;
+      st[DG_NSQP] = s->nsqp;
+      st[DG_NQP] = s->nqp;
+      atomicAdd(J.done, 1u);
+    }
+  }
+};
+
+// The state machine's steps are inlined into the kernel.  Measured alternatives (hipcc -O3 resource
+// usage of k_dg<3, true>, against k_wave<3, true>: 256 VGPRs, 12 B scratch): the steps as noinline calls
+// 116-268 B of scratch with SGPR spills inside the solver's loops (a kernel with calls reserves SGPRs and
+// must keep values across calls in callee-saved registers); the per-workgroup problem addressed through
+// computed pointers instead of a kernel-argument Inputs batch 150-360 B.  Inlined with the kernarg batch:
+// 76 B, spilled at the job boundaries, not in the IPM loop.
+template <int NQ>
+__device__ __forceinline__ bool dg_start(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Dg<NQ> D(*J, *in, wg, t);
+  return D.start(job);
+}
+template <int NQ>
+__device__ __forceinline__ bool dg_feed(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Dg<NQ> D(*J, *in, wg, t);
+  return D.feed(job);
+}
+template <int NQ>
+__device__ __forceinline__ void dg_finish(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Dg<NQ> D(*J, *in, wg, t);
+  D.finish(job);
+}
+
+// one workgroup = one wave = one problem's whole data_generation at a time; `in` is the Inputs batch of
+// one problem per workgroup (the wave solver works on problem index wg of it, as k_wave on a pid), `inp`
+// a device copy of it for the state machine's calls
+template <int NQ, bool FM>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WavesPerEu<NQ>::v, WavesPerEu<NQ>::v)))
+void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJobs jb) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int t = (int)threadIdx.x;
+  const int wg = (int)blockIdx.x;
+  Coop<NQ, FM> C(smem, gptr(jb.regions) + (long long)wg * jb.region_doubles, w, o, t);
+  for (;;) {
+    unsigned idx = 0;
+    if (t == 0) idx = atomicAdd(jb.next, 1u);
+    idx = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl((int)idx, 0));
+    if (idx >= (unsigned)jb.count) break;
+    bool more = dg_start<NQ>(J, inp, wg, t, (int)idx);
+    while (more) {
+      __syncthreads();
+      int it = 0, qit = 0;
+      Lane<NQ> chk(w, o, 0u);
+      if (!chk.supported(in, wg)) {
+        if (t == 0) {
+          in.status[wg] = 5;
+          in.sqp_iter[wg] = 0;
+          in.qp_iter[wg] = 0;
+        }
+      } else {
+        C.from_inputs(in, wg);
+        const int status = C.run(it, qit);
+        C.store(in, wg, status, it, qit);
+      }
+      __syncthreads();
+      more = dg_feed<NQ>(J, inp, wg, t, (int)idx);
+    }
+    dg_finish<NQ>(J, inp, wg, t, (int)idx);
+    __syncthreads();
+  }
+}
+
+}  // namespace vboc

@@ -1295,6 +1295,7 @@ struct WaveJobs {
 
 #include "coop.h"
 #include "ft.h"
+#include "dg.h"
 
 // =================================================================================================
 // C ABI
@@ -1349,6 +1350,12 @@ struct vboc_solver {
   // free-time solver (ft.h): one problem per wave, per-workgroup stage-record regions
   double* ft_regions = nullptr;
   size_t ft_bytes = 0;
+  // device data generation (dg.h): per-workgroup state-machine records
+  double* dg_scratch = nullptr;
+  size_t dg_bytes = 0;
+  DgJobs* dg_jobs = nullptr;        // device copies of the job descriptor and of the per-workgroup batch
+  Inputs* dg_in = nullptr;
+  bool dg_attr[2] = {false, false};
 };
 
 static void default_opts(Opts& o) {
@@ -1492,6 +1499,26 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
   return hipGetLastError();
 }
 
+// the data-generation kernel (dg.h): one problem's whole state machine per wave, the wave solver inside
+template <int NQ, bool FM>
+static hipError_t launch_dg(vboc_solver* h, const DgJobs& J, const Inputs& in, long long groups, hipStream_t st) {
+  const void* fn = (const void*)k_dg<NQ, FM>;
+  bool& attr = h->dg_attr[FM ? 1 : 0];
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wave_lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  WaveJobs jb{nullptr, J.count, J.next, h->regions, h->region_doubles};
+  hipError_t e = hipMemcpyAsync(h->dg_jobs, &J, sizeof(DgJobs), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(h->dg_in, &in, sizeof(Inputs), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);   // J and in live on the host stack
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_dg<NQ, FM>), dim3((unsigned)groups), dim3(64), h->wave_lds, st, h->w, h->o, in,
+                     (const Inputs*)h->dg_in, (const DgJobs*)h->dg_jobs, jb);
+  return hipGetLastError();
+}
+
 extern "C" {
 
 const char* vboc_last_error(void) { return g_err.c_str(); }
@@ -1596,6 +1623,9 @@ int vboc_destroy(vboc_handle h) {
   if (h->host_done) (void)hipHostFree(h->host_done);
   if (h->stage) (void)hipFree(h->stage);
   if (h->ft_regions) (void)hipFree(h->ft_regions);
+  if (h->dg_scratch) (void)hipFree(h->dg_scratch);
+  if (h->dg_jobs) (void)hipFree(h->dg_jobs);
+  if (h->dg_in) (void)hipFree(h->dg_in);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   for (auto ev : h->pev) (void)hipEventDestroy(ev);
@@ -1905,6 +1935,92 @@ static int solve_host(vboc_handle h, const vboc_batch_t* b, bool ft) {
 
 int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, false); }
 int vboc_solve_batch_ft_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, true); }
+
+int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_data_generation: NULL argument");
+  if (h->nq != 2 && h->nq != 3)
+    return fail(VBOC_ERR_UNSUPPORTED, "vboc_data_generation: defined for the double (nq = 2) and triple (nq = 3) pendulum");
+  if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_data_generation: B < 0");
+  b->rows_used = 0;
+  if (b->B == 0) return VBOC_OK;
+  if (b->N_start < 2 || b->N_start + 12 > h->nmax)
+    return fail(VBOC_ERR_ARG, "vboc_data_generation: needs 2 <= N_start and N_start + 12 <= the handle's nmax "
+                              "(horizon extension +9, verification horizons up to N - 1 + 4)");
+  if (!b->ids || !b->rows || !b->row_off || !b->row_cnt || !b->stats || (h->nq == 2 && (!b->ic || !b->ic_slot)))
+    return fail(VBOC_ERR_ARG, "vboc_data_generation: NULL array");
+  if (!h->coop_ok) return fail(VBOC_ERR_HIP, "vboc_data_generation: wave solver unavailable on this device");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  long long groups = b->B < h->n_regions ? b->B : h->n_regions;
+  // resident problems: their hot stage records at the horizons data generation uses (N_start .. +12) fit the MALL
+  const long long cap = h->group_cap > 0 ? h->group_cap
+                                         : (h->mall_mib > 0 ? wave_group_budget(h, b->N_start + 10) : 0);
+  if (cap > 0 && groups > cap) groups = cap;
+  // per-workgroup arrays: the solver's one-problem batch (Inputs layout) + x_sol, u_sol, saved rows, state
+  const int nq = h->nq, NXR = 2 * nq + 1, NU = nq, NP = nq + 1, NX = 2 * nq, nm = h->nmax;
+  const int vr_cap = 2 * nm + 2;
+  const int st_d = (int)(((nq == 2 ? sizeof(DgState<2>) : sizeof(DgState<3>)) + 15) / 16 * 2);
+  const size_t G = (size_t)groups;
+  const size_t dbl = G * ((size_t)(nm + 1) * NXR * 3 + (size_t)nm * NU * 2 + (size_t)(nm + 1) * NU + NP + 6 * NXR +
+                          2 * NU + 1 + (size_t)vr_cap * NX + st_d) + 64;
+  const size_t need = dbl * sizeof(double) + 4 * G * sizeof(int) + 256;
+  if (need > h->dg_bytes) {
+    if (h->dg_scratch) (void)hipFree(h->dg_scratch);
+    h->dg_scratch = nullptr;
+    h->dg_bytes = 0;
+    if (hipMalloc((void**)&h->dg_scratch, need) != hipSuccess)
+      return fail(VBOC_ERR_NOMEM, "vboc_data_generation: hipMalloc of the state-machine records");
+    h->dg_bytes = need;
+  }
+  if (!h->dg_jobs && hipMalloc((void**)&h->dg_jobs, sizeof(DgJobs)) != hipSuccess)
+    return fail(VBOC_ERR_NOMEM, "vboc_data_generation: hipMalloc of the job descriptor");
+  if (!h->dg_in && hipMalloc((void**)&h->dg_in, sizeof(Inputs)) != hipSuccess)
+    return fail(VBOC_ERR_NOMEM, "vboc_data_generation: hipMalloc of the batch descriptor");
+  double* d = h->dg_scratch;
+  auto take = [&](size_t n) { double* r = d; d += (n + 1) & ~(size_t)1; return r; };
+  Inputs in;
+  in.B = (int)groups; in.nmax = nm; in.head = nullptr;
+  double* xg = take(G * (nm + 1) * NXR); double* ug = take(G * nm * NU); double* pp = take(G * NP);
+  double* lbx = take(G * NXR); double* ubx = take(G * NXR); double* lbu = take(G * NU); double* ubu = take(G * NU);
+  double* lbx0 = take(G * NXR); double* ubx0 = take(G * NXR); double* lbxe = take(G * NXR); double* ubxe = take(G * NXR);
+  in.xg = xg; in.ug = ug; in.p = pp; in.lbx = lbx; in.ubx = ubx; in.lbu = lbu; in.ubu = ubu;
+  in.lbx0 = lbx0; in.ubx0 = ubx0; in.lbxe = lbxe; in.ubxe = ubxe;
+  in.xo = take(G * (nm + 1) * NXR); in.uo = take(G * nm * NU); in.cost = take(G);
+  DgJobs J;
+  J.xs = take(G * (nm + 1) * NXR); J.us = take(G * (nm + 1) * NU); J.vr = take(G * vr_cap * NX);
+  J.st = take(G * st_d);
+  J.vr_cap = vr_cap; J.st_doubles = st_d;
+  int* ip = (int*)d;
+  in.N = ip; ip += G;
+  in.status = ip; ip += G;
+  in.sqp_iter = ip; ip += G;
+  in.qp_iter = ip; ip += G;
+  if ((size_t)((char*)ip - (char*)h->dg_scratch) > need) return fail(VBOC_ERR_ARG, "vboc_data_generation: internal size error");
+  J.ids = b->ids; J.count = b->B; J.N_start = b->N_start; J.nmax = nm; J.seed = b->seed;
+  J.q_min = b->q_min; J.q_max = b->q_max; J.v_max = b->v_max; J.u_max = b->u_max; J.dt = b->dt; J.tol = b->tol;
+  J.eps = b->eps; J.g = b->g; J.l1 = b->l1; J.l2 = b->l2; J.m1 = b->m1; J.m2 = b->m2;
+  J.rows = b->rows; J.rows_cap = b->rows_cap; J.row_off = b->row_off; J.row_cnt = b->row_cnt;
+  J.ic = h->nq == 2 ? b->ic : nullptr; J.ic_slot = h->nq == 2 ? b->ic_slot : nullptr; J.stats = b->stats;
+  // counters: [0] job queue, [1] finished problems, [2..3] error flags, [4..5] rows used (u64)
+  J.next = h->head; J.done = h->head + 1; J.err = h->head + 2; J.rows_next = (unsigned long long*)(h->head + 4);
+  HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
+  HIPCHK(hipEventRecord(h->ev0, st));
+  hipError_t e;
+  if (h->nq == 2) e = h->factor_mfma ? launch_dg<2, true>(h, J, in, groups, st) : launch_dg<2, false>(h, J, in, groups, st);
+  else e = h->factor_mfma ? launch_dg<3, true>(h, J, in, groups, st) : launch_dg<3, false>(h, J, in, groups, st);
+  if (e != hipSuccess) return fail(VBOC_ERR_HIP, std::string("vboc_data_generation: ") + hipGetErrorString(e));
+  HIPCHK(hipEventRecord(h->ev1, st));
+  h->launches = 1;
+  h->coop_count = b->B;
+  HIPCHK(hipMemcpyAsync(h->host_done + 4, h->head, 6 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const unsigned* c = h->host_done + 4;
+  b->rows_used = (long long)(((unsigned long long)c[5] << 32) | c[4]);
+  if (c[2]) return fail(VBOC_ERR_NOMEM, "vboc_data_generation: the row pool (rows_cap) overflowed");
+  if (c[3]) return fail(VBOC_ERR_HIP, "vboc_data_generation: a horizon exceeded nmax (internal error)");
+  if (c[1] != (unsigned)b->B) return fail(VBOC_ERR_HIP, "vboc_data_generation: not every problem finished");
+  return VBOC_OK;
+}
 
 int vboc_rk4_batch(int nq, int B, double T, const double* x, const double* u, double* x_out, void* stream) {
   if (nq < 1 || nq > 4 || B < 0) return fail(VBOC_ERR_ARG, "vboc_rk4_batch: bad nq/B");

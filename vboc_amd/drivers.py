@@ -540,6 +540,35 @@ def data_generation_batch(nq, ids, backend, N_start=None, seed=SEED):
     return run_problems(nq, gens, backend, nmax=getattr(backend, "nmax", 200))
 
 
+def data_generation_device(nq, ids, solver, N_start=None, seed=SEED):
+    """`data_generation(v)` for every problem id, with the WHOLE state machine on the GPU
+    (vboc_data_generation: one wave per problem runs the IC sampling, the horizon-extension and
+    verification solves and the twin steps of the sweep, dg.h).  Same return values as
+    `data_generation_batch` - results[i] is what the reference's call returns for ids[i] (triple: list of
+    samples or None; double: 3-tuple) - and stats (solves, rk4, sqp_iter totals).  `solver`: a
+    lib.Solver for nq with nmax >= N_start + 12."""
+    import torch
+    ids_t = torch.as_tensor(np.asarray(ids, dtype=np.int64), device=f"cuda:{solver.device}")
+    out = solver.data_generation_device(ids_t, N_start=N_start, seed=seed)
+    rows = out["rows"].cpu().numpy()
+    off, cnt = out["row_off"].cpu().numpy(), out["row_cnt"].cpu().numpy()
+    ic, slot = out["ic"].cpu().numpy(), out["ic_slot"].cpu().numpy()
+    st = out["stats"].cpu().numpy()
+    results = []
+    for b in range(len(cnt)):
+        if cnt[b] < -1:
+            raise RuntimeError(f"problem {ids[b]}: row pool overflow")
+        samples = None if cnt[b] < 0 else [r.tolist() for r in rows[off[b]:off[b] + cnt[b]]]
+        if nq == 2:
+            icb = [int(ic[b, 0])] + ic[b, 1:].tolist()
+            results.append((samples, icb, None) if slot[b] == 1 else (None, None, icb))
+        else:
+            results.append(samples)
+    stats = dict(solves=int(st[:, 0].sum()), rk4=int(st[:, 1].sum()), sqp_iter=int(st[:, 2].sum()), rounds=1,
+                 per_problem=st)
+    return results, stats
+
+
 def testing_batch(nq, ids, backend, N_start=None, seed=SEED, max_restarts=MAX_TEST_RESTARTS):
     """`testing(v)` for every problem id in `ids`, batched.  Returns (results, stats):
     results[i] is x_0[:2nq] of problem ids[i] (or None)."""

@@ -20,7 +20,7 @@ SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
            "vboc_solve_batch_host", "vboc_solve_batch_ft", "vboc_solve_batch_ft_host", "vboc_rk4_batch", "vboc_rk4_batch_host",
            "vboc_rk4_sens_batch_host", "vboc_last_kernel_ms",
-           "vboc_kernel_stats", "vboc_debug_counters", "vboc_last_error")
+           "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
 
@@ -37,6 +37,20 @@ class Batch(ctypes.Structure):
                 ("lbx_e", ctypes.c_void_p), ("ubx_e", ctypes.c_void_p), ("status", ctypes.c_void_p),
                 ("x_out", ctypes.c_void_p), ("u_out", ctypes.c_void_p), ("cost", ctypes.c_void_p),
                 ("sqp_iter", ctypes.c_void_p), ("qp_iter", ctypes.c_void_p)]
+
+
+class DgBatch(ctypes.Structure):
+    """vboc_dg_batch_t (include/vboc.h): the device data-generation call."""
+    _fields_ = [("B", ctypes.c_int), ("ids", ctypes.c_void_p), ("seed", ctypes.c_ulonglong),
+                ("N_start", ctypes.c_int)] + \
+               [(n, ctypes.c_double) for n in ("q_min", "q_max", "v_max", "u_max", "dt", "tol", "eps", "g", "l1", "l2",
+                                              "m1", "m2")] + \
+               [("rows", ctypes.c_void_p), ("rows_cap", ctypes.c_longlong), ("row_off", ctypes.c_void_p),
+                ("row_cnt", ctypes.c_void_p), ("ic", ctypes.c_void_p), ("ic_slot", ctypes.c_void_p),
+                ("stats", ctypes.c_void_p), ("rows_used", ctypes.c_longlong)]
+
+
+DG_STATS = ("solves", "rk4", "sqp_iter", "n_sqp_iter", "n_qp_iter")   # per problem (vboc_dg_batch_t.stats)
 
 
 def build(verbose=False, extra_flags=(), out=None):
@@ -80,6 +94,7 @@ def load():
     lib.vboc_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_int)]
     lib.vboc_debug_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    lib.vboc_data_generation.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_void_p]
     lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
@@ -176,6 +191,40 @@ class Solver:
         st = stream if stream is not None else torch.cuda.current_stream()
         fn = self.lib.vboc_solve_batch_ft if free_time else self.lib.vboc_solve_batch
         _check(fn(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        return out
+
+    # -- device data generation (the whole data_generation state machine per problem on the GPU) ----
+    def data_generation_device(self, ids, N_start=None, seed=None, rows_cap=None, stream=None):
+        """`data_generation(v)` for every problem id of the int64 cuda tensor `ids` (vboc_data_generation,
+        dg.h).  Returns a dict of device tensors: rows [rows_used, 2nq] (blocks per problem), row_off,
+        row_cnt (-1: None), ic / ic_slot (double pendulum), stats [B, 5] (DG_STATS)."""
+        import torch
+        from .ics import SEED
+        from .systems import system
+        sysd = system(self.nq)
+        N_start = int(N_start or sysd.N)
+        seed = SEED if seed is None else int(seed)
+        assert ids.is_cuda and ids.dtype == torch.int64 and ids.is_contiguous()
+        B = ids.shape[0]
+        dev = ids.device
+        nx = 2 * self.nq
+        if rows_cap is None:
+            rows_cap = B * (2 * (N_start + 12) + 2)   # a problem saves at most 2N rows (quirk A.3 included)
+        rows = torch.empty((max(rows_cap, 1), nx), dtype=torch.float64, device=dev)
+        out = dict(row_off=torch.empty(B, dtype=torch.int64, device=dev), row_cnt=torch.empty(B, dtype=torch.int32, device=dev),
+                   ic=torch.zeros((B, 4), dtype=torch.float64, device=dev), ic_slot=torch.zeros(B, dtype=torch.int32, device=dev),
+                   stats=torch.empty((B, len(DG_STATS)), dtype=torch.float64, device=dev))
+        m = (list(sysd.m) + [0.0, 0.0])[:2]
+        l = (list(sysd.l) + [0.0, 0.0])[:2]
+        b = DgBatch(B=B, ids=ids.data_ptr(), seed=seed, N_start=N_start, q_min=sysd.q_min, q_max=sysd.q_max,
+                    v_max=sysd.v_max, u_max=sysd.u_max, dt=sysd.dt, tol=sysd.tol, eps=sysd.eps, g=sysd.g,
+                    l1=l[0], l2=l[1], m1=m[0], m2=m[1], rows=rows.data_ptr(), rows_cap=rows_cap,
+                    row_off=out["row_off"].data_ptr(), row_cnt=out["row_cnt"].data_ptr(), ic=out["ic"].data_ptr(),
+                    ic_slot=out["ic_slot"].data_ptr(), stats=out["stats"].data_ptr(), rows_used=0)
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        _check(self.lib.vboc_data_generation(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        out["rows"] = rows[:b.rows_used]
+        out["rows_all"] = rows
         return out
 
     def kernel_stats(self):
