@@ -1,21 +1,36 @@
 """VBOC boundary OCP solves/sec - triple pendulum, 1..8 MI355X (BASELINE.json metric).
 
-One step = one batched solve of B boundary OCPs (the first solve of `data_generation`,
-VBOC/triplependulum_vboc.py:32-110: IC law, straight-line guess, N = 100) on each GPU, inputs
-already resident in HBM, followed (N > 1) by the RCCL all-gather of the boundary states x0 that
-feeds the NN fit (configs[3]).  Problem ids are a global counter (Philox per id), so rank r solves
-ids [(step * world + r) * B, ... + B): per-GPU work is fixed as N grows (weak scaling).
+Workloads (--workload):
+  dg-loop      (default) one step = the reference's data-generation loop over B problems per GPU:
+               `data_generation(v)` of VBOC/triplependulum_vboc.py:19-370 for every problem id, i.e. IC
+               sampling, up to 10 horizon-extension solves, the sweep with its twin RK4 steps and the
+               verification solves, the save filter - the whole state machine on the device, one problem
+               per wave with the wave solver in between (vboc_data_generation, vboc_amd/csrc/dg.h) - then
+               X_save in problem order and (N > 1) the RCCL all-gather of every rank's samples that feeds
+               the NN fit.  value = OCP solves (all of them) / s; also boundary problems / s.
+               The W warmup steps and the K timed steps are each issued as ONE persistent launch over their
+               W*B / K*B problems: a launch is bound by throughput plus its single slowest problem (the
+               critical problem, reported under loop.tail), which a launch per step would pay K times.
+               Default B = 20k (the driver's 5 + 20 steps then cover configs[2]'s 100k states five times).
+  first-solve  one step = the first OCP solve of data_generation for B problems (IC law, straight-line
+               guess, N = 100) on the wave solver, inputs resident in HBM, then (N > 1) the all-gather of
+               the boundary states x0.
+Problem ids are a global counter (Philox per id): rank r takes ids [(step * world + r) * B, ... + B), so
+per-GPU work is fixed as N grows (weak scaling).
 
 Output: ONE JSON line on rank 0 (contract in the task statement), with
-  roofline     the dominant kernel.  Default (wave mode) k_wave, the whole solve in one launch per
-               step: algorithmic FP64 work of the launch by the SURVEY 8(d) convention / its duration
-               (HIP events on the solve stream, vboc_last_kernel_ms); bound "mfma" = the FP64 dense
-               peak (78.6 TFLOP/s; vector and matrix are equal on MI355X).  --mode lane: the lane-mode
-               dominant kernel k_qp_factor, algorithmic bytes / duration (vboc_kernel_stats), bound "hbm".
-               traffic: HBM bytes per launch from the committed rocprofv3 PMC passes (FETCH_SIZE x2 +
-               WRITE_SIZE, profiles/*_pmc_<kernel>.json).
-  cpu_baseline the oracle's C restatement (oracle/, test infrastructure) on a bounded sample of the
-               same workload on the host's cores, rank 0, N = 1 only.
+  roofline     the dominant kernel (k_dg / k_wave: the whole step is one launch): algorithmic FP64 flops of
+               the launch by the SURVEY 8(d) convention with the solver's reported iteration counts, over
+               its duration (HIP events on the solve stream, vboc_last_kernel_ms), priced against the FP64
+               dense peak (78.6 TFLOP/s; the Riccati factorisation runs on v_mfma_f64_16x16x4f64, the rest
+               on the FP64 VALU at the same peak).  traffic: memory-side bytes per launch from the committed
+               rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, profiles/*_pmc_<kernel>.json).
+  tail         the launch's critical problem (longest single problem on one wave), when the job queue
+               drained and when the last problem finished (device real-time clock; dg-loop).
+  cpu_baseline the oracle's C restatement (oracle/, test infrastructure) on a bounded sample of the same
+               workload on the host's cores, rank 0, N = 1 only.
+`run(args, engine_factory)` takes another engine (tests/test_distributed.py runs the N = 2 path on gloo with
+the oracle as the engine).
 """
 import argparse
 import json
@@ -29,28 +44,41 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
-FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 dense peak, vector and matrix
 # SURVEY.md 8(d) algorithmic FLOP convention (triple n=7, m=3; double n=5, m=2; pendulum n=3, m=1)
 F_DYN = {3: 6382, 2: 2146, 1: 4 * 14 + 8 * 9 * 4 + 8 * 3 * 4 + 6}
 F_IPM = {3: 3513, 2: 1346, 1: int(2 * 9 * 4 + 2 * 3 * 16 + 64 / 3 + 8 * 16)}
 C_F = {3: 183, 2: 52, 1: 8}
-# UR5 arm (config 5, n = 8, m = 4): same convention; C_f / C_fJ are the sympy CSE op counts of the
-# urdf2casadi-style ABA restatement (oracle/ur5_rbd.py, tools/ur5_flops.py -> tests/golden/flops.json "4")
-_UR5_CF, _UR5_CFJ = None, None
 
 
 def _ur5_counts():
-    import json as _j
-    d = _j.load(open(os.path.join(ROOT, "tests", "golden", "flops.json"))).get("4")
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "flops.json"))).get("4")
     return (d["C_f"], d["C_fJ"]) if d else (None, None)
 
 
+# UR5 arm (config 5, n = 8, m = 4): same convention; C_f / C_fJ are the sympy CSE op counts of the
+# urdf2casadi-style ABA restatement (oracle/ur5_rbd.py, tools/ur5_flops.py -> tests/golden/flops.json "4")
 _UR5_CF, _UR5_CFJ = _ur5_counts()
 if _UR5_CF:
     _n, _m = 8, 4
     F_DYN[4] = 4 * _UR5_CFJ + 8 * _n * _n * (_n + _m) + 8 * _n * (_n + _m) + 2 * _n
     F_IPM[4] = int(2 * _n * _n * (_n + _m) + 2 * _n * (_n + _m) ** 2 + (_n + _m) ** 3 / 3 + 8 * (_n + _m) ** 2)
     C_F[4] = _UR5_CF
+
+NAMES = {1: "pendulum", 2: "double pendulum", 3: "triple pendulum", 4: "UR5 arm"}
+WORKLOAD = {
+    ("dg-loop", 3): "triple-pendulum data_generation loop (VBOC/triplependulum_vboc.py:19-370), {B} problems per GPU "
+                    "per step: every OCP solve (horizon extension + verification) and twin step on the device "
+                    "(configs[2]; configs[3] at 8 GPUs)",
+    ("dg-loop", 2): "double-pendulum data_generation loop (VBOC/doublependulum_vboc.py:19-403), {B} problems per GPU "
+                    "per step (configs[1])",
+    ("first-solve", 3): "triple-pendulum data_generation first OCP solve, N=100, {B} ICs per GPU per step "
+                        "(configs[2]; configs[3] at 8 GPUs)",
+    ("first-solve", 2): "double-pendulum data_generation first OCP solve, N=100, {B} ICs per GPU per step (configs[1])",
+    ("first-solve", 1): "pendulum data_generation first OCP solve, N=50, {B} ICs per GPU per step",
+    ("first-solve", 4): "UR5 (4 revolute joints of ur5.urdf) testing_test first OCP solve, N=100, {B} ICs per GPU "
+                        "per step (configs[4]: 100k states; 8 GPUs at N=8)",
+}
 
 
 def pmc_traffic(kernel):
@@ -65,206 +93,320 @@ def pmc_traffic(kernel):
     return d["traffic_bytes_per_launch"] / 1e9, os.path.relpath(files[-1], ROOT)
 
 
+def dg_flops(nq, stats):
+    """SURVEY 8(d) FP64 flops of a data-generation launch from its per-problem stats (lib.DG_STATS):
+    sum over solves of N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp), plus 4*C_f per twin step."""
+    return float(np.sum((F_DYN[nq] + 8 * C_F[nq]) * stats[:, 3] + F_IPM[nq] * stats[:, 4] + 4 * C_F[nq] * stats[:, 1]))
+
+
 def make_batch(nq, ids, device):
     import torch
     from vboc_amd.ics import data_generation_ics, ur5_ics
     b = ur5_ics(ids) if nq == 4 else data_generation_ics(nq, ids)
     keys = ("N", "x_guess", "u_guess", "p", "lbx", "ubx", "lbu", "ubu", "lbx0", "ubx0", "lbxe", "ubxe")
-    return {k: torch.as_tensor(np.ascontiguousarray(b[k]), device=device) for k in keys}, b
+    return {k: torch.as_tensor(np.ascontiguousarray(b[k]), device=device) for k in keys}
 
 
-def cpu_baseline(nq, B, seconds, threads):
-    """Oracle (CPU FP64 restatement) on the first problems of the workload for ~`seconds`."""
+def order_rows(out):
+    """X_save in problem order (VBOC/triplependulum_vboc.py:404-405 flattens the results in problem order)
+    from the device blocks (one contiguous block per problem, in completion order), on the device."""
+    import torch
+    cnt = out["row_cnt"].clamp(min=0).to(torch.int64)
+    off = out["row_off"]
+    tot = int(cnt.sum())
+    start = torch.cumsum(cnt, 0) - cnt
+    idx = torch.repeat_interleave(off, cnt) + torch.arange(tot, device=cnt.device) - torch.repeat_interleave(start, cnt)
+    return out["rows_all"][idx]
+
+
+class GpuEngine:
+    """The product path: libvboc_amd on one GPU (HIP kernels; no CPU fallback)."""
+
+    def __init__(self, nq, args, local):
+        import torch
+        from vboc_amd import lib
+        self.torch, self.lib = torch, lib
+        self.device = torch.device("cuda", local)
+        torch.cuda.set_device(self.device)
+        nmax = 100 + 20 if args.workload == "dg-loop" else 100
+        self.solver = lib.Solver(nq, nmax, slots=args.slots, device=local)
+        self.solver.set_option("wave_all", 1 if args.mode == "wave" else 0)
+        self.solver.set_option("factor_mfma", 1 if args.factor == "mfma" else 0)
+        self.solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
+        self.stream = torch.cuda.current_stream(self.device)
+        self.kernel = {("dg-loop", "wave"): f"k_dg<{nq}>", ("first-solve", "wave"): f"k_wave<{nq}>",
+                       ("first-solve", "lane"): f"k_qp_factor<{nq}>"}[(args.workload, args.mode)]
+
+    def sync(self):
+        self.torch.cuda.synchronize(self.device)
+
+    def first_solve_batch(self, nq, ids):
+        return make_batch(nq, ids, self.device)
+
+    def first_solve(self, tb):
+        out = self.solver.solve_device(tb, stream=self.stream)
+        return dict(x0=out["x"][:, 0, :], status=out["status"], sqp_iter=out["sqp_iter"], qp_iter=out["qp_iter"])
+
+    def dg(self, ids):
+        ids_t = self.torch.as_tensor(ids, dtype=self.torch.int64, device=self.device)
+        return self.solver.data_generation_device(ids_t, stream=self.stream)
+
+    def kernel_ms(self):
+        return self.solver.last_kernel_ms()[0]
+
+    def lane_stats(self):
+        return self.solver.kernel_stats()
+
+
+def cpu_baseline(nq, workload, B, seconds, threads):
+    """Oracle (CPU FP64 restatement, oracle/) on the first problems of the same workload for ~`seconds`:
+    first-solve - batches of first solves, one problem per OpenMP thread; dg-loop - the batched
+    data_generation driver (vboc_amd.drivers, the restatement pinned against the reference's own
+    function) with the oracle as its solver and twin integrator."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from vboc_amd.ics import data_generation_ics, ur5_ics
-    done, t_total, n = 0, 0.0, max(threads, 8)
-    start = 0
+    done, solves, t_total, start = 0, 0, 0.0, 0
+    n = max(threads, 8)
     while t_total < seconds and start < B:
-        b = ur5_ics(np.arange(start, start + n)) if nq == 4 else data_generation_ics(nq, np.arange(start, start + n))
+        ids = np.arange(start, start + n)
         t0 = time.time()
-        oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
-                           b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], nthreads=threads)
+        if workload == "dg-loop":
+            from vboc_amd.drivers import data_generation_batch
+            _, st = data_generation_batch(nq, ids, oracle.DriverBackend(nq, threads))
+            solves += st["solves"]
+        else:
+            b = ur5_ics(ids) if nq == 4 else data_generation_ics(nq, ids)
+            oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                               b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], nthreads=threads)
+            solves += n
         t_total += time.time() - t0
         done += n
         start += n
-        n = min(4 * n, max(threads, 8) * 64)
-    return done / t_total, done, t_total
+        n = min(4 * n, max(threads, 8) * (16 if workload == "dg-loop" else 64))
+    return solves / t_total, done, solves, t_total
 
 
-NAMES = {1: "pendulum", 2: "double pendulum", 3: "triple pendulum", 4: "UR5 arm"}
-WORKLOAD = {
-    3: "triple-pendulum data_generation first OCP solve, N=100, {B} ICs per GPU per step (configs[2]; configs[3] "
-       "at 8 GPUs)",
-    2: "double-pendulum data_generation first OCP solve, N=100, {B} ICs per GPU per step (configs[1])",
-    1: "pendulum data_generation first OCP solve, N=50, {B} ICs per GPU per step",
-    4: "UR5 (4 revolute joints of ur5.urdf) testing_test first OCP solve, N=100, {B} ICs per GPU per step "
-       "(configs[4]: 100k states; 8 GPUs at N=8)",
-}
-
-
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=100_000, help="problems per GPU per step (configs[2]: 100k)")
+    ap.add_argument("--workload", choices=("dg-loop", "first-solve"), default="dg-loop")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="problems per GPU per step; default 20k for dg-loop (configs[2]'s 100k states every five "
+                         "steps), 100k for first-solve")
     ap.add_argument("--nq", type=int, default=3,
                     help="3: triple pendulum (BASELINE metric); 2 / 1: double / pendulum; 4: UR5 arm (configs[4])")
     ap.add_argument("--slots", type=int, default=65536)
+    ap.add_argument("--max-batches", type=int, default=4,
+                    help="first-solve: distinct input batches held in HBM (steps cycle through them)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--factor", choices=("mfma", "valu"), default="mfma",
                     help="wave solver's Riccati factorisation: FP64 MFMA (default, nq <= 3) or VALU dot-product steps")
     ap.add_argument("--mode", choices=("wave", "lane"), default="wave",
-                    help="wave: one problem per wave (default); lane: lane-per-problem kernels + wave tail")
-    args = ap.parse_args()
+                    help="first-solve: wave (one problem per wave, default) or lane (lane-per-problem kernels)")
+    args = ap.parse_args(argv)
+    if args.batch is None:
+        args.batch = 20_000 if args.workload == "dg-loop" else 100_000
+    if args.workload == "dg-loop" and (args.nq not in (2, 3) or args.mode != "wave"):
+        ap.error("--workload dg-loop runs the double / triple pendulum on the wave solver")
+    return args
 
+
+def run(args, engine_factory=None):
+    """Run the benchmark; returns the JSON line (dict) on rank 0, None elsewhere."""
     import torch
     import torch.distributed as dist
+    from vboc_amd.dist import gather_boundary_states, gather_samples, shard_ids
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    nq, B = args.nq, args.batch
+    engine = (engine_factory or GpuEngine)(nq, args, local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
+        dist.init_process_group("nccl" if engine.device.type == "cuda" else "gloo", rank=rank, world_size=world)
+    dev = engine.device
+    dgl = args.workload == "dg-loop"
 
-    from vboc_amd import lib
-    nq, B = args.nq, args.batch
-    solver = lib.Solver(nq, 100, slots=args.slots, device=local)
-    solver.set_option("wave_all", 1 if args.mode == "wave" else 0)
-    solver.set_option("factor_mfma", 1 if args.factor == "mfma" else 0)
-    solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
-    stream = torch.cuda.current_stream(device)
+    # first-solve inputs: `max_batches` distinct batches generated and copied to HBM before any timing
+    nb = min(args.max_batches, args.warmup + args.steps)
+    batches = [] if dgl else [engine.first_solve_batch(nq, shard_ids(s, world, rank, B)) for s in range(nb)]
+    rec = dict(solves=0.0, problems=0, rows=0, flops=0.0, kernel_ms=0.0, launches=0, sqp=[], status=[], tail=None,
+               stats=None, lane_ms=0.0, lane_launch=0, lane_bytes=0.0)
 
-    from vboc_amd.dist import gather_boundary_states, shard_ids
-
-    def ids_for(step):
-        return shard_ids(step, world, rank, B)
-
-    # inputs for every step generated and copied to HBM before any timing
-    batches = [make_batch(nq, ids_for(s), device)[0] for s in range(args.warmup + args.steps)]
-    outs = []
-
-    def run_step(tb):
-        out = solver.solve_device(tb, stream=stream)
+    def step(s, timed):
+        out = engine.first_solve(batches[s % nb])
         if world > 1:
-            out["gathered"] = gather_boundary_states(out["x"][:, 0, :])
-        return out
+            gather_boundary_states(out["x0"])
+        if timed:
+            sqp, qpi = out["sqp_iter"].cpu().numpy(), out["qp_iter"].cpu().numpy()
+            rec["solves"] += B
+            rec["problems"] += B
+            rec["flops"] += float(np.sum(100 * (F_DYN[nq] * sqp + F_IPM[nq] * qpi + 2 * 4 * C_F[nq] * sqp)))
+            rec["sqp"].append(sqp)
+            rec["status"].append(out["status"].cpu().numpy() == 0)
+            if args.mode == "lane":
+                ms, nl, by = engine.lane_stats()
+                rec["lane_ms"] += ms
+                rec["lane_launch"] += nl
+                rec["lane_bytes"] += by
+            else:
+                rec["kernel_ms"] += engine.kernel_ms()
+                rec["launches"] += 1
 
-    for s in range(args.warmup):
-        run_step(batches[s])
-    torch.cuda.synchronize(device)
+    def dg_steps(first, count, timed):
+        """`count` consecutive steps as ONE persistent launch over their count * B problems (the launch's
+        tail - its slowest problem - is paid once, not once per step), then per step: X_save in problem
+        order and (N > 1) the all-gather of every rank's samples."""
+        if count == 0:
+            return
+        ids = np.concatenate([shard_ids(first + k, world, rank, B) for k in range(count)])
+        out = engine.dg(ids)
+        for k in range(count):
+            sl = slice(k * B, (k + 1) * B)
+            X = order_rows(dict(row_cnt=out["row_cnt"][sl], row_off=out["row_off"][sl], rows_all=out["rows_all"]))
+            if world > 1:
+                X = gather_samples(X)
+            rec["rows"] += X.shape[0] if timed else 0
+        if timed:
+            st = out["stats"].cpu().numpy()
+            rec["solves"] += float(st[:, 0].sum())
+            rec["problems"] += count * B
+            rec["flops"] += dg_flops(nq, st)
+            rec["stats"] = st
+            rec["sqp"].append(st[:, 2] / np.maximum(st[:, 0], 1))
+            rec["status"].append((out["row_cnt"] >= 0).cpu().numpy())
+            rec["kernel_ms"] += engine.kernel_ms()
+            rec["launches"] += 1
 
-    fact_ms, fact_launch, fact_bytes = 0.0, 0, 0.0
-    wave_ms, wave_launch = 0.0, 0
+    if dgl:
+        dg_steps(0, args.warmup, False)
+    else:
+        for s in range(args.warmup):
+            step(s, False)
+    engine.sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(device)
+    engine.sync()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        outs.append(run_step(batches[args.warmup + s]))
-        if args.mode == "lane":
-            ms, nl, by = solver.kernel_stats()
-            fact_ms += ms
-            fact_launch += nl
-            fact_bytes += by
-        else:
-            ms, _ = solver.last_kernel_ms()
-            wave_ms += ms
-            wave_launch += 1
-    torch.cuda.synchronize(device)
+    if dgl:
+        dg_steps(args.warmup, args.steps, True)
+    else:
+        for s in range(args.steps):
+            step(args.warmup + s, True)
+    engine.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    local_flops, local_solves = rec["flops"], rec["solves"]
+    solves, rows = local_solves, rec["rows"]
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed, -1.0], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    status = torch.cat([o["status"] for o in outs]).cpu().numpy()
-    sqp = torch.cat([o["sqp_iter"] for o in outs]).cpu().numpy()
-    qpi = torch.cat([o["qp_iter"] for o in outs]).cpu().numpy()
-    # whole-path FP64 work by the SURVEY 8(d) convention, with the solver's reported K_sqp and K_ipm;
-    # K_ls counted as 2 merit evaluations per SQP iteration (phi(0) + one trial: a lower bound)
-    Nh = 100
-    flops = float(np.sum(Nh * (F_DYN[nq] * sqp + F_IPM[nq] * qpi + 2 * 4 * C_F[nq] * sqp)))
-    local_flops = flops
-    if world > 1:
-        ft = torch.tensor([flops], device=device, dtype=torch.float64)
-        dist.all_reduce(ft)
-        flops = float(ft.item())
-    total = world * args.steps * B
-    value = total / elapsed
-    avg_launch_ms = fact_ms / max(1, fact_launch)
-    achieved_gbs = (fact_bytes / max(1, fact_launch)) / (avg_launch_ms * 1e-3) / 1e9 if fact_launch else None
+        elapsed = float(t[0].item())
+        t = torch.tensor([rec["flops"], local_solves], device=dev, dtype=torch.float64)
+        dist.all_reduce(t)
+        flops, solves = float(t[0].item()), float(t[1].item())   # (gathered rows are already the whole job's)
+    else:
+        flops = local_flops
+    problems = world * args.steps * B
+    value = solves / elapsed
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and engine_factory is None:
         threads = len(os.sched_getaffinity(0))
         threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
-        v, n, t = cpu_baseline(nq, B, args.cpu_seconds, threads)
+        v, n, ns, t = cpu_baseline(nq, args.workload, B, args.cpu_seconds, threads)
+        what = ("the batched data_generation driver on the oracle (oracle/vboc_oracle.c, OpenMP)" if dgl
+                else "first solves on oracle/vboc_oracle.c (OpenMP)")
         cpu = {"value": round(v, 2), "unit": "solves/s", "cores": threads, "kind": "port",
-               "sample": f"first {n} problems of the same workload (oracle/vboc_oracle.c, OpenMP, {t:.1f} s)"}
+               "sample": f"first {n} problems of the same workload ({ns} OCP solves), {what}, {t:.1f} s"}
 
+    kernel = getattr(engine, "kernel", "k_wave")
     if args.mode == "lane":
-        traffic_gb, traffic_src = pmc_traffic("k_qp_factor" if nq == 3 else f"k_qp_factor_nq{nq}")
-        roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1) if achieved_gbs else None,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved_gbs / HBM_PEAK_GBS, 4) if achieved_gbs else None,
+        avg_ms = rec["lane_ms"] / max(1, rec["lane_launch"])
+        gbs = (rec["lane_bytes"] / max(1, rec["lane_launch"])) / (avg_ms * 1e-3) / 1e9 if rec["lane_launch"] else None
+        traffic_gb, src = pmc_traffic("k_qp_factor" if nq == 3 else f"k_qp_factor_nq{nq}")
+        roofline = {"bound": "hbm", "achieved": round(gbs, 1) if gbs else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4) if gbs else None,
                     "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
-                    "traffic_source": traffic_src,
-                    "algorithmic_gb_per_launch": round(fact_bytes / max(1, fact_launch) / 1e9, 4),
-                    "kernel": f"k_qp_factor<{nq}>", "avg_launch_ms": round(avg_launch_ms, 4),
-                    "launches": fact_launch}
+                    "traffic_source": src, "kernel": kernel, "avg_launch_ms": round(avg_ms, 4),
+                    "launches": rec["lane_launch"]}
     else:
-        # PMC passes are per instantiation (profiles/*_pmc_k_wave.json is the triple's k_wave<3>)
-        traffic_gb, traffic_src = pmc_traffic("k_wave" if nq == 3 else f"k_wave_nq{nq}")
-        avg_ms = wave_ms / max(1, wave_launch)
-        per_launch = local_flops / max(1, args.steps)
-        wave_tf = per_launch / (avg_ms * 1e-3) / 1e12 if wave_ms else None
-        roofline = {"bound": "mfma", "achieved": round(wave_tf, 4) if wave_tf else None,
-                    "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(wave_tf / FP64_PEAK_TFLOPS, 5) if wave_tf else None,
+        pmc_name = ("k_dg" if dgl else "k_wave") + ("" if nq == 3 else f"_nq{nq}")
+        traffic_gb, src = pmc_traffic(pmc_name)
+        avg_ms = rec["kernel_ms"] / max(1, rec["launches"])
+        per_launch = local_flops / max(1, rec["launches"])
+        tf = per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms else None
+        roofline = {"bound": "mfma", "achieved": round(tf, 4) if tf else None, "peak": FP64_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(tf / FP64_PEAK_TFLOPS, 5) if tf else None,
                     "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
-                    "traffic_source": traffic_src,
-                    "algorithmic": "FP64 flops per launch, SURVEY.md 8(d): N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp)",
-                    "flops_per_launch": round(per_launch), "kernel": f"k_wave<{nq}>",
-                    "avg_launch_ms": round(avg_ms, 3), "launches": wave_launch}
-    if rank == 0:
-        line = {
-            "metric": "VBOC boundary OCP solves/sec, triple pendulum, 1/2/4/8 MI355X" if nq == 3 else
-                      f"VBOC boundary OCP solves/sec, {NAMES[nq]}, 1/2/4/8 MI355X",
-            "value": round(value, 2),
-            "unit": "solves/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 2),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (Philox-seeded ICs by the reference's " +
-                    ("testing_test law, VBOC/UR5/vboc_multiprocessing_ur5.py)" if nq == 4 else "data_generation law)"),
-            "config": {"workload": WORKLOAD[nq].format(B=B),
-                       "problems_per_gpu": B, "horizon": 100, "parallelism": f"dp{world}", "mode": args.mode,
-                       "allgather": world > 1},
-            "roofline": roofline,
-            "path_fp64": {"achieved": round(flops / elapsed / 1e12, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                          "frac": round(flops / elapsed / 1e12 / FP64_PEAK_TFLOPS, 5),
-                          "convention": "SURVEY.md 8(d): N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp)"},
-            "cpu_baseline": cpu,
-            "solver": {"status_ok_frac": round(float(np.mean(status == 0)), 4),
-                       "sqp_iter_mean": round(float(sqp.mean()), 1), "sqp_iter_max": int(sqp.max())},
-        }
-        print(json.dumps(line), flush=True)
+                    "traffic_source": src,
+                    "pipes": "FP64: Riccati factorisation on v_mfma_f64_16x16x4f64 (factor_mfma), the rest FP64 VALU; "
+                             "peak = FP64 dense (vector = matrix on MI355X); latency-bound dependent recursions",
+                    "algorithmic": "FP64 flops per launch, SURVEY.md 8(d): sum over solves of "
+                                   "N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp)" + (" + 4*C_f per twin step" if dgl else ""),
+                    "flops_per_launch": round(per_launch), "kernel": kernel, "avg_launch_ms": round(avg_ms, 3),
+                    "launches": rec["launches"]}
+    tail = None
+    if dgl and rec["stats"] is not None:
+        from vboc_amd.lib import DG_CLOCK_HZ
+        st = rec["stats"]
+        t0s, t1s = st[:, 5], st[:, 6]
+        ms = 1e3 / DG_CLOCK_HZ
+        tail = {"critical_problem_ms": round(float((t1s - t0s).max()) * ms, 1),
+                "mean_problem_ms": round(float((t1s - t0s).mean()) * ms, 2),
+                "queue_drained_ms": round(float(t0s.max() - t0s.min()) * ms, 1),
+                "last_finish_ms": round(float(t1s.max() - t0s.min()) * ms, 1),
+                "note": "last timed launch, device real-time clock from the first problem's start"}
+    sqp = np.concatenate(rec["sqp"]) if rec["sqp"] else np.zeros(1)
+    ok = np.concatenate(rec["status"]) if rec["status"] else np.zeros(1)
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return None
+    line = {
+        "metric": "VBOC boundary OCP solves/sec, triple pendulum, 1/2/4/8 MI355X" if nq == 3 else
+                  f"VBOC boundary OCP solves/sec, {NAMES[nq]}, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (Philox-seeded ICs by the reference's " +
+                ("testing_test law, VBOC/UR5/vboc_multiprocessing_ur5.py)" if nq == 4 else "data_generation law)"),
+        "config": {"workload": WORKLOAD[(args.workload, nq)].format(B=B), "problems_per_gpu": B,
+                   "horizon_start": 100, "parallelism": f"dp{world}", "mode": args.mode,
+                   "allgather": ("samples" if dgl else "x0") if world > 1 else None},
+        "roofline": roofline,
+        "path_fp64": {"achieved": round(flops / elapsed / 1e12, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                      "frac": round(flops / elapsed / 1e12 / FP64_PEAK_TFLOPS, 5)},
+        "cpu_baseline": cpu,
+        "solver": {"ok_frac": round(float(np.mean(ok)), 4), "sqp_iter_mean": round(float(sqp.mean()), 1),
+                   "sqp_iter_max": round(float(sqp.max()), 1)},
+    }
+    if dgl:
+        line["loop"] = {"boundary_problems_per_s": round(problems / elapsed, 2),
+                        "solves_per_problem": round(solves / problems, 3),
+                        "samples": int(rows), "samples_per_s": round(rows / elapsed, 1), "tail": tail}
     if world > 1:
         dist.destroy_process_group()
+    return line
+
+
+def main(argv=None):
+    line = run(parse(argv))
+    if line is not None:
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

@@ -112,3 +112,22 @@ def solve_batch(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe
     if rc != 0:
         raise RuntimeError(f"oracle solve_batch failed rc={rc}")
     return x_out, u_out, res
+
+
+class DriverBackend:
+    """The oracle behind the batched drivers' backend interface (vboc_amd.drivers: solve(batch),
+    rk4(x, u, T)) - the CPU baseline of bench.py's dg-loop leg and the tests' reference runs."""
+    nmax = 512
+
+    def __init__(self, nq, nthreads=None):
+        self.nq, self.nthreads = nq, nthreads
+
+    def solve(self, b, free_time=False):
+        xo, uo, r = solve_batch(self.nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                                b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], nthreads=self.nthreads,
+                                free_time=free_time)
+        return dict(status=np.array(r["status"]), x=xo, u=uo, cost=np.array(r["cost"]),
+                    sqp_iter=np.array(r["sqp_iter"]), qp_iter=np.array(r["qp_iter"]))
+
+    def rk4(self, x, u, T):
+        return np.stack([rk4(self.nq, T, x[i], u[i]) for i in range(x.shape[0])])

@@ -1,7 +1,9 @@
 """N > 1 path on CPU: two gloo ranks shard the problem ids (vboc_amd.dist.shard_ids), solve their
 shards (the CPU oracle stands in for the GPU solver here) and all-gather the boundary states
 (vboc_amd.dist.gather_boundary_states, the collective bench.py runs over RCCL).  The gathered
-result must equal a single-process solve of all ids, bit for bit."""
+result must equal a single-process solve of all ids, bit for bit.  bench.run itself (step loop, barrier,
+rank-max timing, flop / solve all-reduce, all-gather of the samples) runs at world size 2 on gloo with the
+oracle as its engine."""
 import os
 import socket
 import sys
@@ -65,3 +67,97 @@ def test_two_rank_gather_equals_single_process(tmp_path):
     assert got.shape == ref.shape
     np.testing.assert_array_equal(got, ref)
     assert np.all(np.isin(status, [0, 2]))
+
+
+# ------------------------------------------------------------------------------------------------
+# bench.py's N > 1 path (run(args, engine_factory)) on gloo, the oracle as the engine
+# ------------------------------------------------------------------------------------------------
+class OracleEngine:
+    """bench.GpuEngine's interface on the CPU oracle (test infrastructure)."""
+    kernel = "oracle"
+
+    def __init__(self, nq, args, local):
+        import torch
+        self.torch, self.nq = torch, nq
+        self.device = torch.device("cpu")
+        self.ms = 0.0
+
+    def sync(self):
+        pass
+
+    def first_solve_batch(self, nq, ids):
+        from vboc_amd.ics import data_generation_ics
+        return data_generation_ics(nq, ids)
+
+    def first_solve(self, b):
+        import time
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        t0 = time.perf_counter()
+        xo, _, r = oracle.solve_batch(self.nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                                      b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"],
+                                      opts=oracle.default_opts(max_iter=40), nthreads=1)
+        self.ms = (time.perf_counter() - t0) * 1e3
+        T = self.torch.as_tensor
+        return dict(x0=T(xo[:, 0, :].copy()), status=T(r["status"].copy()), sqp_iter=T(r["sqp_iter"].copy()),
+                    qp_iter=T(r["qp_iter"].copy()))
+
+    def dg(self, ids):
+        import time
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        from vboc_amd.drivers import data_generation_batch
+        t0 = time.perf_counter()
+        res, st = data_generation_batch(self.nq, ids, oracle.DriverBackend(self.nq, 1))
+        self.ms = (time.perf_counter() - t0) * 1e3
+        samples = [r[0] if self.nq == 2 else r for r in res]
+        cnt = np.array([-1 if s is None else len(s) for s in samples])
+        rows = np.array([row for s in samples if s for row in s], dtype=np.float64).reshape(-1, 2 * self.nq)
+        off = np.concatenate([[0], np.cumsum(np.maximum(cnt, 0))[:-1]])
+        stats = np.zeros((len(ids), 7))
+        stats[0, 0], stats[0, 1] = st["solves"], st["rk4"]
+        T = self.torch.as_tensor
+        return dict(rows_all=T(rows), row_off=T(off.astype(np.int64)), row_cnt=T(cnt.astype(np.int32)), stats=T(stats))
+
+    def kernel_ms(self):
+        return self.ms
+
+
+def _bench_worker(rank, world, port, argv, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import json
+    import bench
+    from test_distributed import OracleEngine
+    line = bench.run(bench.parse(argv), engine_factory=OracleEngine)
+    if rank == 0:
+        json.dump(line, open(out_path, "w"))
+
+
+@pytest.mark.parametrize("workload", ["dg-loop", "first-solve"])
+def test_bench_runs_at_world_two_on_gloo(tmp_path, workload):
+    import json
+    import torch.multiprocessing as mp
+    from vboc_amd.dist import shard_ids
+    B, steps = 3, 2
+    argv = ["--gpus", "2", "--nq", "2", "--batch", str(B), "--steps", str(steps), "--warmup", "1",
+            "--workload", workload, "--no-cpu"]
+    out = str(tmp_path / "line.json")
+    mp.spawn(_bench_worker, args=(2, _free_port(), argv, out), nprocs=2, join=True)
+    line = json.load(open(out))
+    assert line["n_gpus"] == 2 and line["steps"] == steps and line["config"]["parallelism"] == "dp2"
+    assert line["value"] > 0 and line["ms_per_step"] > 0
+    eng = OracleEngine(2, None, 0)
+    ids = [shard_ids(s, 2, r, B) for s in range(1, 1 + steps) for r in range(2)]   # the timed steps
+    if workload == "dg-loop":
+        outs = [eng.dg(i) for i in ids]
+        solves = sum(float(o["stats"][:, 0].sum()) for o in outs)
+        rows = sum(int(o["rows_all"].shape[0]) for o in outs)
+        # every rank's samples were all-gathered; solves all-reduced; value = all solves / max-over-ranks time
+        assert line["loop"]["samples"] == rows
+        assert abs(line["loop"]["solves_per_problem"] - solves / (2 * steps * B)) < 1e-3
+        assert abs(line["value"] - solves / (line["ms_per_step"] * steps / 1e3)) < 0.01 * line["value"] + 0.01
+    else:
+        assert abs(line["value"] - 2 * steps * B / (line["ms_per_step"] * steps / 1e3)) < 0.01 * line["value"] + 0.01

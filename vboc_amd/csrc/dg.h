@@ -54,14 +54,15 @@ struct DgJobs {
   unsigned* done;
 };
 
-// per-problem statistics: OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter
-enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_NSTAT };
+// per-problem statistics: OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, and
+// the wave's start / end time of the problem (s_memrealtime, 100 MHz constant clock)
+enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_NSTAT };
 
 template <int NQ>
 struct DgState {
   int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, pad0, pad1;
   double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
-  double sqp, nsqp, nqp;
+  double sqp, nsqp, nqp, t0;
   double ran[2], store_ic[4], xsym[2 * NQ];
 };
 
@@ -233,6 +234,7 @@ struct Dg {
 #pragma clang fp contract(off)
     job = job_;
     pid = J.ids[job];
+    s->t0 = (double)__builtin_amdgcn_s_memrealtime();
     const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max, eps = J.eps;
     s->phase = HEXT; s->N = J.N_start; s->ext = 0; s->f = 0; s->at_limit = 0; s->N_test = 0; s->ver = 0;
     s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0;
@@ -593,6 +595,8 @@ struct Dg {
       st[DG_SQP] = s->sqp;
       st[DG_NSQP] = s->nsqp;
       st[DG_NQP] = s->nqp;
+      st[DG_T0] = s->t0;
+      st[DG_T1] = (double)__builtin_amdgcn_s_memrealtime();
       atomicAdd(J.done, 1u);
     }
   }

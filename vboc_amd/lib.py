@@ -50,7 +50,9 @@ class DgBatch(ctypes.Structure):
                 ("stats", ctypes.c_void_p), ("rows_used", ctypes.c_longlong)]
 
 
-DG_STATS = ("solves", "rk4", "sqp_iter", "n_sqp_iter", "n_qp_iter")   # per problem (vboc_dg_batch_t.stats)
+# per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
+DG_STATS = ("solves", "rk4", "sqp_iter", "n_sqp_iter", "n_qp_iter", "t0", "t1")
+DG_CLOCK_HZ = 100e6
 
 
 def build(verbose=False, extra_flags=(), out=None):
