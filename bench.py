@@ -81,16 +81,20 @@ WORKLOAD = {
 }
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, problems=None):
     """HBM traffic per launch of `kernel` from the newest committed rocprofv3 PMC summary
     (profiles/*_pmc_<kernel>.json, made by tools/pmc_summary.py from FETCH_SIZE / WRITE_SIZE passes of
-    this bench command, gfx950-corrected).  None if there is none."""
+    this bench command, gfx950-corrected); for the dg-loop (launch sizes differ) the per-problem figure
+    scaled to `problems`.  None if there is none."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_pmc_{kernel}.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    return d["traffic_bytes_per_launch"] / 1e9, os.path.relpath(files[-1], ROOT)
+    src = os.path.relpath(files[-1], ROOT)
+    if problems is not None and "traffic_bytes_per_problem" in d:
+        return d["traffic_bytes_per_problem"] * problems / 1e9, src + " (per problem x problems per launch)"
+    return d["traffic_bytes_per_launch"] / 1e9, src
 
 
 def dg_flops(nq, stats):
@@ -338,7 +342,7 @@ def run(args, engine_factory=None):
                     "launches": rec["lane_launch"]}
     else:
         pmc_name = ("k_dg" if dgl else "k_wave") + ("" if nq == 3 else f"_nq{nq}")
-        traffic_gb, src = pmc_traffic(pmc_name)
+        traffic_gb, src = pmc_traffic(pmc_name, args.steps * B if dgl else None)
         avg_ms = rec["kernel_ms"] / max(1, rec["launches"])
         per_launch = local_flops / max(1, rec["launches"])
         tf = per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms else None

@@ -10,11 +10,13 @@ so a last-bit difference in a guess may propagate to rounding-level differences 
 """
 import json
 import os
+import sys
 
 import numpy as np
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
 
 
 def _samples(nq, r):
@@ -102,3 +104,42 @@ def test_device_loop_properties_at_scale():
     dup = (np.abs(v) <= sysd.v_max + 1e-9).all(1)
     assert (inside | dup).all()
     assert (np.abs(v) <= sysd.v_max + 1e-6).all() and (q >= sysd.q_min - 1e-6).all() and (q <= sysd.q_max + 1e-6).all()
+
+
+class _FailingGpu:
+    """The host driver's GPU backend with the fixtures' deterministic failure injection on top."""
+
+    def __init__(self, nq, fail_mod):
+        from vboc_amd.drivers import GpuBackend
+        from oracle_backend import forced_failure
+        self.gpu, self.fail_mod, self.ff = GpuBackend(nq, nmax=120), fail_mod, forced_failure
+        self.nmax = self.gpu.nmax
+
+    def solve(self, b, free_time=False):
+        r = self.gpu.solve(b)
+        st = np.array(r["status"], copy=True)
+        for i in range(st.shape[0]):
+            if self.ff(b["lbx0"][i, 0], self.fail_mod):
+                st[i] = 4
+        return dict(r, status=st)
+
+    def rk4(self, x, u, T):
+        return self.gpu.rk4(x, u, T)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq", [3, 2])
+def test_device_loop_restart_branches_match_host_driver(nq):
+    """With the same failure injection (status 4 when int(|q_0| 1e6) % 3 == 0), the perturbed restarts of
+    the horizon extension (:138-174; the double's store_ic bookkeeping), the failed-problem return and the
+    unresolved verification branch run on the device exactly as in the host driver."""
+    from vboc_amd import lib
+    from vboc_amd.drivers import data_generation_batch, data_generation_device
+    ids = np.arange(2000, 2032)
+    host, hst = data_generation_batch(nq, ids, _FailingGpu(nq, 3), N_start=100)
+    s = lib.Solver(nq, 120)
+    s.set_option("dg_fail_mod", 3)
+    dev, dst = data_generation_device(nq, ids, s, N_start=100)
+    assert dst["solves"] == hst["solves"] and dst["rk4"] == hst["rk4"] and dst["solves"] > 3 * len(ids)
+    same, worst = _compare(nq, dev, host, 0.0 if nq == 3 else 1e-9)
+    assert same == len(ids) if nq == 3 else same >= 0.9 * len(ids), (same, worst)

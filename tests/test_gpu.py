@@ -34,8 +34,8 @@ def _gpu(nq, b, **opts):
         s.close()
 
 
-def _compare(nq, b, max_iter, coop=8192, wave=0):
-    g = _gpu(nq, b, nlp_solver_max_iter=max_iter, coop_threshold=coop, wave_all=wave)
+def _compare(nq, b, max_iter, coop=8192, wave=0, **opts):
+    g = _gpu(nq, b, nlp_solver_max_iter=max_iter, coop_threshold=coop, wave_all=wave, **opts)
     xo, uo, r = _oracle(nq, b, max_iter=max_iter)
     assert np.mean(g["status"] == r["status"]) >= 0.98, (g["status"], r["status"])
     assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= 0.95
@@ -288,3 +288,42 @@ def test_pendulum_vboc_run_on_gpu(tmp_path):
     assert r["fit"]["val"] <= 1e-4 or r["fit"]["iterations"] >= 100 * int(r["X"].shape[0] * 100 / 64)
     assert r["rmse"] < 1.0
     assert (tmp_path / "model_1dof_vboc_10").exists()
+
+
+# problems of the data_generation first-solve law whose oracle SQP runs the longest (found with
+# oracle.solve_batch over ids 0..1535, max_iter 1000): 988 and 358 stop at max_iter (status 2), 832 / 1464 /
+# 703 / 125 / 73 converge after 701 / 664 / 632 / 556 / 519 iterations
+LONG_TAIL = (988, 358, 832, 1464, 703, 125, 73)
+
+
+@pytest.mark.parametrize("factor", ["mfma", "valu"])
+def test_parity_triple_full_iteration_budget_with_long_tail(factor):
+    """The triple at the reference's nlp_solver_max_iter = 1000 (VBOC/triplependulum_class_vboc.py:136) on
+    a batch holding the long-tail problems the bench hits, on the default wave solver (both Riccati
+    factorisations)."""
+    from vboc_amd.ics import data_generation_ics
+    ids = np.concatenate([np.arange(40), LONG_TAIL])
+    b = data_generation_ics(3, ids)
+    g, r = _compare(3, b, max_iter=1000, wave=1, factor_mfma=1 if factor == "mfma" else 0)
+    tail = np.arange(40, len(ids))
+    assert (g["status"][tail] == r["status"][tail]).all(), (g["status"][tail], r["status"][tail])
+    assert (r["sqp_iter"][tail] >= 500).all()
+    ok = tail[r["status"][tail] == 0]
+    assert np.abs(g["cost"][ok] - r["cost"][ok]).max() <= 2e-3
+
+
+@pytest.mark.parametrize("nq", [1, 2, 3])
+def test_shooting_sensitivities_match_golden(nq):
+    """The solvers' linearisation (ERK4 + forward sensitivities, vboc_rk4_sens_batch_host) against the
+    golden shooting Jacobians from the reference's own f_expl (tests/golden/make_golden.py: RK4 with
+    h = 1 on the dt-scaled model, tf / N = 1): A = d x1 / d x, B = d x1 / d u without the dt row/column."""
+    import os
+    from vboc_amd import lib
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", f"dynamics_{nq}.npz"))
+    nx = 2 * nq
+    for i in range(g["x"].shape[0]):
+        x, u = g["x"][i], g["u"][i]
+        x1, A, B = lib.rk4_sens_host(nq, float(x[nx]), x[None, :nx], u[None])
+        np.testing.assert_allclose(x1[0], g["shoot_x1"][i, :nx], rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(A[0], g["shoot_jac"][i][:nx, :nx], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(B[0], g["shoot_jac"][i][:nx, nx + 1:], rtol=1e-10, atol=1e-12)

@@ -1,7 +1,9 @@
 """Per-launch HBM traffic of one kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
 
 Usage: python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv>
-       <bench_line.json> [kernel-substring] > profiles/<round>_pmc_<kernel>.json
+       <bench_line.json> [kernel-substring] [sq_counter_collection.csv] > profiles/<round>_pmc_<kernel>.json
+The optional SQ pass adds the instruction / busy counters of the launch (FP64 MFMA ops, MFMA busy cycles,
+VALU and LDS instructions, GRBM_GUI_ACTIVE).
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE (KB) reports half the bytes of wide
 coalesced streaming reads, so it is doubled; WRITE_SIZE (KB) is taken as is.  The algorithmic bytes
@@ -35,9 +37,18 @@ def main():
         alg = rf["achieved"] * 1e9 * rf["avg_launch_ms"] * 1e-3
         out.update(algorithmic_bytes_per_launch=alg, traffic_over_algorithmic=(fetch_b + write_b) / alg)
     else:                      # FP64 roofline: arithmetic intensity against HBM traffic
+        if "loop" in line:     # dg-loop: launches differ in size, so the bench scales a per-problem figure
+            probs = line["config"]["problems_per_gpu"] * line["steps"]
+            out.update(problems_per_launch=probs, traffic_bytes_per_problem=(fetch_b + write_b) / probs)
         out.update(flops_per_launch=rf["flops_per_launch"],
                    flop_per_hbm_byte=rf["flops_per_launch"] / (fetch_b + write_b),
                    hbm_gbs_during_launch=(fetch_b + write_b) / (rf["avg_launch_ms"] * 1e-3) / 1e9)
+    if len(sys.argv) > 5:
+        sq = {}
+        for r in csv.DictReader(open(sys.argv[5])):
+            if kernel in r["Kernel_Name"]:
+                sq[r["Counter_Name"]] = sq.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        out["sq_counters_per_launch"] = sq
     print(json.dumps(out, indent=1))
 
 

@@ -30,6 +30,7 @@ struct DgJobs {
   const long long* ids;        // problem ids (Philox keys), one per job
   int count;
   int N_start, nmax;
+  int fail_mod;                // test-only failure injection (solver option dg_fail_mod), 0 = off
   unsigned long long seed;
   // system constants (vboc_amd/systems.py; VBOC/triplependulum_vboc.py:381-393)
   double q_min, q_max, v_max, u_max, dt, tol, eps, g, l1, l2, m1, m2;
@@ -314,6 +315,10 @@ struct Dg {
     s->sqp += (double)it;
     s->nsqp += (double)N * (double)it;
     s->nqp += (double)N * (double)qit;
+    if (J.fail_mod > 0) {   // tests: status 4 when int(|q_0| 1e6) % fail_mod == 0 (tests/oracle_backend.py)
+      const long long q = (long long)(fabs(qlb0()[0]) * 1e6);
+      if (q % J.fail_mod == 0) ((int*)in.status)[wg] = 4;
+    }
     const bool more = s->phase == HEXT ? on_hext() : on_verif();
     if (more) return true;
     return s->phase == SWEEP ? sweep() : false;   // one inlined copy of the sweep (with its RK4)

@@ -1356,6 +1356,7 @@ struct vboc_solver {
   DgJobs* dg_jobs = nullptr;        // device copies of the job descriptor and of the per-workgroup batch
   Inputs* dg_in = nullptr;
   bool dg_attr[2] = {false, false};
+  int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
 };
 
 static void default_opts(Opts& o) {
@@ -1659,6 +1660,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "factor_mfma") h->factor_mfma = v != 0.0 && h->nq <= 3;
   else if (s == "wave_groups") h->group_cap = (long long)v;
   else if (s == "mall_mib") h->mall_mib = v;
+  else if (s == "dg_fail_mod") h->dg_fail_mod = (int)v;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
     if (h->profile && h->pev.empty()) {
@@ -1997,6 +1999,7 @@ int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
   in.qp_iter = ip; ip += G;
   if ((size_t)((char*)ip - (char*)h->dg_scratch) > need) return fail(VBOC_ERR_ARG, "vboc_data_generation: internal size error");
   J.ids = b->ids; J.count = b->B; J.N_start = b->N_start; J.nmax = nm; J.seed = b->seed;
+  J.fail_mod = h->dg_fail_mod;
   J.q_min = b->q_min; J.q_max = b->q_max; J.v_max = b->v_max; J.u_max = b->u_max; J.dt = b->dt; J.tol = b->tol;
   J.eps = b->eps; J.g = b->g; J.l1 = b->l1; J.l2 = b->l2; J.m1 = b->m1; J.m2 = b->m2;
   J.rows = b->rows; J.rows_cap = b->rows_cap; J.row_off = b->row_off; J.row_cnt = b->row_cnt;

@@ -27,6 +27,7 @@ import numpy as np
 from .drivers import data_generation_batch, heldout_set, testing_batch
 from .ics import SEED
 from .learn import DirTrainer, dir_features, position_stats
+from .systems import system
 
 
 def samples_array(nq, results):
@@ -75,22 +76,34 @@ def make_test_set(nq, backend, num_prob=1000, first_id=0, out_dir=None, seed=SEE
     return X, stats
 
 
+def _generate(nq, backend, ids, N_start, seed):
+    """data_generation for `ids`: on the product GPU backend the whole state machine runs on the device
+    (drivers.data_generation_device, vboc_data_generation); other backends (the oracle in the tests) go
+    through the host driver.  Both return the reference's per-problem results in problem order."""
+    from .drivers import data_generation_device
+    solver = getattr(backend, "solver", None)
+    if solver is not None and hasattr(solver, "data_generation_device") and \
+            solver.nmax >= (N_start or system(nq).N) + 12:
+        return data_generation_device(nq, ids, solver, N_start=N_start, seed=seed)
+    return data_generation_batch(nq, ids, backend, N_start=N_start, seed=seed)
+
+
 def _round(nq, backend, iteration, num_prob, N_start, seed):
-    """One data-generation round, sharded over ranks when torch.distributed is initialised."""
+    """One data-generation round over the problem ids [iteration * num_prob, (iteration + 1) * num_prob),
+    split into contiguous per-rank shards (np.array_split) when torch.distributed is initialised, so any
+    world size solves the same id set; the samples are all-gathered in rank (= problem) order."""
     import torch.distributed as dist
-    from .dist import gather_samples, shard_ids
+    from .dist import gather_samples
+    ids = np.arange(iteration * num_prob, (iteration + 1) * num_prob)
     if dist.is_available() and dist.is_initialized():
         import torch
         world, rank = dist.get_world_size(), dist.get_rank()
-        per = -(-num_prob // world)
-        ids = shard_ids(iteration, world, rank, per)
-        res, stats = data_generation_batch(nq, ids, backend, N_start=N_start, seed=seed)
+        res, stats = _generate(nq, backend, np.array_split(ids, world)[rank], N_start, seed)
         local = torch.from_numpy(samples_array(nq, res))
         if dist.get_backend() == "nccl":
             local = local.cuda()
         return gather_samples(local).cpu().numpy(), stats
-    ids = np.arange(iteration * num_prob, (iteration + 1) * num_prob)
-    res, stats = data_generation_batch(nq, ids, backend, N_start=N_start, seed=seed)
+    res, stats = _generate(nq, backend, ids, N_start, seed)
     return samples_array(nq, res), stats
 
 
