@@ -157,8 +157,9 @@ int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const dou
  *   row_off[B], row_cnt[B]  block of problem b; row_cnt -1 = the reference returns None
  *   ic[B][4], ic_slot[B]    double pendulum store_ic and its tuple position (1 success, 2 failure);
  *                       may be NULL for the triple
- *   stats[B][7]         OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, start and
- *                       end time of the problem on its wave (device real-time clock, 100 MHz ticks)
+ *   stats[B][9]         OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, start and
+ *                       end time of the problem on its wave (device real-time clock, 100 MHz ticks), the
+ *                       first solve's status and SQP iterations
  *   rows_used           OUT: rows written
  * Requires N_start + 12 <= nmax of the handle. */
 typedef struct {

@@ -57,13 +57,14 @@ struct DgJobs {
 
 // per-problem statistics: OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, and
 // the wave's start / end time of the problem (s_memrealtime, 100 MHz constant clock)
-enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_NSTAT };
+// and the first solve's status and SQP iterations
+enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST1, DG_IT1, DG_NSTAT };
 
 template <int NQ>
 struct DgState {
   int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, pad0, pad1;
   double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
-  double sqp, nsqp, nqp, t0;
+  double sqp, nsqp, nqp, t0, st1, it1;
   double ran[2], store_ic[4], xsym[2 * NQ];
 };
 
@@ -312,6 +313,10 @@ struct Dg {
     pid = J.ids[job];
     const int N = nreq();
     const int it = in.sqp_iter[wg], qit = in.qp_iter[wg];
+    if (s->solves == 1) {
+      s->st1 = (double)this->status();
+      s->it1 = (double)it;
+    }
     s->sqp += (double)it;
     s->nsqp += (double)N * (double)it;
     s->nqp += (double)N * (double)qit;
@@ -602,6 +607,8 @@ struct Dg {
       st[DG_NQP] = s->nqp;
       st[DG_T0] = s->t0;
       st[DG_T1] = (double)__builtin_amdgcn_s_memrealtime();
+      st[DG_ST1] = s->st1;
+      st[DG_IT1] = s->it1;
       atomicAdd(J.done, 1u);
     }
   }
