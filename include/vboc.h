@@ -161,7 +161,12 @@ int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const dou
  *                       end time of the problem on its wave (device real-time clock, 100 MHz ticks), the
  *                       first solve's status and SQP iterations
  *   rows_used           OUT: rows written
- * Requires N_start + 12 <= nmax of the handle. */
+ *   spec_solves, spec_used  OUT: speculative restarts (below)
+ * Requires N_start + 12 <= nmax of the handle.
+ * Speculative restarts (solver option "dg_speculate", default 1): when a horizon-extension solve fails, the
+ * inputs of the problem's later attempts (perturbed restarts, up to 10 attempts) are known in advance, so
+ * other waves solve them in parallel and the problem takes the results in order; results are identical to
+ * the sequential chain.  Only solves the problem consumes count in stats. */
 typedef struct {
   int B;
   const long long* ids;
@@ -176,6 +181,8 @@ typedef struct {
   int* ic_slot;
   double* stats;
   long long rows_used;
+  long long spec_solves;   /* OUT: speculative restart solves run by other waves */
+  long long spec_used;     /* OUT: of them, taken by their problem (the rest is extra work, never counted) */
 } vboc_dg_batch_t;
 int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* batch, void* stream);
 

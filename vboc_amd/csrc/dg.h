@@ -53,7 +53,23 @@ struct DgJobs {
   unsigned long long* rows_next;
   unsigned* err;               // [0] pool overflow, [1] horizon > nmax
   unsigned* done;
+  // speculative restarts (see "Speculative restarts" below); spec_events == 0 switches them off
+  int spec_events, spec_stride;   // events in the pool, doubles per event
+  double* spec;                   // [spec_events][spec_stride]: snapshot header, then DG_SPEC_JOBS results
+  int* spec_claim;                // [spec_events][DG_SPEC_JOBS + 1]: 0 free, 1 claimed
+  int* spec_done;                 // [spec_events][DG_SPEC_JOBS + 1]: 1 = result written
+  int* spec_cancel;               // [spec_events]: 1 = the owner no longer needs the event's results
+  int* spec_q;                    // [spec_events * DG_SPEC_JOBS] queue of (event, job) + 1, 0 = not yet written
+  unsigned* spec_ev_next;         // event allocator
+  unsigned* spec_q_tail;          // queue: entries pushed / popped
+  unsigned* spec_q_head;
+  unsigned long long* spec_count; // [0] speculative solves run by other waves, [1] of them used
 };
+
+// a horizon extension gives up after 10 solves (VBOC/triplependulum_vboc.py:107): a failure at attempt a
+// leaves at most 9 further attempts to speculate on
+constexpr int DG_SPEC_JOBS = 9;
+constexpr int DG_SPEC_HDR = 48;   // doubles of an event's snapshot header
 
 // per-problem statistics: OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, and
 // the wave's start / end time of the problem (s_memrealtime, 100 MHz constant clock)
@@ -62,7 +78,8 @@ enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST
 
 template <int NQ>
 struct DgState {
-  int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, pad0, pad1;
+  int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, spec_ev,
+      spec_base;
   double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
   double sqp, nsqp, nqp, t0, st1, it1;
   double ran[2], store_ic[4], xsym[2 * NQ];
@@ -100,6 +117,29 @@ __device__ __forceinline__ double np_norm(const double* v) {
   double s = v[0] * v[0];
   UNR for (int i = 1; i < n; ++i) s = fma(v[i], v[i], s);
   return sqrt(s);
+}
+
+// Cross-wave data of the speculative restarts (event snapshots, results, flags) is read and written with
+// relaxed agent-scope atomics: on gfx950 these bypass the non-coherent per-XCD L2 state (sc1) and need no
+// fence.  A release / acquire pair would instead write back / invalidate a whole XCD's L2 on every publish
+// and on every poll of a waiting wave, which evicts the resident problems' stage records of every other
+// wave on that XCD (measured: +16 s of queue time on the 400k-problem launch).  A writer orders its data
+// before its flag with s_waitcnt vmcnt(0) (all of the wave's stores completed); a reader issues its data
+// loads only after its flag load returned.
+__device__ __forceinline__ void st_coh(double* p, double v) {
+  __hip_atomic_store((unsigned long long*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_coh(const double* p) {
+  return __longlong_as_double((long long)__hip_atomic_load((unsigned long long*)p, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_flag(int* p, int v) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_flag(const int* p) {
+  return __hip_atomic_load((int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int NQ>
@@ -239,7 +279,7 @@ struct Dg {
     s->t0 = (double)__builtin_amdgcn_s_memrealtime();
     const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max, eps = J.eps;
     s->phase = HEXT; s->N = J.N_start; s->ext = 0; s->f = 0; s->at_limit = 0; s->N_test = 0; s->ver = 0;
-    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0;
+    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0;
     s->sqp = 0.0; s->nsqp = 0.0; s->nqp = 0.0; s->cost = 1e6;
     int di = 0;
     auto draw = [&]() { return philox_uniform(pid, di++, J.seed, 0u); };
@@ -292,23 +332,14 @@ struct Dg {
       ub0[NQ + j] = v_max;
     }
     lb0[NX] = J.dt; ub0[NX] = J.dt;
-    // the bounds every OCP_solve of data_generation passes (:381-393)
-    double* lbx = (double*)in.lbx + (long long)wg * NXR; double* ubx = (double*)in.ubx + (long long)wg * NXR;
-    double* lbxe = (double*)in.lbxe + (long long)wg * NXR; double* ubxe = (double*)in.ubxe + (long long)wg * NXR;
-    double* lbu = (double*)in.lbu + (long long)wg * NU; double* ubu = (double*)in.ubu + (long long)wg * NU;
-    UNR for (int j = 0; j < NQ; ++j) {
-      lbx[j] = q_min; ubx[j] = q_max; lbx[NQ + j] = v_min; ubx[NQ + j] = v_max;
-      lbxe[j] = q_min; ubxe[j] = q_max; lbxe[NQ + j] = 0.0; ubxe[NQ + j] = 0.0;
-      lbu[j] = -J.u_max; ubu[j] = J.u_max;
-    }
-    lbx[NX] = J.dt; ubx[NX] = J.dt; lbxe[NX] = J.dt; ubxe[NX] = J.dt;
+    set_bounds();
     straight_guess(J.N_start, qpos);
     request(J.N_start);
     return true;
   }
 
   // the solve just finished: account it and run the state machine to its next request
-  __device__ __forceinline__ bool feed(int job_) {
+  __device__ __forceinline__ int feed(int job_) {
     job = job_;
     pid = J.ids[job];
     const int N = nreq();
@@ -324,19 +355,186 @@ struct Dg {
       const long long q = (long long)(fabs(qlb0()[0]) * 1e6);
       if (q % J.fail_mod == 0) ((int*)in.status)[wg] = 4;
     }
-    const bool more = s->phase == HEXT ? on_hext() : on_verif();
-    if (more) return true;
-    return s->phase == SWEEP ? sweep() : false;   // one inlined copy of the sweep (with its RK4)
+    const int more = s->phase == HEXT ? on_hext() : (on_verif() ? 1 : 0);
+    if (more) return more;
+    return s->phase == SWEEP && sweep() ? 1 : 0;   // one inlined copy of the sweep (with its RK4)
+  }
+
+  // one perturbed restart of the horizon extension (:138-174): the cost direction p and the free initial
+  // positions (the double: ran, q_init_oth and store_ic) move by <= 0.01, drawn from stream 2
+  __device__ __forceinline__ void perturb() {
+#pragma clang fp contract(off)
+    const double q_min = J.q_min, q_max = J.q_max, eps = J.eps;
+    double* P = pp();
+    double *lb0 = qlb0(), *ub0 = qub0();
+    const int js = s->joint_sel;
+    if constexpr (GRAV) {
+      double r0 = s->ran[0], r1 = s->ran[1];
+      { const double a = rng_random(); const double c = rng_pm1(); r0 = r0 + a * c * 0.01; }
+      { const double a = rng_random(); const double c = rng_pm1(); r1 = r1 + a * c * 0.01; }
+      double rr[2] = {r0, r1};
+      const double nw = np_norm<2>(rr);
+      if (js == 0) { P[0] = r0 / nw; P[1] = r1 / nw; }
+      else { P[0] = r1 / nw; P[1] = r0 / nw; }
+      P[2] = 0.0;
+      double qo = s->q_init_oth;
+      { const double a = rng_random(); const double c = rng_pm1(); qo = qo + a * c * 0.01; }
+      if (qo > q_max - eps) qo = qo - eps;
+      if (qo < q_min + eps) qo = qo + eps;
+      const int jo = 1 - js;
+      lb0[jo] = qo; ub0[jo] = qo;
+      s->ran[0] = r0; s->ran[1] = r1; s->q_init_oth = qo;
+      s->store_ic[0] = (double)(s->vel_sel + 1 + js); s->store_ic[1] = r0; s->store_ic[2] = r1; s->store_ic[3] = qo;
+    } else {
+      double rans[NQ];
+      UNR for (int k = 0; k < NQ; ++k) {
+        const double a = rng_random();
+        const double c = rng_pm1();
+        rans[k] = P[k] + a * c * 0.01;
+      }
+      const double nw = np_norm<NQ>(rans);
+      UNR for (int k = 0; k < NQ; ++k) P[k] = rans[k] / nw;
+      P[NQ] = 0.0;
+      const double a = rng_random();
+      const double c = rng_pm1();
+      const double dev = a * c * 0.01;
+      UNR for (int j = 0; j < NQ; ++j) {
+        if (j != js) {
+          double val = lb0[j] + dev;
+          if (val > q_max - eps) val = val - eps;
+          if (val < q_min + eps) val = val + eps;
+          lb0[j] = val;
+          ub0[j] = val;
+        }
+      }
+    }
+  }
+
+  // ---- Speculative restarts ----
+  // A horizon-extension solve that fails (status != 0, in practice max_iter = 1000) is repeated with a
+  // perturbed problem, up to 10 attempts in all; the perturbations depend only on the problem's random
+  // stream, not on the failed solves, so the inputs of every later attempt - assuming the ones before it
+  // fail too - are known as soon as the first failure is.  The slowest problems of a launch are exactly
+  // such chains (10 x 1000 SQP iterations in a row on one wave, the launch tail).  At the first failure
+  // the owner publishes an event (a snapshot of its restart state) and queues the later attempts as jobs
+  // that idle or free waves solve in parallel; the owner walks the chain in order, taking a job's result
+  // when another wave solved it and solving it itself otherwise, and cancels the event at the first
+  // success.  Results are those of the sequential chain (same inputs, same deterministic solver); unused
+  // speculative solves are counted apart (spec_count) and never in the solve statistics.
+  enum : int { H_N = 0, H_JS, H_VS, H_QIS, H_QFS, H_RAN, H_QO = H_RAN + 2, H_IC, H_RNG = H_IC + 4, H_PID, H_NJOBS,
+               H_P, H_LB = H_P + NP, H_UB = H_LB + NXR, H_END = H_UB + NXR };
+  static_assert(H_END <= DG_SPEC_HDR, "event header");
+  __device__ __forceinline__ double* spec_hdr(int ev) const { return J.spec + (long long)ev * J.spec_stride; }
+  __device__ __forceinline__ double* spec_res(int ev, int j) const {
+    return spec_hdr(ev) + DG_SPEC_HDR + (long long)(j - 1) * (4 + (J.nmax + 1) * NXR + J.nmax * NU);
+  }
+  __device__ __forceinline__ bool claim(int ev, int j) const {
+    int r = 0;
+    if (t == 0) r = atomicCAS(&J.spec_claim[ev * (DG_SPEC_JOBS + 1) + j], 0, 1) == 0 ? 1 : 0;
+    return __builtin_amdgcn_readfirstlane(__shfl(r, 0)) != 0;
+  }
+  __device__ __forceinline__ void cancel_event() {
+    const int ev = s->spec_ev;
+    if (ev >= 0 && t == 0) __hip_atomic_store(&J.spec_cancel[ev], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s->spec_ev = -1;
+  }
+  // publish the restart state of attempt `att` (already perturbed into p / q_init) and queue attempts
+  // att + 1 .. 10 as jobs 1 .. 10 - att
+  __device__ __forceinline__ void spawn(int att, int N) {
+    if (J.spec_events <= 0) return;
+    unsigned e = 0;
+    if (t == 0) e = atomicAdd(J.spec_ev_next, 1u);
+    const int ev = __builtin_amdgcn_readfirstlane(__shfl((int)e, 0));
+    if (ev >= J.spec_events) return;   // pool exhausted: this chain runs sequentially
+    const int nj = 10 - att;
+    double* h = spec_hdr(ev);
+    const double *P = pp(), *lb0 = qlb0(), *ub0 = qub0();
+    st_coh(h + H_N, N); st_coh(h + H_JS, s->joint_sel); st_coh(h + H_VS, s->vel_sel);
+    st_coh(h + H_QIS, s->q_init_sel); st_coh(h + H_QFS, s->q_fin_sel);
+    st_coh(h + H_RAN, s->ran[0]); st_coh(h + H_RAN + 1, s->ran[1]); st_coh(h + H_QO, s->q_init_oth);
+    UNR for (int c = 0; c < 4; ++c) st_coh(h + H_IC + c, s->store_ic[c]);
+    st_coh(h + H_RNG, s->rng_pos); st_coh(h + H_PID, (double)pid); st_coh(h + H_NJOBS, nj);
+    UNR for (int c = 0; c < NP; ++c) st_coh(h + H_P + c, P[c]);
+    UNR for (int c = 0; c < NXR; ++c) { st_coh(h + H_LB + c, lb0[c]); st_coh(h + H_UB + c, ub0[c]); }
+    if (t == 0) {
+      const unsigned q = atomicAdd(J.spec_q_tail, (unsigned)nj);
+      for (int j = 1; j <= nj; ++j) st_flag(&J.spec_q[q + j - 1], ev * (DG_SPEC_JOBS + 1) + j + 1);
+    }
+    s->spec_ev = ev;
+    s->spec_base = att;
+  }
+  // the owner takes job j's result (solved by another wave) as its own solve of the current attempt
+  __device__ __forceinline__ void take_result(int ev, int j, int N) {
+    const int* dn = &J.spec_done[ev * (DG_SPEC_JOBS + 1) + j];
+    while (ld_flag(dn) == 0) __builtin_amdgcn_s_sleep(8);
+    const double* r = spec_res(ev, j);
+    for (int e = t; e < (N + 1) * NXR; e += 64) ((double*)in.xo)[row(0) * NXR + e] = ld_coh(r + 4 + e);
+    for (int e = t; e < N * NU; e += 64)
+      ((double*)in.uo)[((long long)wg * J.nmax) * NU + e] = ld_coh(r + 4 + (J.nmax + 1) * NXR + e);
+    ((int*)in.status)[wg] = (int)ld_coh(r);
+    ((double*)in.cost)[wg] = ld_coh(r + 1);
+    ((int*)in.sqp_iter)[wg] = (int)ld_coh(r + 2);
+    ((int*)in.qp_iter)[wg] = (int)ld_coh(r + 3);
+    request(N);
+    if (t == 0) atomicAdd(&J.spec_count[1], 1ull);
+    __syncthreads();
+  }
+  // a free wave runs job j of event ev: the owner's restart state plus j perturbations, straight guess
+  __device__ __forceinline__ void spec_prepare(int ev, int j) {
+    const double* h = spec_hdr(ev);
+    const int N = (int)ld_coh(h + H_N);
+    pid = (long long)ld_coh(h + H_PID);
+    s->joint_sel = (int)ld_coh(h + H_JS); s->vel_sel = (int)ld_coh(h + H_VS);
+    s->q_init_sel = ld_coh(h + H_QIS); s->q_fin_sel = ld_coh(h + H_QFS);
+    s->ran[0] = ld_coh(h + H_RAN); s->ran[1] = ld_coh(h + H_RAN + 1); s->q_init_oth = ld_coh(h + H_QO);
+    UNR for (int c = 0; c < 4; ++c) s->store_ic[c] = ld_coh(h + H_IC + c);
+    s->rng_pos = (int)ld_coh(h + H_RNG);
+    double *P = pp(), *lb0 = qlb0(), *ub0 = qub0();
+    UNR for (int c = 0; c < NP; ++c) P[c] = ld_coh(h + H_P + c);
+    UNR for (int c = 0; c < NXR; ++c) { lb0[c] = ld_coh(h + H_LB + c); ub0[c] = ld_coh(h + H_UB + c); }
+    set_bounds();
+    for (int k = 0; k < j; ++k) perturb();
+    __syncthreads();
+    straight_guess(N, qlb0());
+    ((int*)in.N)[wg] = N;
+  }
+  __device__ __forceinline__ void spec_store(int ev, int j) {
+    const int N = nreq();
+    double* r = spec_res(ev, j);
+    for (int e = t; e < (N + 1) * NXR; e += 64) st_coh(r + 4 + e, xo(0)[e]);
+    for (int e = t; e < N * NU; e += 64) st_coh(r + 4 + (J.nmax + 1) * NXR + e, uo(0)[e]);
+    st_coh(r, (double)status()); st_coh(r + 1, in.cost[wg]);
+    st_coh(r + 2, (double)in.sqp_iter[wg]); st_coh(r + 3, (double)in.qp_iter[wg]);
+    if (t == 0) {
+      st_flag(&J.spec_done[ev * (DG_SPEC_JOBS + 1) + j], 1);
+      atomicAdd(&J.spec_count[0], 1ull);
+    }
+  }
+
+  // the bounds every OCP_solve of data_generation passes (:381-393)
+  __device__ __forceinline__ void set_bounds() {
+    const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max;
+    double* lbx = (double*)in.lbx + (long long)wg * NXR; double* ubx = (double*)in.ubx + (long long)wg * NXR;
+    double* lbxe = (double*)in.lbxe + (long long)wg * NXR; double* ubxe = (double*)in.ubxe + (long long)wg * NXR;
+    double* lbu = (double*)in.lbu + (long long)wg * NU; double* ubu = (double*)in.ubu + (long long)wg * NU;
+    UNR for (int j = 0; j < NQ; ++j) {
+      lbx[j] = q_min; ubx[j] = q_max; lbx[NQ + j] = v_min; ubx[NQ + j] = v_max;
+      lbxe[j] = q_min; ubxe[j] = q_max; lbxe[NQ + j] = 0.0; ubxe[NQ + j] = 0.0;
+      lbu[j] = -J.u_max; ubu[j] = J.u_max;
+    }
+    lbx[NX] = J.dt; ubx[NX] = J.dt; lbxe[NX] = J.dt; ubxe[NX] = J.dt;
   }
 
   // ---- horizon extension (:105-174) ----
-  __device__ __forceinline__ bool on_hext() {
+  // returns 0: no solve pending (sweep or done), 1: solve the request, 2: the request's result is in place
+  __device__ __forceinline__ int on_hext() {
 #pragma clang fp contract(off)
     const int status = this->status();
     const double q_min = J.q_min, q_max = J.q_max, eps = J.eps;
     int N = s->N;
     s->ext += 1;
     if (status == 0) {
+      cancel_event();   // a success ends the chain of failed attempts the event speculated on
       const double cost_new = in.cost[wg];
       if (cost_new > s->cost - J.tol) {
         sweep_init();
@@ -347,62 +545,33 @@ struct Dg {
       N = N + 1;
       s->N = N;
     } else {
-      double* P = pp();
-      double *lb0 = qlb0(), *ub0 = qub0();
-      const int js = s->joint_sel;
-      if constexpr (GRAV) {
-        double r0 = s->ran[0], r1 = s->ran[1];
-        { const double a = rng_random(); const double c = rng_pm1(); r0 = r0 + a * c * 0.01; }
-        { const double a = rng_random(); const double c = rng_pm1(); r1 = r1 + a * c * 0.01; }
-        double rr[2] = {r0, r1};
-        const double nw = np_norm<2>(rr);
-        if (js == 0) { P[0] = r0 / nw; P[1] = r1 / nw; }
-        else { P[0] = r1 / nw; P[1] = r0 / nw; }
-        P[2] = 0.0;
-        double qo = s->q_init_oth;
-        { const double a = rng_random(); const double c = rng_pm1(); qo = qo + a * c * 0.01; }
-        if (qo > q_max - eps) qo = qo - eps;
-        if (qo < q_min + eps) qo = qo + eps;
-        const int jo = 1 - js;
-        lb0[jo] = qo; ub0[jo] = qo;
-        s->ran[0] = r0; s->ran[1] = r1; s->q_init_oth = qo;
-        s->store_ic[0] = (double)(s->vel_sel + 1 + js); s->store_ic[1] = r0; s->store_ic[2] = r1; s->store_ic[3] = qo;
-      } else {
-        double rans[NQ];
-        UNR for (int k = 0; k < NQ; ++k) {
-          const double a = rng_random();
-          const double c = rng_pm1();
-          rans[k] = P[k] + a * c * 0.01;
-        }
-        const double nw = np_norm<NQ>(rans);
-        UNR for (int k = 0; k < NQ; ++k) P[k] = rans[k] / nw;
-        P[NQ] = 0.0;
-        const double a = rng_random();
-        const double c = rng_pm1();
-        const double dev = a * c * 0.01;
-        UNR for (int j = 0; j < NQ; ++j) {
-          if (j != js) {
-            double val = lb0[j] + dev;
-            if (val > q_max - eps) val = val - eps;
-            if (val < q_min + eps) val = val + eps;
-            lb0[j] = val;
-            ub0[j] = val;
+      perturb();
+      __syncthreads();
+      s->cost = 1e6;
+      if (s->ext < 10) {
+        // the next attempt (ext + 1) repeats with perturbed p / q_init: speculate on the ones after it
+        const int att = s->ext + 1;
+        const int ev = s->spec_ev;
+        const int j = att - s->spec_base;
+        if (ev >= 0 && j >= 1 && j <= DG_SPEC_JOBS && j <= 10 - s->spec_base) {
+          if (!claim(ev, j)) {            // another wave solves / solved this attempt: take its result
+            take_result(ev, j, N);
+            return 2;
           }
+        } else if (ev < 0) {
+          spawn(att, N);
         }
       }
-      double qpos[NQ];
-      UNR for (int j = 0; j < NQ; ++j) qpos[j] = lb0[j];
-      __syncthreads();
-      straight_guess(N, qpos);
-      s->cost = 1e6;
+      straight_guess(N, qlb0());
     }
     if (s->ext >= 10) {     // all 10 solves used without an accepted horizon: None
+      cancel_event();
       s->fail = 1;
       s->phase = DONE;
       return false;
     }
     request(N);
-    return true;
+    return 1;
   }
 
   // ---- sweep along the optimal trajectory (:177-365) ----
@@ -626,7 +795,7 @@ __device__ __forceinline__ bool dg_start(const DgJobs* J, const Inputs* in, int 
   return D.start(job);
 }
 template <int NQ>
-__device__ __forceinline__ bool dg_feed(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+__device__ __forceinline__ int dg_feed(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
   Dg<NQ> D(*J, *in, wg, t);
   return D.feed(job);
 }
@@ -635,10 +804,26 @@ __device__ __forceinline__ void dg_finish(const DgJobs* J, const Inputs* in, int
   Dg<NQ> D(*J, *in, wg, t);
   D.finish(job);
 }
+template <int NQ>
+__device__ __forceinline__ void dg_spec_prepare(const DgJobs* J, const Inputs* in, int wg, int t, int ev, int j) {
+  Dg<NQ> D(*J, *in, wg, t);
+  D.spec_prepare(ev, j);
+}
+template <int NQ>
+__device__ __forceinline__ void dg_spec_store(const DgJobs* J, const Inputs* in, int wg, int t, int ev, int j) {
+  Dg<NQ> D(*J, *in, wg, t);
+  D.spec_store(ev, j);
+}
 
-// one workgroup = one wave = one problem's whole data_generation at a time; `in` is the Inputs batch of
-// one problem per workgroup (the wave solver works on problem index wg of it, as k_wave on a pid), `inp`
-// a device copy of it for the state machine's calls
+// wave-uniform value of lane 0
+__device__ __forceinline__ int dg_bcast(int v) { return __builtin_amdgcn_readfirstlane(__shfl(v, 0)); }
+
+// one workgroup = one wave: it owns one problem's whole data_generation at a time, or - once the problem
+// queue is drained - runs one speculative restart solve for another problem's owner (they shorten the
+// chains of failing solves that make the launch tail).  `in` is the Inputs batch of one problem per workgroup (the wave solver works on problem index wg
+// of it, as k_wave on a pid), `inp` a device copy of it for the state machine.  A wave with nothing to do
+// waits (s_sleep) while other waves' problems may still publish restart jobs, and leaves once every
+// problem is finished - an exit every wave reaches.
 template <int NQ, bool FM>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WavesPerEu<NQ>::v, WavesPerEu<NQ>::v)))
 void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJobs jb) {
@@ -646,31 +831,86 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
   const int t = (int)threadIdx.x;
   const int wg = (int)blockIdx.x;
   Coop<NQ, FM> C(smem, gptr(jb.regions) + (long long)wg * jb.region_doubles, w, o, t);
+  const int count = J->count;
+  const bool spec = J->spec_events > 0;
   for (;;) {
-    unsigned idx = 0;
-    if (t == 0) idx = atomicAdd(jb.next, 1u);
-    idx = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl((int)idx, 0));
-    if (idx >= (unsigned)jb.count) break;
-    bool more = dg_start<NQ>(J, inp, wg, t, (int)idx);
-    while (more) {
-      __syncthreads();
-      int it = 0, qit = 0;
-      Lane<NQ> chk(w, o, 0u);
-      if (!chk.supported(in, wg)) {
-        if (t == 0) {
-          in.status[wg] = 5;
-          in.sqp_iter[wg] = 0;
-          in.qp_iter[wg] = 0;
-        }
-      } else {
-        C.from_inputs(in, wg);
-        const int status = C.run(it, qit);
-        C.store(in, wg, status, it, qit);
+    int mode = 0, idx = 0, ev = 0, jj = 0, code = 0;
+    // 1. the next problem
+    {
+      int got = -1;
+      if (t == 0 && __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)count) {
+        const unsigned i = atomicAdd(jb.next, 1u);
+        if (i < (unsigned)count) got = (int)i;
       }
-      __syncthreads();
-      more = dg_feed<NQ>(J, inp, wg, t, (int)idx);
+      got = dg_bcast(got);
+      if (got >= 0) {
+        idx = got;
+        mode = 1;
+        code = dg_start<NQ>(J, inp, wg, t, idx) ? 1 : 0;
+      }
     }
-    dg_finish<NQ>(J, inp, wg, t, (int)idx);
+    // 2. no problem left: a queued speculative restart of a chain that is still running (they only run
+    //    on waves the problem queue no longer feeds, so they never take throughput from the bulk)
+    if (mode == 0 && spec) {
+      int got = -1;
+      if (t == 0) {
+        const unsigned h = __hip_atomic_load(J->spec_q_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned tl = __hip_atomic_load(J->spec_q_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned hh = h;
+        if (h < tl && __hip_atomic_compare_exchange_strong(J->spec_q_head, &hh, h + 1, __ATOMIC_RELAXED,
+                                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          int e;
+          while ((e = ld_flag(&J->spec_q[h])) == 0) __builtin_amdgcn_s_sleep(2);
+          got = e - 1;
+        }
+      }
+      got = dg_bcast(got);
+      if (got >= 0) {
+        ev = got / (DG_SPEC_JOBS + 1);
+        jj = got % (DG_SPEC_JOBS + 1);
+        int ok = 0;
+        if (t == 0 && ld_flag(&J->spec_cancel[ev]) == 0)
+          ok = atomicCAS(&J->spec_claim[ev * (DG_SPEC_JOBS + 1) + jj], 0, 1) == 0 ? 1 : 0;
+        if (!dg_bcast(ok)) continue;
+        dg_spec_prepare<NQ>(J, inp, wg, t, ev, jj);
+        mode = 2;
+        code = 1;
+      }
+    }
+    // 3. nothing to do: leave once every problem is finished, else wait for restart jobs
+    if (mode == 0) {
+      int fin = 0;
+      if (t == 0) fin = __hip_atomic_load(J->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)count;
+      if (dg_bcast(fin) || !spec) break;
+      __builtin_amdgcn_s_sleep(64);
+      continue;
+    }
+    while (code) {
+      if (code == 1) {
+        __syncthreads();
+        int it = 0, qit = 0;
+        Lane<NQ> chk(w, o, 0u);
+        if (!chk.supported(in, wg)) {
+          if (t == 0) {
+            in.status[wg] = 5;
+            in.sqp_iter[wg] = 0;
+            in.qp_iter[wg] = 0;
+          }
+        } else {
+          C.from_inputs(in, wg);
+          const int status = C.run(it, qit);
+          C.store(in, wg, status, it, qit);
+        }
+        __syncthreads();
+      }
+      if (mode == 1) {
+        code = dg_feed<NQ>(J, inp, wg, t, idx);
+      } else {
+        dg_spec_store<NQ>(J, inp, wg, t, ev, jj);
+        code = 0;
+      }
+    }
+    if (mode == 1) dg_finish<NQ>(J, inp, wg, t, idx);
     __syncthreads();
   }
 }

@@ -1357,6 +1357,9 @@ struct vboc_solver {
   Inputs* dg_in = nullptr;
   bool dg_attr[2] = {false, false};
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
+  bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
+  void* dg_spec = nullptr;          // their pool (events, results, control words, queue)
+  size_t dg_spec_bytes = 0;
 };
 
 static void default_opts(Opts& o) {
@@ -1627,6 +1630,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->dg_scratch) (void)hipFree(h->dg_scratch);
   if (h->dg_jobs) (void)hipFree(h->dg_jobs);
   if (h->dg_in) (void)hipFree(h->dg_in);
+  if (h->dg_spec) (void)hipFree(h->dg_spec);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   for (auto ev : h->pev) (void)hipEventDestroy(ev);
@@ -1661,6 +1665,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "wave_groups") h->group_cap = (long long)v;
   else if (s == "mall_mib") h->mall_mib = v;
   else if (s == "dg_fail_mod") h->dg_fail_mod = (int)v;
+  else if (s == "dg_speculate") h->dg_speculate = v != 0.0;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
     if (h->profile && h->pev.empty()) {
@@ -1694,6 +1699,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "coop_threshold") *v = h->coop_threshold;
   else if (s == "coop_available") *v = h->coop_ok ? 1.0 : 0.0;
   else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
+  else if (s == "dg_speculate") *v = h->dg_speculate ? 1.0 : 0.0;
   else if (s == "factor_mfma") *v = h->factor_mfma ? 1.0 : 0.0;
   else if (s == "wave_groups") *v = (double)h->n_regions;
   else if (s == "mall_mib") *v = h->mall_mib;
@@ -2004,8 +2010,38 @@ int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
   J.eps = b->eps; J.g = b->g; J.l1 = b->l1; J.l2 = b->l2; J.m1 = b->m1; J.m2 = b->m2;
   J.rows = b->rows; J.rows_cap = b->rows_cap; J.row_off = b->row_off; J.row_cnt = b->row_cnt;
   J.ic = h->nq == 2 ? b->ic : nullptr; J.ic_slot = h->nq == 2 ? b->ic_slot : nullptr; J.stats = b->stats;
-  // counters: [0] job queue, [1] finished problems, [2..3] error flags, [4..5] rows used (u64)
+  // counters: [0] job queue, [1] finished problems, [2..3] error flags, [4..5] rows used (u64),
+  // [6] speculation events, [7] / [8] restart-job queue tail / head, [10..13] speculative solves run / used (u64)
   J.next = h->head; J.done = h->head + 1; J.err = h->head + 2; J.rows_next = (unsigned long long*)(h->head + 4);
+  J.spec_ev_next = h->head + 6; J.spec_q_tail = h->head + 7; J.spec_q_head = h->head + 8;
+  J.spec_count = (unsigned long long*)(h->head + 10);
+  // speculative restarts: one event per failed horizon-extension chain, at most min(B, 8192) per launch
+  J.spec_events = 0; J.spec_stride = 0; J.spec = nullptr;
+  J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = nullptr;
+  size_t spec_ctl = 0;
+  if (h->dg_speculate) {
+    const int E = b->B < 8192 ? b->B : 8192;
+    const long long res = 4 + (long long)(nm + 1) * NXR + (long long)nm * NU;
+    const long long stride = DG_SPEC_HDR + DG_SPEC_JOBS * res;
+    spec_ctl = sizeof(int) * ((size_t)E * (2 * (DG_SPEC_JOBS + 1) + 1 + DG_SPEC_JOBS));
+    const size_t sneed = spec_ctl + sizeof(double) * (size_t)E * (size_t)stride + 256;
+    if (sneed > h->dg_spec_bytes) {
+      if (h->dg_spec) (void)hipFree(h->dg_spec);
+      h->dg_spec = nullptr;
+      h->dg_spec_bytes = 0;
+      if (hipMalloc(&h->dg_spec, sneed) != hipSuccess)
+        return fail(VBOC_ERR_NOMEM, "vboc_data_generation: hipMalloc of the speculation pool");
+      h->dg_spec_bytes = sneed;
+    }
+    int* ci = (int*)h->dg_spec;
+    J.spec_claim = ci; ci += (size_t)E * (DG_SPEC_JOBS + 1);
+    J.spec_done = ci; ci += (size_t)E * (DG_SPEC_JOBS + 1);
+    J.spec_cancel = ci; ci += E;
+    J.spec_q = ci;
+    J.spec = (double*)((char*)h->dg_spec + ((spec_ctl + 255) & ~(size_t)255));
+    J.spec_events = E; J.spec_stride = (int)stride;
+    HIPCHK(hipMemsetAsync(h->dg_spec, 0, spec_ctl, st));
+  }
   HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
   HIPCHK(hipEventRecord(h->ev0, st));
   hipError_t e;
@@ -2015,10 +2051,12 @@ int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
   HIPCHK(hipEventRecord(h->ev1, st));
   h->launches = 1;
   h->coop_count = b->B;
-  HIPCHK(hipMemcpyAsync(h->host_done + 4, h->head, 6 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(h->host_done, h->head, 14 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  const unsigned* c = h->host_done + 4;
+  const unsigned* c = h->host_done;
   b->rows_used = (long long)(((unsigned long long)c[5] << 32) | c[4]);
+  b->spec_solves = (long long)(((unsigned long long)c[11] << 32) | c[10]);
+  b->spec_used = (long long)(((unsigned long long)c[13] << 32) | c[12]);
   if (c[2]) return fail(VBOC_ERR_NOMEM, "vboc_data_generation: the row pool (rows_cap) overflowed");
   if (c[3]) return fail(VBOC_ERR_HIP, "vboc_data_generation: a horizon exceeded nmax (internal error)");
   if (c[1] != (unsigned)b->B) return fail(VBOC_ERR_HIP, "vboc_data_generation: not every problem finished");

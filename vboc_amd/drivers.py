@@ -565,7 +565,7 @@ def data_generation_device(nq, ids, solver, N_start=None, seed=SEED):
         else:
             results.append(samples)
     stats = dict(solves=int(st[:, 0].sum()), rk4=int(st[:, 1].sum()), sqp_iter=int(st[:, 2].sum()), rounds=1,
-                 per_problem=st)
+                 per_problem=st, spec_solves=out["spec_solves"], spec_used=out["spec_used"])
     return results, stats
 
 

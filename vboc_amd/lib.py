@@ -47,7 +47,8 @@ class DgBatch(ctypes.Structure):
                                               "m1", "m2")] + \
                [("rows", ctypes.c_void_p), ("rows_cap", ctypes.c_longlong), ("row_off", ctypes.c_void_p),
                 ("row_cnt", ctypes.c_void_p), ("ic", ctypes.c_void_p), ("ic_slot", ctypes.c_void_p),
-                ("stats", ctypes.c_void_p), ("rows_used", ctypes.c_longlong)]
+                ("stats", ctypes.c_void_p), ("rows_used", ctypes.c_longlong), ("spec_solves", ctypes.c_longlong),
+                ("spec_used", ctypes.c_longlong)]
 
 
 # per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
@@ -222,11 +223,13 @@ class Solver:
                     v_max=sysd.v_max, u_max=sysd.u_max, dt=sysd.dt, tol=sysd.tol, eps=sysd.eps, g=sysd.g,
                     l1=l[0], l2=l[1], m1=m[0], m2=m[1], rows=rows.data_ptr(), rows_cap=rows_cap,
                     row_off=out["row_off"].data_ptr(), row_cnt=out["row_cnt"].data_ptr(), ic=out["ic"].data_ptr(),
-                    ic_slot=out["ic_slot"].data_ptr(), stats=out["stats"].data_ptr(), rows_used=0)
+                    ic_slot=out["ic_slot"].data_ptr(), stats=out["stats"].data_ptr(), rows_used=0, spec_solves=0,
+                    spec_used=0)
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         _check(self.lib.vboc_data_generation(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
         out["rows"] = rows[:b.rows_used]
         out["rows_all"] = rows
+        out["spec_solves"], out["spec_used"] = b.spec_solves, b.spec_used
         return out
 
     def kernel_stats(self):
