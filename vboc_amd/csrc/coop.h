@@ -25,6 +25,21 @@
 // one or two LDS-DMAs); NQ = 4 is the UR5 arm (NX = 8: two outputs per lane, windows of up to three DMAs).
 #pragma once
 
+// ring depths (slots / stages of prefetch) of the factorisation and of the vector / forward / costate
+// recursions; build-time knobs for measurements
+#ifndef VBOC_NSF
+#define VBOC_NSF 4
+#endif
+#ifndef VBOC_DF
+#define VBOC_DF 2
+#endif
+#ifndef VBOC_NSV
+#define VBOC_NSV 8
+#endif
+#ifndef VBOC_DV
+#define VBOC_DV 6
+#endif
+
 namespace vboc {
 
 typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -58,8 +73,8 @@ struct WaveLayout {
   static constexpr int P_FAC = (W_FAC + 127) / 128, P_VEC = (W_VEC + 127) / 128, P_FWD = (W_FWD + 127) / 128,
                        P_COS = (W_COS + 127) / 128;
   static constexpr int P_VMAX = P_VEC > P_FWD ? (P_VEC > P_COS ? P_VEC : P_COS) : (P_FWD > P_COS ? P_FWD : P_COS);
-  static constexpr int RSF = NQ <= 3 ? 256 : 128 * P_FAC, NSF = 4, DF = 2, RSV = NQ <= 3 ? 128 : 128 * P_VMAX,
-                       NSV = 8, DV = 6;
+  static constexpr int RSF = NQ <= 3 ? 256 : 128 * P_FAC, NSF = VBOC_NSF, DF = VBOC_DF,
+                       RSV = NQ <= 3 ? 128 : 128 * P_VMAX, NSV = VBOC_NSV, DV = VBOC_DV;
   static constexpr int RING_D = NSF * RSF > NSV * RSV ? NSF * RSF : NSV * RSV;
   static_assert(OB % 2 == 0 && OZ % 2 == 0 && OD % 2 == 0 && OK % 2 == 0 && OPE % 2 == 0 && OC % 2 == 0 &&
                     OACL % 2 == 0 && OX % 2 == 0,
@@ -1140,14 +1155,16 @@ struct Coop {
       vmwait<(L::DV - 1) * PV>();
       vld(vslot(0), acl, cc, pe);
     }
+    // p_{k+1} reaches every lane by readlane (lane q holds component q): the recursion's dependent chain
+    // carries no LDS round trip
+    double pv[NX];
+    UNR for (int q = 0; q < NX; ++q) pv[q] = rdlane(pcur, q);
     for (int j = 0; j < cnt; ++j) {
       const int k = N - 1 - j;
-      const int rb = L::PV + (j & 1) * NX, wb = L::PV + ((j + 1) & 1) * NX;
       vdma(j + L::DV);
       vmwait<(L::DV - 1) * PV>();   // stage of sweep index j + 1 has landed
       dbg_check(vslot((j + 1) % L::NSV), N - 2 - j >= 1 ? N - 2 - j : 1, L::LO_VEC, L::W_VEC, 2);
-      double pv[NX], an[NX], cn, pn;
-      UNR for (int q = 0; q < NX; ++q) pv[q] = s[rb + q];
+      double an[NX], cn, pn;
       vld(vslot((j + 1) % L::NSV), an, cn, pn);
       __builtin_amdgcn_sched_barrier(0);
       double p0 = cc, p1 = 0.0;
@@ -1155,11 +1172,10 @@ struct Coop {
       UNR for (int q = 1; q < NX; q += 2) p1 += acl[q] * pv[q];
       if (t < NX) s[L::XS + k * NX + t] = pe + pcur;
       pcur = p0 + p1;
-      if (t < NX) s[wb + t] = pcur;
+      UNR for (int q = 0; q < NX; ++q) pv[q] = rdlane(pcur, q);
       UNR for (int q = 0; q < NX; ++q) acl[q] = an[q];
       cc = cn;
       pe = pn;
-      lsync();
     }
     if (t < NX) s[L::PV + t] = pcur;
     __syncthreads();
@@ -1300,27 +1316,25 @@ struct Coop {
         vmwait<(L::DV - 1) * PW>();
         fld(vslot(0), acl, cc);
       }
+      // dx_k reaches every lane by readlane (lane q holds component q): no LDS round trip in the chain
+      double dx[NX];
+      UNR for (int q = 0; q < NX; ++q) dx[q] = s[L::DXV + q];
       for (int j = 0; j < cnt; ++j) {
         const int k = 1 + j;
-        const int rb = L::DXV + (j & 1) * NX, wb = L::DXV + ((j + 1) & 1) * NX;
         wdma(j + L::DV);
         vmwait<(L::DV - 1) * PW>();
         dbg_check(vslot((j + 1) % L::NSV), 2 + j < N ? 2 + j : N - 1, L::LO_FWD, L::W_FWD, 3);
-        double dx[NX], an[NX], cn;
-        UNR for (int q = 0; q < NX; ++q) dx[q] = s[rb + q];
+        double an[NX], cn;
         fld(vslot((j + 1) % L::NSV), an, cn);
         __builtin_amdgcn_sched_barrier(0);
         double p0 = cc, p1 = 0.0;
         UNR for (int q = 0; q < NX; q += 2) p0 += acl[q] * dx[q];
         UNR for (int q = 1; q < NX; q += 2) p1 += acl[q] * dx[q];
         const double dn = p0 + p1;
-        if (t < NX) {
-          s[wb + t] = dn;
-          s[L::XS + (k + 1) * NX + t] = dn;
-        }
+        if (t < NX) s[L::XS + (k + 1) * NX + t] = dn;
+        UNR for (int q = 0; q < NX; ++q) dx[q] = rdlane(dn, q);
         UNR for (int q = 0; q < NX; ++q) acl[q] = an[q];
         cc = cn;
-        lsync();
       }
     }
     __syncthreads();   // dx rows (global) visible to the stage-parallel pass
