@@ -286,6 +286,7 @@ def run(args, engine_factory=None):
             rec["status"].append((out["row_cnt"] >= 0).cpu().numpy())
             rec["kernel_ms"] += engine.kernel_ms()
             rec["launches"] += 1
+            rec["spec"] = (int(out.get("spec_solves", 0)), int(out.get("spec_used", 0)))
 
     if dgl:
         dg_steps(0, args.warmup, False)
@@ -401,7 +402,13 @@ def run(args, engine_factory=None):
     if dgl:
         line["loop"] = {"boundary_problems_per_s": round(problems / elapsed, 2),
                         "solves_per_problem": round(solves / problems, 3),
-                        "samples": int(rows), "samples_per_s": round(rows / elapsed, 1), "tail": tail}
+                        "samples": int(rows), "samples_per_s": round(rows / elapsed, 1), "tail": tail,
+                        "speculative_restarts": {"run_by_other_waves": rec.get("spec", (0, 0))[0],
+                                                 "used": rec.get("spec", (0, 0))[1],
+                                                 "note": "solves of later attempts of failed horizon-extension "
+                                                         "chains run ahead on waves the problem queue no longer "
+                                                         "feeds; only used ones are in value (as the problem's "
+                                                         "own solves)"}}
     if world > 1:
         dist.destroy_process_group()
     return line
