@@ -297,7 +297,11 @@ struct Coop {
   }
 
   // debug (-DVBOC_DBG_CHECK): compare a landed ring window with a direct global read of the same fields
+  // (-DVBOC_DBG_TAGS=mask limits it to the rings whose tag bit is set: 1 factor, 2 vec, 3 fwd, 4 costate)
   __device__ __forceinline__ void dbg_check(int kb, int k, int lo, int W, int tag) const {
+#if defined(VBOC_DBG_CHECK) && defined(VBOC_DBG_TAGS)
+    if (!((VBOC_DBG_TAGS >> tag) & 1)) return;
+#endif
 #ifdef VBOC_DBG_CHECK
     int bad = -1;
     double a0 = 0.0, b0 = 0.0;
@@ -845,10 +849,11 @@ struct Coop {
       if (j >= 1) ring_wb<OK, OC>((j - 1) % L::NSF, k + 1);
       fdma(j + 2);
       SPROF(4)
-      // VMEM ops issued after stage k's DMAs: j = 0: 2P, j = 1: 2P + 1, else 2P + 2
-      if (j == 0) vmwait<2 * P>();
-      else if (j == 1) vmwait<2 * P + 1>();
-      else vmwait<2 * P + 2>();
+      // stage k's DMAs have landed once at most the 2P DMAs issued after them are outstanding.  The wait
+      // counts loads only: the ring_wb stores issued in between complete out of order with the loads, and
+      // counting them (2P + 1 / 2P + 2, as before) let the wait pass with the last part of stage k's window
+      // still in flight whenever they completed first
+      vmwait<2 * P>();
       dbg_check(kb, k, 0, L::W_FAC, 1);
       SPROF(3)
       if (k >= 1) {
@@ -972,9 +977,7 @@ struct Coop {
       const int k = N - 1 - j, kb = fslot(j % L::NSF);
       if (j >= 1) ring_wb<OK, OC>((j - 1) % L::NSF, k + 1);
       fdma(j + 2);
-      if (j == 0) vmwait<2 * P>();
-      else if (j == 1) vmwait<2 * P + 1>();
-      else vmwait<2 * P + 2>();
+      vmwait<2 * P>();   // loads only, as in factor()
       dbg_check(kb, k, 0, L::W_FAC, 1);
       double g0 = s[kb + goff[0]] * gm[0], g1 = s[kb + goff[1]] * gm[1];
       const double hv = s[kb + hoff];
@@ -1516,13 +1519,23 @@ struct Coop {
     const double h = par(PF::H);
     const double sv = par(PF::S) + alpha * st(0, ODZ);
     double val = 0.0, viol = 0.0;
-    for (int k = t; k <= N; k += 64) {
+    // The arm (NQ = 4) runs the stage trips with a wave-uniform trip count: lanes past N evaluate stage N
+    // and discard it by select (same additions in the same order for the live lanes).  With the usual
+    // `k = t; k <= N; k += 64` loop the last trip runs the rigid-body RK4 (~430 registers, SGPRs spilled to
+    // VGPR lanes, VGPRs to AGPRs) under a partial exec mask, and that build returned wrong merit values on a
+    // few problems per batch: longer line searches than the oracle's, 3 % SQP-iteration agreement
+    // (profiles/r02p_ur5_merit_bisect.log).
+    constexpr bool UNI = NQ == 4;
+    for (int k0 = UNI ? 0 : t; k0 <= N; k0 += 64) {
+      const bool live = !UNI || k0 + t <= N;
+      const int k = UNI ? (live ? k0 + t : N) : k0;
+      auto acc = [live](double& a, double x) { a = live ? a + x : a; };
       const gdouble* rec = &g[(long long)k * REC];
       UNR for (int i = 0; i < NZ; ++i) {
         double lb, ub;
         if (!box(k, i, lb, ub)) continue;
         const double v = rec[OZ + i] + alpha * rec[ODZ + i];
-        viol += fmax(0.0, lb - v) + fmax(0.0, v - ub);
+        acc(viol, fmax(0.0, lb - v) + fmax(0.0, v - ub));
       }
       if (k > 0) {
         const gdouble* rp = &g[(long long)(k - 1) * REC];
@@ -1537,11 +1550,11 @@ struct Coop {
         rk4<NQ>(h, xp, up, phi);
         UNR for (int i = 0; i < NX; ++i) {
           const double xn = rec[OZ + i] + alpha * rec[ODZ + i];
-          val += rp[OWPI + i] * fabs(phi[i] - xn);
+          acc(val, rp[OWPI + i] * fabs(phi[i] - xn));
         }
         if (k == N) {
           UNR for (int j = 0; j < NQ; ++j)
-            val += par(PF::WNU + j) * fabs(rec[OZ + NQ + j] + alpha * rec[ODZ + NQ + j] - par(PF::VFIN + j));
+            acc(val, par(PF::WNU + j) * fabs(rec[OZ + NQ + j] + alpha * rec[ODZ + NQ + j] - par(PF::VFIN + j)));
         }
       }
     }
