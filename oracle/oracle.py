@@ -21,7 +21,9 @@ class Opts(ctypes.Structure):
                 ("alpha_min", ctypes.c_double), ("alpha_reduction", ctypes.c_double),
                 ("lm", ctypes.c_double), ("mu0", ctypes.c_double), ("ipm_push", ctypes.c_double),
                 ("ipm_tau", ctypes.c_double), ("qp_tol_stat", ctypes.c_double),
-                ("qp_tol_eq", ctypes.c_double), ("qp_tol_comp", ctypes.c_double)]
+                ("qp_tol_eq", ctypes.c_double), ("qp_tol_comp", ctypes.c_double),
+                ("hc", ctypes.c_int), ("hc_xc", ctypes.c_double), ("hc_yc", ctypes.c_double),
+                ("hc_lh", ctypes.c_double), ("hc_uh", ctypes.c_double)]
 
 
 RESULT_DTYPE = np.dtype([("status", "i4"), ("sqp_iter", "i4"), ("qp_iter", "i4"), ("pad", "i4"),
@@ -114,17 +116,36 @@ def solve_batch(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe
     return x_out, u_out, res
 
 
+def cartesian_opts():
+    """vboc_opts_t fields of the Cartesian double pendulum's keep-out circle (vboc_amd.systems)."""
+    from vboc_amd.systems import cartesian_constraint
+    c = cartesian_constraint()
+    return dict(hc=1, hc_xc=c.x_c, hc_yc=c.y_c, hc_lh=c.lh, hc_uh=c.uh)
+
+
+def hc_value(x):
+    """h(x) of the keep-out circle for rows x[..., :2] (the chain tip's squared distance to the centre)."""
+    from vboc_amd.systems import cartesian_constraint, system
+    c, l = cartesian_constraint(), system(2).l
+    X = l[0] * np.sin(x[..., 0]) + l[1] * np.sin(x[..., 1])
+    Y = l[0] * np.cos(x[..., 0]) + l[1] * np.cos(x[..., 1])
+    return (X - c.x_c) ** 2 + (Y - c.y_c) ** 2
+
+
 class DriverBackend:
     """The oracle behind the batched drivers' backend interface (vboc_amd.drivers: solve(batch),
     rk4(x, u, T)) - the CPU baseline of bench.py's dg-loop leg and the tests' reference runs."""
     nmax = 512
 
-    def __init__(self, nq, nthreads=None):
+    def __init__(self, nq, nthreads=None, **opts):
+        """opts: vboc_opts_t fields, e.g. the Cartesian keep-out circle (cartesian_opts())."""
         self.nq, self.nthreads = nq, nthreads
+        self.opts = opts
 
     def solve(self, b, free_time=False):
+        o = default_opts(**self.opts) if self.opts else None
         xo, uo, r = solve_batch(self.nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
-                                b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], nthreads=self.nthreads,
+                                b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], opts=o, nthreads=self.nthreads,
                                 free_time=free_time)
         return dict(status=np.array(r["status"]), x=xo, u=uo, cost=np.array(r["cost"]),
                     sqp_iter=np.array(r["sqp_iter"]), qp_iter=np.array(r["qp_iter"]))

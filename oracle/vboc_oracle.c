@@ -406,6 +406,13 @@ typedef struct {
   double d[NZ], daff[NZ];
   double K[NU * NX], kf[NU], Lr[(NU + 1) * (NU + 1)], M[(NU + 1) * NQ], Y[(NU + 1) * NQ], Pe[NX];
   double qpi[NX];              /* QP costate (recovered) */
+  /* Cartesian path constraint lh <= h(x_k) <= uh (stages 1..N-1, see hc_on) */
+  double hv, hg[NQ];           /* h(x_k) and dh/dtheta at the iterate */
+  double hll, hlu;             /* NLP multipliers */
+  double hL, hU;               /* bounds of c'dz in step space */
+  double htl, htu, hql, hqu;   /* QP slacks and their duals */
+  double hr0l, hr0u;           /* slack residuals at the QP start (current = rs * r0) */
+  double hatl, hatu, haql, haqu;  /* affine (predictor) directions of slacks and duals */
 } stage_t;
 
 typedef struct {
@@ -423,6 +430,7 @@ typedef struct {
   /* QP bookkeeping */
   double S[NQ * NQ], lin_e[NQ];
   double rs;                                    /* residual scale prod(1 - alpha) */
+  int hc;                                       /* Cartesian path constraint on (opts.hc) */
 } prob_t;
 
 /* number of step variables of stage k and their kind */
@@ -455,6 +463,28 @@ static void comp(const prob_t* P, int k, int i, double* val, double* lb, double*
 
 static double cost_grad(const prob_t* P, int k, int i) { return (k == 0 && i == 0) ? P->cs : 0.0; }
 
+/* Cartesian path constraint of VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160:
+ *   h(x) = (sum_j l_j sin th_j - x_c)^2 + (sum_j l_j cos th_j - y_c)^2,  lh <= h(x_k) <= uh
+ * on the path stages (ACADOS con_h_expr).  Stage 0's positions are fixed, so there h is a constant:
+ * it is checked once before the solve (vboc_oracle_solve), and the QP carries the constraint on
+ * stages 1..N-1 as a general row c'dz in [lh - h, uh - h] with c = dh/dtheta (exact_hess_constr = 0:
+ * no constraint curvature in the Hessian) and slack variables (HPIPM's general-constraint form). */
+static int hc_on(const prob_t* P, int k) { return P->hc && k >= 1 && k < P->N; }
+static double hc_eval(const prob_t* P, const double* x, double* grad) {
+  const int nq = P->m.nq;
+  double X = 0.0, Y = 0.0;
+  for (int j = 0; j < nq; ++j) { X += P->m.l[j] * sin(x[j]); Y += P->m.l[j] * cos(x[j]); }
+  const double dx = X - P->o.hc_xc, dy = Y - P->o.hc_yc;
+  if (grad)
+    for (int j = 0; j < nq; ++j) grad[j] = 2.0 * dx * (P->m.l[j] * cos(x[j])) - 2.0 * dy * (P->m.l[j] * sin(x[j]));
+  return dx * dx + dy * dy;
+}
+static double hc_dot(const prob_t* P, const stage_t* s, const double* d) {
+  double t = 0.0;
+  for (int j = 0; j < P->m.nq; ++j) t += s->hg[j] * d[j];
+  return t;
+}
+
 static void set_x0(prob_t* P) {
   const int nq = P->m.nq;
   for (int j = 0; j < nq; ++j) { P->st[0].x[j] = P->q0[j]; P->st[0].x[nq + j] = P->s * P->dir[j]; }
@@ -472,6 +502,7 @@ static void linearize(prob_t* P) {
     double phi[NX];
     rk4_sens(&P->m, P->h, s->x, s->u, phi, s->A, s->B);
     for (int i = 0; i < nx; ++i) s->b[i] = phi[i] - P->st[k + 1].x[i];
+    if (hc_on(P, k)) s->hv = hc_eval(P, s->x, s->hg);
   }
   /* F0 = [A0 g, B0], g = [0; dir] */
   stage_t* s0 = &P->st[0];
@@ -503,6 +534,7 @@ static void nlp_residuals(const prob_t* P, double* rstat, double* req, double* r
         if (i < nx) {
           for (int r = 0; r < nx; ++r) gr += s->A[r * nx + i] * s->pi[r];
           gr -= P->st[k - 1].pi[i];
+          if (hc_on(P, k) && i < nq) gr += s->hg[i] * (s->hlu - s->hll);
         } else {
           for (int r = 0; r < nx; ++r) gr += s->B[r * nu + (i - nx)] * s->pi[r];
         }
@@ -515,6 +547,10 @@ static void nlp_residuals(const prob_t* P, double* rstat, double* req, double* r
         in = fmax(in, fmax(lb - v, v - ub));
         cp = fmax(cp, fmax(fabs(s->ll[i] * (v - lb)), fabs(s->lu[i] * (ub - v))));
       }
+    }
+    if (hc_on(P, k)) {
+      in = fmax(in, fmax(P->o.hc_lh - s->hv, s->hv - P->o.hc_uh));
+      cp = fmax(cp, fmax(fabs(s->hll * (s->hv - P->o.hc_lh)), fabs(s->hlu * (P->o.hc_uh - s->hv))));
     }
   }
   *rstat = st; *req = eq; *rineq = in; *rcomp = cp;
@@ -613,6 +649,7 @@ static int newton_solve(prob_t* P, int factor, double* nu_new) {
         for (int i = 0; i < nx; ++i)
           for (int j = 0; j < nx; ++j) {
             double t = (i == j) ? s->H[i] : 0.0;
+            if (hc_on(P, k) && i < nq && j < nq) t += (s->hql / s->htl + s->hqu / s->htu) * s->hg[i] * s->hg[j];
             for (int q = 0; q < nx; ++q) t += AP[i * nx + q] * s->A[q * nx + j];
             for (int a = 0; a < nu; ++a) t += Sux[a * nx + i] * s->K[a * nx + j];
             Pn[i * nx + j] = t;
@@ -726,6 +763,18 @@ static void mr_add(minratio_t* m, double t, double dt) {
 }
 
 /* returns 0 converged, 1 max-iter (usable step), -1 failure */
+/* Newton directions of the path constraint's slacks and duals from the step d of stage s (smu = 0 and
+   zero affine directions give the predictor's) */
+static void hc_dir(const prob_t* P, const stage_t* s, double smu, double* dtl, double* dtu, double* dql,
+                   double* dqu) {
+  const double cd = hc_dot(P, s, s->d), rl = P->rs * s->hr0l, ru = P->rs * s->hr0u;
+  const double rcl = smu - s->htl * s->hql - s->hatl * s->haql, rcu = smu - s->htu * s->hqu - s->hatu * s->haqu;
+  *dtl = cd + rl;
+  *dtu = ru - cd;
+  *dql = (rcl - s->hql * *dtl) / s->htl;
+  *dqu = (rcu - s->hqu * *dtu) / s->htu;
+}
+
 static int qp_solve(prob_t* P, int* iters) {
   const int nx = P->m.nx, nu = P->m.nu, nq = P->m.nq, N = P->N;
   const vboc_opts_t* o = &P->o;
@@ -750,6 +799,23 @@ static int qp_solve(prob_t* P, int* iters) {
     }
   }
   for (int j = 0; j < nq; ++j) P->qnu[j] = 0.0;
+  /* path constraint rows: slacks from the initial c'dz, clipped to ipm_push (infeasible start,
+     the residual r0 is driven out like the dynamics residual) */
+  for (int k = 1; k < N; ++k) {
+    if (!hc_on(P, k)) continue;
+    stage_t* s = &P->st[k];
+    const double gd = hc_dot(P, s, s->dz);
+    s->hL = o->hc_lh - s->hv;
+    s->hU = o->hc_uh - s->hv;
+    s->htl = fmax(gd - s->hL, o->ipm_push);
+    s->htu = fmax(s->hU - gd, o->ipm_push);
+    s->hql = o->mu0 / s->htl;
+    s->hqu = o->mu0 / s->htu;
+    s->hr0l = gd - s->hL - s->htl;
+    s->hr0u = s->hU - gd - s->htu;
+    s->hatl = s->hatu = s->haql = s->haqu = 0.0;
+    nbox += 2;
+  }
   /* initial residuals: dynamics e0, terminal e0_N (stored in st[N].e0[0..nq)) */
   double e00 = 0.0, rd0 = 0.0;
   for (int k = 0; k < N; ++k) {
@@ -773,8 +839,11 @@ static int qp_solve(prob_t* P, int* iters) {
   }
   for (int k = 0; k <= N; ++k) {
     const stage_t* s = &P->st[k];
+    const int hk = hc_on(P, k);
+    if (hk) e00 = fmax(e00, fmax(fabs(s->hr0l), fabs(s->hr0u)));
     for (int i = 0; i < nz_of(P, k); ++i)
-      rd0 = fmax(rd0, fabs(rho * s->dz[i] + cost_grad(P, k, i) - s->ql[i] + s->qu[i]));
+      rd0 = fmax(rd0, fabs(rho * s->dz[i] + cost_grad(P, k, i) - s->ql[i] + s->qu[i] +
+                           ((hk && i < nq) ? s->hg[i] * (s->hqu - s->hql) : 0.0)));
   }
   P->rs = 1.0;
   int it, status = 1;
@@ -788,6 +857,7 @@ static int qp_solve(prob_t* P, int* iters) {
         if (!isfinite(s->Lb[i])) continue;
         mu += (s->dz[i] - s->Lb[i]) * s->ql[i] + (s->Ub[i] - s->dz[i]) * s->qu[i];
       }
+      if (hc_on(P, k)) mu += s->htl * s->hql + s->htu * s->hqu;
     }
     mu /= (double)nbox;
     if (!isfinite(mu)) { status = -1; break; }
@@ -802,6 +872,11 @@ static int qp_solve(prob_t* P, int* iters) {
           H += s->ql[i] * itl + s->qu[i] * itu;
         }
         s->H[i] = H; s->g[i] = g;
+      }
+      if (hc_on(P, k)) {
+        s->hatl = s->hatu = s->haql = s->haqu = 0.0;
+        const double gam = s->hql * (P->rs * s->hr0l) / s->htl - s->hqu * (P->rs * s->hr0u) / s->htu;
+        for (int j = 0; j < nq; ++j) s->g[j] += s->hg[j] * gam;
       }
     }
     if (newton_solve(P, 1, nu_new)) { status = -1; break; }
@@ -818,6 +893,15 @@ static int qp_solve(prob_t* P, int* iters) {
         mr_add(&ma, s->ql[i], dll);
         mr_add(&ma, s->qu[i], dlu);
       }
+      if (hc_on(P, k)) {
+        double dtl, dtu, dql, dqu;
+        hc_dir(P, s, 0.0, &dtl, &dtu, &dql, &dqu);
+        s->hatl = dtl; s->hatu = dtu; s->haql = dql; s->haqu = dqu;
+        mr_add(&ma, s->htl, dtl);
+        mr_add(&ma, s->htu, dtu);
+        mr_add(&ma, s->hql, dql);
+        mr_add(&ma, s->hqu, dqu);
+      }
     }
     const double aa = ma.n / ma.d;
     double muaff = 0.0;
@@ -829,6 +913,8 @@ static int qp_solve(prob_t* P, int* iters) {
         double dll = -s->ql[i] - s->ql[i] * d * itl, dlu = -s->qu[i] + s->qu[i] * d * itu;
         muaff += (tl + aa * d) * (s->ql[i] + aa * dll) + (tu - aa * d) * (s->qu[i] + aa * dlu);
       }
+      if (hc_on(P, k))
+        muaff += (s->htl + aa * s->hatl) * (s->hql + aa * s->haql) + (s->htu + aa * s->hatu) * (s->hqu + aa * s->haqu);
     }
     muaff /= (double)nbox;
     double sig = muaff / mu;
@@ -845,6 +931,12 @@ static int qp_solve(prob_t* P, int* iters) {
         double rl = smu - tl * s->ql[i] - d * dll;
         double ru = smu - tu * s->qu[i] + d * dlu;
         s->g[i] = rho * s->dz[i] + cost_grad(P, k, i) - s->ql[i] - rl * itl + s->qu[i] + ru * itu;
+      }
+      if (hc_on(P, k)) {
+        const double rl = P->rs * s->hr0l, ru = P->rs * s->hr0u;
+        const double rcl = smu - s->htl * s->hql - s->hatl * s->haql, rcu = smu - s->htu * s->hqu - s->hatu * s->haqu;
+        const double gam = -s->hql + s->hqu - (rcl - s->hql * rl) / s->htl + (rcu - s->hqu * ru) / s->htu;
+        for (int j = 0; j < nq; ++j) s->g[j] += s->hg[j] * gam;
       }
     }
     if (newton_solve(P, 0, nu_new)) { status = -1; break; }
@@ -863,6 +955,14 @@ static int qp_solve(prob_t* P, int* iters) {
         mr_add(&mx, s->ql[i], dll);
         mr_add(&mx, s->qu[i], dlu);
       }
+      if (hc_on(P, k)) {
+        double dtl, dtu, dql, dqu;
+        hc_dir(P, s, smu, &dtl, &dtu, &dql, &dqu);
+        mr_add(&mx, s->htl, dtl);
+        mr_add(&mx, s->htu, dtu);
+        mr_add(&mx, s->hql, dql);
+        mr_add(&mx, s->hqu, dqu);
+      }
     }
     const double amax = mx.n / mx.d;
     double alpha = fmin(1.0, o->ipm_tau * amax);
@@ -880,6 +980,12 @@ static int qp_solve(prob_t* P, int* iters) {
           s->qu[i] += alpha * dlu;
         }
         s->dz[i] += alpha * d;
+      }
+      if (hc_on(P, k)) {
+        double dtl, dtu, dql, dqu;
+        hc_dir(P, s, smu, &dtl, &dtu, &dql, &dqu);
+        s->htl += alpha * dtl; s->htu += alpha * dtu;
+        s->hql += alpha * dql; s->hqu += alpha * dqu;
       }
     }
     for (int j = 0; j < nq; ++j) P->qnu[j] += alpha * (nu_new[j] - P->qnu[j]);
@@ -903,6 +1009,7 @@ static int qp_solve(prob_t* P, int* iters) {
       double ln[NX];
       for (int i = 0; i < nx; ++i) {
         double t = rho * s->dz[i] - s->ql[i] + s->qu[i];
+        if (hc_on(P, k) && i < nq) t += s->hg[i] * (s->hqu - s->hql);
         for (int q = 0; q < nx; ++q) t += s->A[q * nx + i] * lam[q];
         ln[i] = t;
       }
@@ -944,6 +1051,10 @@ static double merit(const prob_t* P, double alpha) {
     rk4(&P->m, P->h, xk, uk, phi);
     for (int i = 0; i < nx; ++i) xn[i] = s1->x[i] + alpha * s1->dz[i];
     for (int i = 0; i < nx; ++i) val += P->st[k].wpi[i] * fabs(phi[i] - xn[i]);
+    if (hc_on(P, k + 1)) {
+      const double hv = hc_eval(P, xn, NULL);
+      val += P->wbnd * (fmax(0.0, P->o.hc_lh - hv) + fmax(0.0, hv - P->o.hc_uh));
+    }
     memcpy(xk, xn, sizeof(xk));
     if (k + 1 < N) for (int a = 0; a < nu; ++a) uk[a] = s1->u[a] + alpha * s1->dz[nx + a];
   }
@@ -978,6 +1089,7 @@ static void sqp(prob_t* P, vboc_result_t* res) {
       stage_t* s = &P->st[k];
       if (k < N) for (int i = 0; i < nx; ++i) s->wpi[i] = wupd(s->wpi[i], s->qpi[i]);
       for (int i = 0; i < nz_of(P, k); ++i) lmax = fmax(lmax, fmax(s->ql[i], s->qu[i]));
+      if (hc_on(P, k)) lmax = fmax(lmax, fmax(s->hql, s->hqu));
     }
     for (int j = 0; j < nq; ++j) P->wnu[j] = wupd(P->wnu[j], P->qnu[j]);
     P->wbnd = wupd(P->wbnd, lmax);
@@ -1009,6 +1121,10 @@ static void sqp(prob_t* P, vboc_result_t* res) {
         s->ll[i] += alpha * (s->ql[i] - s->ll[i]);
         s->lu[i] += alpha * (s->qu[i] - s->lu[i]);
       }
+      if (hc_on(P, k)) {
+        s->hll += alpha * (s->hql - s->hll);
+        s->hlu += alpha * (s->hqu - s->hlu);
+      }
       if (k < N) for (int i = 0; i < nx; ++i) s->pi[i] += alpha * (s->qpi[i] - s->pi[i]);
     }
     for (int j = 0; j < nq; ++j) P->nu[j] += alpha * (P->qnu[j] - P->nu[j]);
@@ -1034,6 +1150,7 @@ void vboc_oracle_default_opts(vboc_opts_t* o) {
   /* QP: tol_stat from qp_solver_tol_stat = 1e-3 (triplependulum_class_vboc.py:135); the other
      HPIPM tolerances keep their library defaults (1e-8). */
   o->qp_tol_stat = 1e-3; o->qp_tol_eq = 1e-8; o->qp_tol_comp = 1e-8;
+  o->hc = 0; o->hc_xc = o->hc_yc = o->hc_lh = o->hc_uh = 0.0;
 }
 
 void vboc_oracle_model(int nq, const double* th, const double* om, const double* u, double* acc,
@@ -1095,7 +1212,23 @@ int vboc_oracle_solve(int nq, int N, const double* x_guess, const double* u_gues
     for (int i = 0; i < 2 * nq; ++i) P.st[k].x[i] = x_guess[k * nxr + i];
     if (k < N) for (int a = 0; a < nq; ++a) P.st[k].u[a] = u_guess[k * nq + a];
   }
-  sqp(&P, res);
+  P.hc = opts->hc != 0;
+  if (P.hc && !P.m.chain) { free(P.st); return -2; }  /* the Cartesian constraint is the chains' tip */
+  int infeasible0 = 0;
+  if (P.hc) {
+    /* stage 0: positions fixed, h constant - an initial state inside the keep-out region makes every
+       QP infeasible; reported as a QP failure without iterating */
+    const double h0 = hc_eval(&P, P.q0, NULL);
+    infeasible0 = !(h0 >= opts->hc_lh && h0 <= opts->hc_uh);
+  }
+  if (infeasible0) {
+    memset(res, 0, sizeof(*res));
+    res->status = 4;
+    res->cost = NAN;
+    set_x0(&P);
+  } else {
+    sqp(&P, res);
+  }
   for (int k = 0; k <= N; ++k) {
     for (int i = 0; i < 2 * nq; ++i) x_out[k * nxr + i] = P.st[k].x[i];
     x_out[k * nxr + 2 * nq] = P.h;

@@ -11,6 +11,11 @@ typedef struct {
   double alpha_min, alpha_reduction, lm;
   double mu0, ipm_push, ipm_tau;
   double qp_tol_stat, qp_tol_eq, qp_tol_comp;
+  /* Cartesian path constraint (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160):
+     hc != 0 => hc_lh <= (sum_j l sin th_j - hc_xc)^2 + (sum_j l cos th_j - hc_yc)^2 <= hc_uh at
+     stages 0..N-1 of the pendulum chains (nq 2, 3) */
+  int hc;
+  double hc_xc, hc_yc, hc_lh, hc_uh;
 } vboc_opts_t;
 
 typedef struct {

@@ -10,7 +10,10 @@ from scipy.optimize import minimize
 import oracle
 
 
-def slsqp(nq, b, i, maxiter=500):
+def slsqp(nq, b, i, maxiter=500, hc=None):
+    """hc: optional (x_c, y_c, lh, uh) - the Cartesian keep-out circle lh <= |tip(x_k) - c|^2 <= uh on
+    stages 1..N-1 (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160), written here
+    independently of the oracle as SLSQP inequality constraints with their own Jacobian."""
     N = int(b["N"][i])
     h = b["lbx"][i, 2 * nq]
     p = b["p"][i]
@@ -65,9 +68,36 @@ def slsqp(nq, b, i, maxiter=500):
     lo = [bb[0] if bb[0] is not None else -1e9 for bb in bounds]
     hi = [bb[1] if bb[1] is not None else 1e9 for bb in bounds]
     z0 = np.clip(z0, lo, hi)
+    cons = [dict(type="eq", fun=eq, jac=eqjac)]
+    if hc is not None:
+        xc, yc, lh, uh = hc
+        L = np.full(nq, 0.8)
+
+        def tip(X):
+            return (np.sin(X[1:N, :nq]) @ L - xc, np.cos(X[1:N, :nq]) @ L - yc)
+
+        def ineq(z):
+            _, X = unpack(z)
+            dx, dy = tip(X)
+            hv = dx * dx + dy * dy
+            return np.r_[hv - lh, uh - hv]
+
+        def ineqjac(z):
+            _, X = unpack(z)
+            dx, dy = tip(X)
+            J = np.zeros((2 * (N - 1), nv))
+            for k in range(1, N):
+                g = 2 * dx[k - 1] * L * np.cos(X[k, :nq]) - 2 * dy[k - 1] * L * np.sin(X[k, :nq])
+                c0 = 1 + N * nq + (k - 1) * nx
+                J[k - 1, c0:c0 + nq] = g
+                J[N - 1 + k - 1, c0:c0 + nq] = -g
+            return J
+        cons.append(dict(type="ineq", fun=ineq, jac=ineqjac))
     r = minimize(lambda z: cs * z[0], z0, jac=lambda z: np.r_[cs, np.zeros(nv - 1)], bounds=bounds,
-                 constraints=[dict(type="eq", fun=eq, jac=eqjac)], method="SLSQP",
-                 options=dict(maxiter=maxiter, ftol=1e-10))
+                 constraints=cons, method="SLSQP", options=dict(maxiter=maxiter, ftol=1e-10))
+    if hc is not None:
+        _, X = unpack(r.x)
+        return r.fun, bool(r.success), float(np.abs(eq(r.x)).max()), float(ineq(r.x)[:N - 1].min())
     return r.fun, bool(r.success), float(np.abs(eq(r.x)).max())
 
 

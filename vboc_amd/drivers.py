@@ -647,6 +647,71 @@ def ur5_set(results):
 
 
 # ------------------------------------------------------------------------------------------------
+# Cartesian double pendulum (VBOC/Cartesian constraints/): the main block of vboc_multiprocessing.py fans
+# `testing_test` (:19-129) out over Pool(30) for the 1k test set (:557-562) and the 100k training set
+# (:567-585), on OCPdoublependulumINIT with the end-effector keep-out circle (the solver backend must carry
+# systems.cartesian_constraint()).  Same state machine as the UR5's: extend N while the cost drops by more
+# than tol, return [x_0] (5 values, dt included: ocp_solver.get(0, "x")); a failed solve returns None.
+# ------------------------------------------------------------------------------------------------
+def cartesian_problem(pid, U, N_start=100):
+    """Generator for one Cartesian `testing_test` problem; U: the problem's uniform block
+    (ics.CART_STREAM), drawn in the reference's order (:33-50)."""
+    from .ics import CART_DRAWS
+    sysd = system(2)
+    tol = sysd.tol                                # nlp_solver_tol_stat (:547)
+    v_max, v_min, q_max, q_min, tau_max, dt = sysd.v_max, -sysd.v_max, sysd.q_max, sysd.q_min, sysd.u_max, sysd.dt
+    draw = iter(float(v) for v in U[:CART_DRAWS])
+    pick = lambda seq: seq[min(int(next(draw) * len(seq)), len(seq) - 1)]
+    p = np.zeros(3)
+    for j in range(2):
+        r = next(draw)
+        p[j] = r * pick([-1, 1])
+    p = p / norm(p)
+    q_init_lb, q_init_ub = np.full(5, v_min), np.full(5, v_max)
+    q_init_lb[-1] = q_init_ub[-1] = dt
+    q0 = np.empty(2)
+    for j in range(2):
+        q0[j] = q_min + next(draw) * (q_max - q_min)
+        q_init_lb[j] = q_init_ub[j] = q0[j]
+    q_lb, q_ub = q_init_lb.copy(), q_init_ub.copy()
+    q_lb[:2], q_ub[:2] = q_min, q_max
+    u_lb, u_ub = np.full(2, -tau_max), np.full(2, tau_max)
+    q_fin_lb, q_fin_ub = q_lb.copy(), q_ub.copy()
+    q_fin_lb[2:4] = q_fin_ub[2:4] = 0.0
+    N = N_start
+    x_guess = np.zeros(5)
+    x_guess[:2] = q0
+    x_guess[-1] = dt
+    xg = np.tile(x_guess, (N, 1))
+    ug = np.zeros((N, 2))
+    cost_old = 1e6
+    while True:
+        res = yield Solve(N, xg, ug, p, q_lb, q_ub, u_lb, u_ub, q_init_lb, q_init_ub, q_fin_lb, q_fin_ub)
+        if res.status != 0:
+            return None
+        if res.cost > cost_old - tol:
+            return [res.x[0].copy()]
+        cost_old = res.cost
+        xg = np.empty((N + 1, 5))
+        ug = np.empty((N + 1, 2))
+        xg[:N] = res.x[:N]
+        ug[:N] = res.u[:N]
+        xg[N] = res.x[N]
+        ug[N] = 0.0
+        N = N + 1
+
+
+def cartesian_testing_batch(ids, backend, N_start=100, seed=SEED):
+    """`testing_test(v)` of the Cartesian driver for every problem id, batched.  Returns (results, stats):
+    results[i] is [x_0] (5 floats) or None.  `backend` solves with the keep-out circle."""
+    from .ics import CART_DRAWS, CART_STREAM
+    ids = np.asarray(ids)
+    U = uniforms(ids, CART_DRAWS, seed, stream=CART_STREAM)
+    gens = [cartesian_problem(int(pid), U[b], N_start) for b, pid in enumerate(ids)]
+    return run_problems(2, gens, backend, nmax=getattr(backend, "nmax", 200))
+
+
+# ------------------------------------------------------------------------------------------------
 # pendulum VBOC data generation (free-time OCPs)
 # ------------------------------------------------------------------------------------------------
 PEND_N_START, PEND_EPS = 50, 1e-3   # VBOC/pendulum_vboc.py:21, :47

@@ -211,6 +211,34 @@ def ur5_ics(ids, N=100, seed=SEED):
                  ubxe=np.tile(col(np.r_[XMAX[:NQ], np.zeros(NQ)]), (B, 1)))
 
 
+CART_DRAWS = 6   # testing_test of the Cartesian driver: (random, choice) per joint for p, one random per joint
+CART_STREAM = 6
+
+
+def cartesian_ics(ids, N=100, seed=SEED):
+    """First OCP of the Cartesian double pendulum's `testing_test`
+    (VBOC/Cartesian constraints/vboc_multiprocessing.py:19-92), what its main block fans out for the test
+    and training sets (:557-572): p[l] = random() * choice([-1, 1]), normalised; q_init ~ U(q_min, q_max)
+    per joint; velocities free in [-v_max, v_max]; constant guess [q_init, 0, 0, dt]; u = 0.  Philox
+    stream 6.  The keep-out circle is an OCP-level constraint (systems.cartesian_constraint)."""
+    sysd = system(2)
+    ids = np.asarray(ids)
+    B = ids.shape[0]
+    U = uniforms(ids, CART_DRAWS, seed, stream=CART_STREAM)
+    r = np.stack([U[:, 2 * j] * _choice(U[:, 2 * j + 1], [-1.0, 1.0]) for j in range(2)], axis=1)
+    p = np.zeros((B, 3))
+    p[:, :2] = r / _row_norms(r)
+    qi = sysd.q_min + U[:, 4:6] * (sysd.q_max - sysd.q_min)
+    dt = sysd.dt
+    lbx0 = np.concatenate([qi, np.full((B, 2), -sysd.v_max), np.full((B, 1), dt)], axis=1)
+    ubx0 = np.concatenate([qi, np.full((B, 2), sysd.v_max), np.full((B, 1), dt)], axis=1)
+    xg = np.zeros((B, N + 1, 5))
+    xg[:, :, :2] = qi[:, None, :]
+    xg[:, :, 4] = dt
+    b = _bounds(sysd, B, N, xg, np.zeros((B, N, 2)), p, lbx0, ubx0)
+    return b
+
+
 def pendulum_free_time_ics(ids, N_range=(20, 60), seed=SEED):
     """Free-time pendulum OCPs shaped like VBOC/pendulum_vboc.py's solves (OCPpendulum.OCP_solve,
     VBOC/pendulum_class_vboc.py:107-130): sweep direction v_sel = +-v_max (:55-77), a fixed initial

@@ -52,3 +52,21 @@ _SYS = {
 
 def system(nq):
     return _SYS[int(nq)]
+
+
+@dataclass(frozen=True)
+class CartesianConstraint:
+    """End-effector keep-out circle of the Cartesian double pendulum
+    (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160):
+    lh <= (l1 sin th1 + l2 sin th2 - x_c)^2 + (l1 cos th1 + l2 cos th2 - y_c)^2 <= uh on the path stages.
+    The constants are evaluated with the reference's expressions (radius = l2/4, y_c = -l1 - l2/2)."""
+    x_c: float
+    y_c: float
+    lh: float
+    uh: float
+
+
+def cartesian_constraint():
+    l1, l2 = _SYS[2].l
+    radius = l2 / 4
+    return CartesianConstraint(x_c=0.0, y_c=-l1 - l2 / 2, lh=radius ** 2, uh=1e6)
