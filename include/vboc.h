@@ -25,6 +25,8 @@
  *                             state machine of VBOC/triplependulum_vboc.py:19-370 (fan-out :399-405) /
  *                             VBOC/doublependulum_vboc.py:19-403, with its OCP_solve calls (:110,262) and
  *                             twin-integrator steps (:346-353), run on the device
+ *   vboc_set_path_constraint <- model.con_h_expr + constraints.lh / uh of the Cartesian double pendulum
+ *                             (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160)
  *   vboc_destroy           <- solver object destruction (acados_template __del__ -> free)
  *   vboc_last_error        <- Python exceptions raised by acados_template on bad fields
  *
@@ -113,6 +115,17 @@ int vboc_destroy(vboc_handle h);
  * initial position q_0 has int(|q_0| 1e6) % dg_fail_mod == 0, exercising the restart branches). */
 int vboc_set_option(vboc_handle h, const char* field, double value);
 int vboc_get_option(vboc_handle h, const char* field, double* value);
+
+/* Nonlinear path constraint of the OCP (an OCP-level definition, like ACADOS's con_h_expr / lh / uh):
+ *   kind 1: end-effector keep-out circle of the pendulum chain (nq 2 or 3, link length 0.8),
+ *           lh <= (sum_j l sin theta_j - x_c)^2 + (sum_j l cos theta_j - y_c)^2 <= uh
+ *           on stages 0..N-1 (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160);
+ *           at stage 0 the positions are fixed, so a problem whose initial position violates it gets
+ *           status 4 (QP failure) without iterating;
+ *   kind 0: no path constraint (the default).
+ * Solves with the constraint run on the lane-per-problem kernels (wave_all is ignored); the free-time
+ * solver and vboc_data_generation refuse a handle that carries one (VBOC_ERR_UNSUPPORTED). */
+int vboc_set_path_constraint(vboc_handle h, int kind, double x_c, double y_c, double lh, double uh);
 
 /* Batched solve, every pointer a DEVICE pointer (inputs resident in HBM).  Kernels are enqueued on
  * `stream`; the call returns when every problem of the batch is finished (the SQP/IPM loops are

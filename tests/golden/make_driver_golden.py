@@ -29,9 +29,12 @@ The UR5's `testing_test` (VBOC/UR5/vboc_multiprocessing_ur5.py:369-466, what tha
 out for its test and training sets) is extracted the same way and run against the drop-in OCPUR5INIT
 (vboc_amd.ur5) with the oracle injected; `random` serves the problem's ics.UR5_STREAM block.
 
-Usage: python tests/golden/make_driver_golden.py [dg|test|pend|ur5]
+The Cartesian double pendulum's `testing_test` (VBOC/Cartesian constraints/vboc_multiprocessing.py:19-129) is
+run the same way on the drop-in vboc_amd.cartesian.OCPdoublependulumINIT (keep-out circle on the oracle).
+
+Usage: python tests/golden/make_driver_golden.py [dg|test|pend|ur5|cart]
   ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json, tests/golden/driver_1.json,
-      tests/golden/testing_ur5.json
+      tests/golden/testing_ur5.json, tests/golden/testing_cartesian.json
 """
 import ast
 import json
@@ -262,6 +265,36 @@ def main_ur5():
                    "results": out}, f)
 
 
+CART_IDS = list(range(0, 48))
+CART_FAIL_MOD = 11   # a few forced failures on top of the infeasible initial positions
+
+
+def main_cartesian():
+    """The Cartesian double pendulum's `testing_test` (VBOC/Cartesian constraints/vboc_multiprocessing.py:19-129)
+    on the drop-in vboc_amd.cartesian.OCPdoublependulumINIT (keep-out circle) with the oracle injected."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_backend import OracleOcpBackend
+    from vboc_amd import ocp as dropin
+    from vboc_amd.cartesian import OCPdoublependulumINIT
+    from vboc_amd.ics import CART_DRAWS, CART_STREAM
+    dropin.use_backend(OracleOcpBackend(CART_FAIL_MOD))
+    code = extract(os.path.join(REF, "Cartesian constraints", "vboc_multiprocessing.py"), "testing_test")
+    ocp = OCPdoublependulumINIT()
+    g = dict(np=np, norm=norm, ocp=ocp, system_sel=2, v_max=ocp.dthetamax, v_min=-ocp.dthetamax,
+             q_max=ocp.thetamax, q_min=ocp.thetamin, tau_max=ocp.Cmax, dt_sym=1e-2, N_start=100,
+             tol=ocp.ocp.solver_options.nlp_solver_tol_stat)
+    exec(code, g)
+    U = uniforms(np.array(CART_IDS), CART_DRAWS, SEED, stream=CART_STREAM)
+    out = []
+    for b, pid in enumerate(CART_IDS):
+        g["random"] = FakeRandom(U[b], ProblemRNG(pid, SEED, stream=CART_STREAM + 1))
+        out.append(tolist(g["testing_test"](pid)))
+        print("cartesian", pid, out[-1], flush=True)
+    with open(os.path.join(HERE, "testing_cartesian.json"), "w") as f:
+        json.dump({"nq": 2, "ids": CART_IDS, "N_start": 100, "seed": SEED, "fail_mod": CART_FAIL_MOD,
+                   "results": out}, f)
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("dg", "all"):
@@ -272,3 +305,5 @@ if __name__ == "__main__":
         main_pendulum()
     if what in ("ur5", "all"):
         main_ur5()
+    if what in ("cart", "all"):
+        main_cartesian()

@@ -20,11 +20,14 @@ def forced_failure(q0, fail_mod):
     return fail_mod > 0 and int(abs(float(q0)) * 1e6) % fail_mod == 0
 
 
-def _oracle_solve(nq, b, fail_mod=0, free_time=False):
+def _oracle_solve(nq, b, fail_mod=0, free_time=False, hc=None):
     import oracle
+    o = None
+    if hc is not None:
+        o = oracle.default_opts(hc=1, hc_xc=hc.x_c, hc_yc=hc.y_c, hc_lh=hc.lh, hc_uh=hc.uh)
     xo, uo, r = oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"],
                                    b["lbu"], b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"],
-                                   free_time=free_time)
+                                   opts=o, free_time=free_time)
     st = np.array(r["status"], copy=True)
     for i in range(st.shape[0]):
         if forced_failure(b["lbx0"][i, 0], fail_mod):
@@ -36,11 +39,11 @@ class OracleBackend:
     """Batched drivers' backend on the oracle."""
     nmax = 512
 
-    def __init__(self, nq, fail_mod=0):
-        self.nq, self.fail_mod = nq, fail_mod
+    def __init__(self, nq, fail_mod=0, path_constraint=None):
+        self.nq, self.fail_mod, self.hc = nq, fail_mod, path_constraint
 
     def solve(self, b, free_time=False):
-        return _oracle_solve(self.nq, b, self.fail_mod, free_time)
+        return _oracle_solve(self.nq, b, self.fail_mod, free_time, self.hc)
 
     def rk4(self, x, u, T):
         import oracle
@@ -50,12 +53,15 @@ class OracleBackend:
 class OracleOcpBackend:
     """Drop-in classes' backend on the oracle (vboc_amd.ocp.use_backend)."""
 
-    def __init__(self, fail_mod=0):
-        self.fail_mod = fail_mod
+    def __init__(self, fail_mod=0, path_constraint=None):
+        self.fail_mod, self.hc = fail_mod, path_constraint
+
+    def with_path_constraint(self, c):
+        return OracleOcpBackend(self.fail_mod, c)
 
     def solve_host(self, b, free_time=False):
         nq = b["u_guess"].shape[2]
-        return _oracle_solve(nq, b, self.fail_mod, free_time)
+        return _oracle_solve(nq, b, self.fail_mod, free_time, self.hc)
 
     def rk4(self, nq, T, x, u):
         import oracle

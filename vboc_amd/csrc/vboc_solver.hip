@@ -47,6 +47,10 @@ struct Opts {
   double qp_tol_stat, qp_tol_eq, qp_tol_comp;
   double alpha_min, alpha_red, lm, mu0, push, tau;
   int max_iter, qp_max_iter;
+  // Cartesian path constraint hlh <= |tip(theta_k) - (hxc, hyc)|^2 <= huh on stages 0..N-1 (hc != 0;
+  // vboc_set_path_constraint, VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160)
+  int hc;
+  double hxc, hyc, hlh, huh;
 };
 
 // Slot-major workspace.  Field counts per stage are fixed by NQ.
@@ -56,6 +60,7 @@ struct Work {
   double *DZ, *QL, *QU, *E0;                  // IPM iterate (step, bound duals), initial residual
   double *K, *KF, *LR, *M, *Y, *PE, *D, *DAFF, *QPI;  // Riccati factors, directions, costate
   double *F0, *LR0, *M0, *Y0, *PE0, *PAR;     // stage-0 specials, problem parameters (per slot)
+  double* HC;                                 // path-constraint rows (allocated with the constraint)
   long long S;                                // number of slots (lanes)
 };
 
@@ -110,6 +115,12 @@ struct Lane {
   static constexpr int FX = NX, FU = NU, FPI = NX, FZ = NZ, FA = NX * NX, FB = NX * NU, FK = NU * NX,
                        FLR = NU * NU, FM = NU * NQ;
   using PF = Par<NQ>;
+  // per-stage fields of the Cartesian path-constraint row (w.HC; stages 1..N-1, see hc_on): h and
+  // dh/dtheta at the iterate, NLP multipliers, QP slacks / duals, their residuals at the QP start and
+  // their affine directions
+  enum : int {
+    HV = 0, HG = 1, HLL = 1 + NQ, HLU, HTL, HTU, HQL, HQU, HR0L, HR0U, HATL, HATU, HAQL, HAQU, FHC
+  };
 
   const Work& w;
   const Opts& o;
@@ -150,6 +161,38 @@ struct Lane {
     return (gptr(base) + ((long long)wv * fp(F)) * 128 + ln * 2)[(f >> 1) * 128 + (f & 1)];
   }
   __device__ __forceinline__ gdouble& par(int f) const { return at0(w.PAR, PF::COUNT, f); }
+
+  // ---- Cartesian path constraint (oracle/vboc_oracle.c hc_*): the chain tip's squared distance to the
+  // centre, a general row c'dz in [lh - h, uh - h] with c = dh/dtheta on stages 1..N-1 (stage 0's
+  // positions are fixed: checked once in k_refill) ----
+  __device__ __forceinline__ bool hc_on(int k) const { return o.hc && k >= 1 && k < N; }
+  __device__ __forceinline__ gdouble& hcf(int k, int f) const { return at(w.HC, FHC, k, f); }
+  __device__ __forceinline__ double hc_eval(const double* x, double* grad) const {
+    constexpr double l = Chain<NQ>::l;
+    double X = 0.0, Y = 0.0;
+    UNR for (int j = 0; j < NQ; ++j) { X += l * sin(x[j]); Y += l * cos(x[j]); }
+    const double dx = X - o.hxc, dy = Y - o.hyc;
+    if (grad) {
+      UNR for (int j = 0; j < NQ; ++j) grad[j] = 2.0 * dx * (l * cos(x[j])) - 2.0 * dy * (l * sin(x[j]));
+    }
+    return dx * dx + dy * dy;
+  }
+  // Newton directions of the row's slacks and duals from the stage step d (corrector right-hand sides
+  // with the stored affine directions when CORR, the predictor's otherwise)
+  template <bool CORR>
+  __device__ __forceinline__ void hc_dir(int k, const double (&d)[NZ], double smu, double& dtl, double& dtu,
+                                         double& dql, double& dqu) const {
+    double cd = 0.0;
+    UNR for (int j = 0; j < NQ; ++j) cd += hcf(k, HG + j) * d[j];
+    const double htl = hcf(k, HTL), htu = hcf(k, HTU), hql = hcf(k, HQL), hqu = hcf(k, HQU);
+    const double rl = rs * hcf(k, HR0L), ru = rs * hcf(k, HR0U);
+    const double rcl = CORR ? smu - htl * hql - hcf(k, HATL) * hcf(k, HAQL) : -htl * hql;
+    const double rcu = CORR ? smu - htu * hqu - hcf(k, HATU) * hcf(k, HAQU) : -htu * hqu;
+    dtl = cd + rl;
+    dtu = ru - cd;
+    dql = (rcl - hql * dtl) / htl;
+    dqu = (rcu - hqu * dtu) / htu;
+  }
 
   // ---------------------------------------------------------------------------------------------
   // stage component view: value, bounds, boxed flag of the NZ step components of stage k
@@ -250,6 +293,7 @@ struct Lane {
     for (int k = 0; k <= N; ++k) {
       UNR for (int i = 0; i < NX; ++i) atv(w.X, FX, k, i) = xg[(long long)k * NXR + i];
       UNR for (int i = 0; i < NZ; ++i) { atv(w.LL, FZ, k, i) = 0.0; atv(w.LU, FZ, k, i) = 0.0; }
+      if (o.hc && k >= 1 && k < N) { atv(w.HC, FHC, k, HLL) = 0.0; atv(w.HC, FHC, k, HLU) = 0.0; }
       if (k < N) {
         UNR for (int a = 0; a < NU; ++a) atv(w.U, FU, k, a) = ug[(long long)k * NU + a];
         UNR for (int i = 0; i < NX; ++i) { atv(w.PI, FPI, k, i) = 0.0; atv(w.WPI, FX, k, i) = 0.0; }
@@ -301,6 +345,11 @@ struct Lane {
           if (c < NX) at(w.A, FA, k, i * NX + c) = v;
           else at(w.Bm, FB, k, i * NU + (c - NX)) = v;
         });
+        if (hc_on(k)) {
+          double g[NQ];
+          hcf(k, HV) = hc_eval(xk, g);
+          UNR for (int j = 0; j < NQ; ++j) hcf(k, HG + j) = g[j];
+        }
         UNR for (int i = 0; i < NX; ++i) {
           const double xn = at(w.X, FX, k + 1, i);
           const double b = x1[i] - xn;
@@ -345,6 +394,7 @@ struct Lane {
           if (c < NX) {
             UNR for (int r = 0; r < NX; ++r) gr += at(w.A, FA, k, r * NX + c) * pik[r];
             gr -= pprev[c];
+            if (c < NQ && hc_on(k)) gr += hcf(k, HG + c) * (hcf(k, HLU) - hcf(k, HLL));
           } else {
             UNR for (int r = 0; r < NX; ++r) gr += at(w.Bm, FB, k, r * NU + (c - NX)) * pik[r];
           }
@@ -356,6 +406,11 @@ struct Lane {
         const double ll = at(w.LL, FZ, k, c), lu = at(w.LU, FZ, k, c);
         in = fmax(in, fmax(lb[c] - z[c], z[c] - ub[c]));
         cp = fmax(cp, fmax(fabs(ll * (z[c] - lb[c])), fabs(lu * (ub[c] - z[c]))));
+      }
+      if (hc_on(k)) {
+        const double hv = hcf(k, HV), hll = hcf(k, HLL), hlu = hcf(k, HLU);
+        in = fmax(in, fmax(o.hlh - hv, hv - o.huh));
+        cp = fmax(cp, fmax(fabs(hll * (hv - o.hlh)), fabs(hlu * (o.huh - hv))));
       }
       UNR for (int i = 0; i < NX; ++i) pprev[i] = pik[i];
     }
@@ -396,7 +451,7 @@ struct Lane {
       double z[NZ], lb[NZ], ub[NZ];
       bool bx[NZ];
       stage_box(k, z, lb, ub, bx);
-      double dz[NZ];
+      double dz[NZ], qlv[NZ], quv[NZ];
       UNR for (int i = 0; i < NZ; ++i) {
         double ql = 0.0, qu = 0.0, d0 = 0.0;
         if (bx[i]) {
@@ -411,8 +466,28 @@ struct Lane {
         at(w.DZ, FZ, k, i) = d0;
         at(w.QL, FZ, k, i) = ql;
         at(w.QU, FZ, k, i) = qu;
-        rd0 = fmax(rd0, fabs(o.lm * d0 + cgrad(k, i) - ql + qu));
+        qlv[i] = ql;
+        quv[i] = qu;
       }
+      double hgam = 0.0, hg[NQ];
+      const bool hk = hc_on(k);
+      if (hk) {
+        // slacks from the initial c'dz, clipped to ipm_push (infeasible start, residual r0 scaled by rs)
+        double gd = 0.0;
+        UNR for (int j = 0; j < NQ; ++j) { hg[j] = hcf(k, HG + j); gd += hg[j] * dz[j]; }
+        const double hv = hcf(k, HV), L = o.hlh - hv, U = o.huh - hv;
+        const double tl = fmax(gd - L, o.push), tu = fmax(U - gd, o.push);
+        const double ql = o.mu0 / tl, qu = o.mu0 / tu;
+        const double r0l = gd - L - tl, r0u = U - gd - tu;
+        hcf(k, HTL) = tl; hcf(k, HTU) = tu; hcf(k, HQL) = ql; hcf(k, HQU) = qu;
+        hcf(k, HR0L) = r0l; hcf(k, HR0U) = r0u;
+        musum += tl * ql + tu * qu;
+        nbox += 2.0;
+        e00 = fmax(e00, fmax(fabs(r0l), fabs(r0u)));
+        hgam = qu - ql;
+      }
+      UNR for (int i = 0; i < NZ; ++i)
+        rd0 = fmax(rd0, fabs(o.lm * dz[i] + cgrad(k, i) - qlv[i] + quv[i] + ((hk && i < NQ) ? hg[i < NQ ? i : 0] * hgam : 0.0)));
       if (k > 0) {
         // residual of stage k-1 dynamics at the initial point
         const int kp = k - 1;
@@ -493,6 +568,19 @@ struct Lane {
           g[i] += -c[i].ql - rl * c[i].itl + c[i].qu + ru * c[i].itu;
         }
       }
+    }
+    if (hc_on(k)) {
+      const double htl = hcf(k, HTL), htu = hcf(k, HTU), hql = hcf(k, HQL), hqu = hcf(k, HQU);
+      const double rl = rs * hcf(k, HR0L), ru = rs * hcf(k, HR0U);
+      double gam;
+      if (corr) {
+        const double rcl = smu - htl * hql - hcf(k, HATL) * hcf(k, HAQL);
+        const double rcu = smu - htu * hqu - hcf(k, HATU) * hcf(k, HAQU);
+        gam = -hql + hqu - (rcl - hql * rl) / htl + (rcu - hqu * ru) / htu;
+      } else {
+        gam = hql * rl / htl - hqu * ru / htu;
+      }
+      UNR for (int j = 0; j < NQ; ++j) g[j] += hcf(k, HG + j) * gam;
     }
   }
 
@@ -632,10 +720,17 @@ struct Lane {
           }
         }
         // Pn = diag(Hx) - W'W + A' P A   (A streamed column by column)
-        double Pn[NX * NX];
+        double Pn[NX * NX], hsig = 0.0, hgk[NQ];
+        const bool hk = hc_on(k);
+        UNR for (int j = 0; j < NQ; ++j) hgk[j] = 0.0;
+        if (hk) {
+          hsig = hcf(k, HQL) / hcf(k, HTL) + hcf(k, HQU) / hcf(k, HTU);
+          UNR for (int j = 0; j < NQ; ++j) hgk[j] = hcf(k, HG + j);
+        }
         UNR for (int i = 0; i < NX; ++i)
           UNR for (int j = 0; j <= i; ++j) {
             double t = (i == j) ? H[i] : 0.0;
+            if (hk && i < NQ && j < NQ) t += hsig * hgk[i < NQ ? i : 0] * hgk[j < NQ ? j : 0];
             UNR for (int a = 0; a < NU; ++a) t -= W[a * NX + i] * W[a * NX + j];
             Pn[i * NX + j] = t;
           }
@@ -845,6 +940,21 @@ struct Lane {
         mr.add(c[i].ql, dll);
         mr.add(c[i].qu, dlu);
       }
+      if (hc_on(k)) {
+        double dtl, dtu, dql, dqu;
+        hc_dir<CORR>(k, d, smu, dtl, dtu, dql, dqu);
+        const double htl = hcf(k, HTL), htu = hcf(k, HTU), hql = hcf(k, HQL), hqu = hcf(k, HQU);
+        if (!CORR) {
+          hcf(k, HATL) = dtl; hcf(k, HATU) = dtu; hcf(k, HAQL) = dql; hcf(k, HAQU) = dqu;
+          c0 += htl * hql + htu * hqu;
+          c1 += htl * dql + dtl * hql + htu * dqu + dtu * hqu;
+          c2 += dtl * dql + dtu * dqu;
+        }
+        mr.add(htl, dtl);
+        mr.add(htu, dtu);
+        mr.add(hql, dql);
+        mr.add(hqu, dqu);
+      }
     }
     amax = mr.value();
   }
@@ -867,6 +977,15 @@ struct Lane {
         at(w.QL, FZ, k, i) = qln;
         at(w.QU, FZ, k, i) = qun;
         musum += (c[i].tl + alpha * d) * qln + (c[i].tu - alpha * d) * qun;
+      }
+      if (hc_on(k)) {
+        double dk[NZ], dtl, dtu, dql, dqu;
+        UNR for (int i = 0; i < NZ; ++i) dk[i] = at(w.D, FZ, k, i);
+        hc_dir<true>(k, dk, smu, dtl, dtu, dql, dqu);
+        const double tl = hcf(k, HTL) + alpha * dtl, tu = hcf(k, HTU) + alpha * dtu;
+        const double ql = hcf(k, HQL) + alpha * dql, qu = hcf(k, HQU) + alpha * dqu;
+        hcf(k, HTL) = tl; hcf(k, HTU) = tu; hcf(k, HQL) = ql; hcf(k, HQU) = qu;
+        musum += tl * ql + tu * qu;
       }
     }
     mu = musum / nbox;
@@ -945,6 +1064,7 @@ struct Lane {
       UNR for (int i = 0; i < NX; ++i) {
         const double dz = at(w.DZ, FZ, k, i);
         double t = o.lm * dz - at(w.QL, FZ, k, i) + at(w.QU, FZ, k, i);
+        if (i < NQ && hc_on(k)) t += hcf(k, HG + (i < NQ ? i : 0)) * (hcf(k, HQU) - hcf(k, HQL));
         UNR for (int q = 0; q < NX; ++q) t += at(w.A, FA, k, q * NX + i) * lam[q];
         ln[i] = t;
       }
@@ -989,6 +1109,10 @@ struct Lane {
           val += at(w.WPI, FX, k - 1, i) * fabs(phi[i] - xn);
           xk[i] = xn;
         }
+        if (hc_on(k)) {
+          const double hv = hc_eval(xk, nullptr);
+          val += par(PF::WBND) * (fmax(0.0, o.hlh - hv) + fmax(0.0, hv - o.huh));
+        }
       }
       if (k < N) {
         if (k == 0) {
@@ -1010,6 +1134,7 @@ struct Lane {
         UNR for (int i = 0; i < NX; ++i) at(w.WPI, FX, k, i) = wupd(at(w.WPI, FX, k, i), at(w.QPI, FPI, k, i));
       }
       UNR for (int i = 0; i < NZ; ++i) lmax = fmax(lmax, fmax(at(w.QL, FZ, k, i), at(w.QU, FZ, k, i)));
+      if (hc_on(k)) lmax = fmax(lmax, fmax((double)hcf(k, HQL), (double)hcf(k, HQU)));
     }
     UNR for (int j = 0; j < NQ; ++j) par(PF::WNU + j) = wupd(par(PF::WNU + j), par(PF::QNU + j));
     par(PF::WBND) = wupd(par(PF::WBND), lmax);
@@ -1032,6 +1157,12 @@ struct Lane {
         gdouble& lu = at(w.LU, FZ, k, i);
         ll += alpha * (at(w.QL, FZ, k, i) - ll);
         lu += alpha * (at(w.QU, FZ, k, i) - lu);
+      }
+      if (hc_on(k)) {
+        gdouble& hll = hcf(k, HLL);
+        gdouble& hlu = hcf(k, HLU);
+        hll += alpha * (hcf(k, HQL) - hll);
+        hlu += alpha * (hcf(k, HQU) - hlu);
       }
       if (k < N) {
         UNR for (int i = 0; i < NX; ++i) {
@@ -1098,6 +1229,23 @@ __global__ __launch_bounds__(256) void k_refill(Work w, Opts o, Inputs in, SlotS
     atomicAdd(ss.done, 1u);
     ss(IS_PID, slot) = -1;   // pull another problem next round
     return;
+  }
+  if (o.hc) {
+    // Cartesian constraint at stage 0: positions fixed, h constant - outside [lh, uh] every QP is
+    // infeasible; reported as a QP failure without iterating (oracle/vboc_oracle.c, vboc_oracle_solve)
+    constexpr int NXR = 2 * NQ + 1;
+    double q0[NQ];
+    UNR for (int j = 0; j < NQ; ++j) q0[j] = in.lbx0[(long long)cand * NXR + j];
+    const double h0 = L.hc_eval(q0, nullptr);
+    if (!(h0 >= o.hlh && h0 <= o.huh)) {
+      in.status[cand] = 4;
+      in.cost[cand] = NAN;
+      in.sqp_iter[cand] = 0;
+      in.qp_iter[cand] = 0;
+      atomicAdd(ss.done, 1u);
+      ss(IS_PID, slot) = -1;
+      return;
+    }
   }
   L.load(in, (int)cand);
   ss(IS_PID, slot) = (int)cand;
@@ -1368,6 +1516,7 @@ static void default_opts(Opts& o) {
   o.alpha_min = 1e-2; o.alpha_red = 0.3; o.lm = 1e-5;
   o.mu0 = 1.0; o.push = 1e-2; o.tau = 0.995;
   o.max_iter = 1000; o.qp_max_iter = 100;
+  o.hc = 0; o.hxc = o.hyc = o.hlh = o.huh = 0.0;
 }
 
 static int par_count(int nq) {
@@ -1601,6 +1750,7 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
   auto take0 = [&](size_t fields) { double* r = p; p += ev(fields) * (size_t)slots; return r; };
   Work& w = h->w;
   w.S = slots;
+  w.HC = nullptr;
   w.X = take(NX); w.U = take(NU); w.PI = take(NX); w.LL = take(NZ); w.LU = take(NZ); w.WPI = take(NX);
   w.A = take(NX * NX); w.Bm = take(NX * NU); w.BD = take(NX);
   w.DZ = take(NZ); w.QL = take(NZ); w.QU = take(NZ); w.E0 = take(NX);
@@ -1622,6 +1772,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->pool) (void)hipFree(h->pool);
   if (h->head) (void)hipFree(h->head);
   if (h->ist) (void)hipFree(h->ist);
+  if (h->w.HC) (void)hipFree(h->w.HC);
   if (h->list) (void)hipFree(h->list);
   if (h->regions) (void)hipFree(h->regions);
   if (h->host_done) (void)hipHostFree(h->host_done);
@@ -1710,6 +1861,26 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   return VBOC_OK;
 }
 
+int vboc_set_path_constraint(vboc_handle h, int kind, double x_c, double y_c, double lh, double uh) {
+  if (!h) return fail(VBOC_ERR_ARG, "vboc_set_path_constraint: NULL handle");
+  if (kind == 0) { h->o.hc = 0; return VBOC_OK; }
+  if (kind != 1) return fail(VBOC_ERR_ARG, "vboc_set_path_constraint: unknown kind");
+  if (h->nq != 2 && h->nq != 3)
+    return fail(VBOC_ERR_UNSUPPORTED, "vboc_set_path_constraint: the keep-out circle needs a pendulum chain (nq 2 or 3)");
+  if (!(lh <= uh)) return fail(VBOC_ERR_ARG, "vboc_set_path_constraint: lh > uh");
+  if (!h->w.HC) {
+    const size_t f = h->nq == 2 ? (size_t)Lane<2>::FHC : (size_t)Lane<3>::FHC;
+    HIPCHK(hipSetDevice(h->device));
+    const hipError_t e = hipMalloc((void**)&h->w.HC, sizeof(double) * ev(f) * (size_t)(h->nmax + 1) * (size_t)h->slots);
+    if (e != hipSuccess) {
+      h->w.HC = nullptr;
+      return fail(VBOC_ERR_NOMEM, "vboc_set_path_constraint: hipMalloc constraint rows");
+    }
+  }
+  h->o.hc = 1; h->o.hxc = x_c; h->o.hyc = y_c; h->o.hlh = lh; h->o.huh = uh;
+  return VBOC_OK;
+}
+
 int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_solve_batch: NULL argument");
   if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_solve_batch: B < 0");
@@ -1741,7 +1912,7 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   SlotState ss{h->ist, h->head + 1, h->head + 2, (unsigned long long*)(h->head + 4), h->slots};
   const dim3 grid((unsigned)(lanes / 256)), block(256);
   HIPCHK(hipEventRecord(h->ev0, st));
-  if (h->wave_all && h->coop_ok) {
+  if (h->wave_all && h->coop_ok && !h->o.hc) {
     // every problem on its own wave, pulled from the input queue (head[0])
     WaveJobs jb{nullptr, b->B, h->head, h->regions, h->region_doubles};
     h->launches = 1;
@@ -1779,7 +1950,7 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
     HIPCHK(hipStreamSynchronize(st));
     h->host_done[0] = h->host_done[5];
     const unsigned pulled = h->host_done[4] < (unsigned)b->B ? h->host_done[4] : (unsigned)b->B;
-    if (h->coop_ok && h->coop_threshold > 0 && h->host_done[4] >= (unsigned)b->B &&
+    if (h->coop_ok && h->coop_threshold > 0 && !h->o.hc && h->host_done[4] >= (unsigned)b->B &&
         (double)(pulled - h->host_done[0]) <= h->coop_threshold && h->host_done[0] < (unsigned)b->B) {
       // queue drained, few problems left: finish each of them on one LDS-resident wave
       HIPCHK(hipMemsetAsync(h->head + 3, 0, sizeof(unsigned), st));
@@ -1853,6 +2024,7 @@ int vboc_kernel_stats(vboc_handle h, double* factor_ms, long long* factor_launch
 
 int vboc_solve_batch_ft(vboc_handle h, const vboc_batch_t* b, void* stream) {
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: NULL argument");
+  if (h->o.hc) return fail(VBOC_ERR_UNSUPPORTED, "vboc_solve_batch_ft: no path constraint in the free-time OCP");
   if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: B < 0");
   if (b->nmax > h->nmax || b->nmax < 1)
     return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: batch nmax exceeds the handle's nmax");
@@ -1948,6 +2120,8 @@ int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_data_generation: NULL argument");
   if (h->nq != 2 && h->nq != 3)
     return fail(VBOC_ERR_UNSUPPORTED, "vboc_data_generation: defined for the double (nq = 2) and triple (nq = 3) pendulum");
+  if (h->o.hc)
+    return fail(VBOC_ERR_UNSUPPORTED, "vboc_data_generation: the VBOC data generation has no path constraint (clear it first)");
   if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_data_generation: B < 0");
   b->rows_used = 0;
   if (b->B == 0) return VBOC_OK;

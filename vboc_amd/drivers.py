@@ -444,12 +444,15 @@ def testing_problem(nq, pid, U, rng, N_start, max_restarts=MAX_TEST_RESTARTS):
 class GpuBackend:
     """The product backend: batched OCP solves and twin steps on the GPU (libvboc_amd)."""
 
-    def __init__(self, nq, nmax=200, device=0, **options):
+    def __init__(self, nq, nmax=200, device=0, path_constraint=None, **options):
+        """path_constraint: systems.CartesianConstraint for the Cartesian double pendulum's OCP."""
         from . import lib
         self.lib = lib
         self.nq = nq
         self.nmax = nmax
         self.solver = lib.Solver(nq, nmax, device=device, **options)
+        if path_constraint is not None:
+            self.solver.set_path_constraint(path_constraint)
 
     def solve(self, batch, free_time=False):
         return self.solver.solve_host(batch, free_time=free_time)

@@ -20,7 +20,8 @@ SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
            "vboc_solve_batch_host", "vboc_solve_batch_ft", "vboc_solve_batch_ft_host", "vboc_rk4_batch", "vboc_rk4_batch_host",
            "vboc_rk4_sens_batch_host", "vboc_last_kernel_ms",
-           "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_last_error")
+           "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_set_path_constraint",
+           "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
 
@@ -84,6 +85,7 @@ def load():
                                 ctypes.POINTER(ctypes.c_void_p)]
     lib.vboc_destroy.argtypes = [ctypes.c_void_p]
     lib.vboc_set_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_double]
+    lib.vboc_set_path_constraint.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_double] * 4
     lib.vboc_get_option.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double)]
     lib.vboc_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch), ctypes.c_void_p]
     lib.vboc_solve_batch_host.argtypes = [ctypes.c_void_p, ctypes.POINTER(Batch)]
@@ -139,6 +141,14 @@ class Solver:
 
     def set_option(self, field, value):
         _check(self.lib.vboc_set_option(self.h, field.encode(), float(value)))
+
+    def set_path_constraint(self, c=None):
+        """The OCP's nonlinear path constraint (vboc_set_path_constraint): c = systems.CartesianConstraint
+        (the keep-out circle of VBOC/Cartesian constraints/), None = none."""
+        if c is None:
+            _check(self.lib.vboc_set_path_constraint(self.h, 0, 0.0, 0.0, 0.0, 0.0))
+        else:
+            _check(self.lib.vboc_set_path_constraint(self.h, 1, float(c.x_c), float(c.y_c), float(c.lh), float(c.uh)))
 
     def get_option(self, field):
         v = ctypes.c_double()

@@ -37,13 +37,17 @@ def use_backend(backend):
     _BACKEND = backend
 
 
-def _shared_solver(nq, nmax):
-    """One HIP handle per (nq, nmax) per process (the reference builds one solver per process)."""
+def _shared_solver(nq, nmax, path_constraint=None):
+    """One HIP handle per (nq, nmax, path constraint) per process (the reference builds one solver per
+    process).  path_constraint: systems.CartesianConstraint of the Cartesian double pendulum, or None."""
     if _BACKEND is not None:
-        return _BACKEND
-    key = (nq, nmax)
+        return _BACKEND if path_constraint is None else _BACKEND.with_path_constraint(path_constraint)
+    key = (nq, nmax, path_constraint)
     if key not in _SOLVERS:
-        _SOLVERS[key] = lib.Solver(nq, nmax, slots=256)
+        s = lib.Solver(nq, nmax, slots=256)
+        if path_constraint is not None:
+            s.set_path_constraint(path_constraint)
+        _SOLVERS[key] = s
     return _SOLVERS[key]
 
 
@@ -77,9 +81,12 @@ class OcpSolver:
         self.nx = 2 * self.nq + 1
         self.nu = self.nq
         self.N = ocp_def.ocp.dims.N
-        self._lib = _shared_solver(self.nq, self.NMAX)
+        self._lib = self._bind()
         self._stats = dict(sqp_iter=0, qp_iter=0, time_tot=0.0, status=0)
         self.reset()
+
+    def _bind(self):
+        return _shared_solver(self.nq, self.NMAX)
 
     # -- AcadosOcpSolver API ----------------------------------------------------------------------
     def reset(self):
