@@ -335,3 +335,12 @@ def test_ur5_run_on_oracle(tmp_path):
     sd = torch.load(tmp_path / "model_4dof_vboc", weights_only=True)
     assert sd["linear_relu_stack.0.weight"].shape == (32, 8)
     assert np.load(tmp_path / "data_4dof_vboc_test.npy").shape == r["X_test"].shape
+    # resume (X_old, VBOC/UR5/vboc_multiprocessing_ur5.py:501,530): the previous rows first, new ids after them
+    r2 = ur5_run(OracleBackend(4), num_test=8, num_train=16, out_dir=str(tmp_path), device="cpu", minibatch=8,
+                 hidden=32, resume=True)
+    n_old = r["X_train"].shape[0]
+    np.testing.assert_array_equal(r2["X_train"][:n_old], r["X_train"])
+    assert r2["X_train"].shape[0] > n_old
+    assert not any((r2["X_train"][n_old:] == row).all(1).any() for row in r["X_train"])
+    assert np.load(tmp_path / "data_4dof_vboc_train.npy").shape == r2["X_train"].shape
+    assert (tmp_path / "data_4dof_vboc_train.next_id").read_text() == str(8 + 24 + 16)

@@ -194,7 +194,7 @@ def pendulum_vboc_run(out_dir=None, device="cuda", seed=0, backend=None, it_max=
 
 
 def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device="cuda", seed=0,
-            minibatch=1 << 15, hidden=1000, log=None):
+            minibatch=1 << 15, hidden=1000, log=None, resume=False):
     """VBOC/UR5/vboc_multiprocessing_ur5.py's main block (config 5) on one GPU:
       test set      `testing_test` over ids [0, num_test) (:487-498)      -> data_4dof_vboc_test.npy
       training set  `testing_test` over ids [num_test, + num_train) (:506-528) -> data_4dof_vboc_train.npy
@@ -203,9 +203,12 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
       fit           NeuralNetDIR(8, 1000, 1), Adam lr 1e-3, minibatch 2^15, EMA beta 0.95, stop at val <= 1e-3
                     or it_max = 20 * int(n * 100 / 2^15) steps (:530-595), on the HIP-graph trainer
       RMSE          on the training and the test data (:597-625); artefacts model_/mean_/std_4dof_vboc.
-    Difference: the reference appends the new rows to a training set loaded from a previous run (X_old,
-    :501, :530); here the run starts from an empty one.  Returns dict(X_test, X_train, fit, rmse_train,
-    rmse_test, stats)."""
+    resume: the reference appends the new rows to the training set of a previous run (X_old = np.load of
+    data_4dof_vboc_train.npy, :501; X_tot = concatenate((X_old, X_save)), :530) and fits on all of it.  With
+    resume=True and out_dir holding a previous run, X_old is loaded the same way and the new problems continue
+    after the previous run's ids (data_4dof_vboc_train.next_id, written by every run), so a resumed run adds
+    new initial states instead of repeating the Philox-keyed ones.  Returns dict(X_test, X_train, fit,
+    rmse_train, rmse_test, stats)."""
     import torch
     from .drivers import GpuBackend, ur5_set, ur5_testing_batch
     log = log or (lambda *a: None)
@@ -215,9 +218,19 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
     X_test = ur5_set(res)
     log(f"test set: {X_test.shape[0]} rows of {num_test} in {time.time() - t0:.1f} s")
     t1 = time.time()
-    res, st_train = ur5_testing_batch(np.arange(num_test, num_test + num_train), backend)
-    X_train = ur5_set(res)
-    log(f"training set: {X_train.shape[0]} rows of {num_train} in {time.time() - t1:.1f} s")
+    first, X_old = num_test, np.zeros((0, 8))
+    old_path = os.path.join(out_dir, "data_4dof_vboc_train.npy") if out_dir else None
+    if resume:
+        if not (old_path and os.path.exists(old_path)):
+            raise FileNotFoundError("ur5_run(resume=True) needs out_dir with a previous data_4dof_vboc_train.npy")
+        X_old = np.load(old_path)                      # allow_pickle=False: plain float64 rows
+        with open(old_path[:-4] + ".next_id") as f:
+            first = int(f.read())
+    res, st_train = ur5_testing_batch(np.arange(first, first + num_train), backend)
+    X_save = ur5_set(res)
+    X_train = np.concatenate((X_old, X_save))
+    log(f"training set: {X_save.shape[0]} new rows of {num_train} in {time.time() - t1:.1f} s, "
+        f"{X_train.shape[0]} with the previous run's")
     mean, std = position_stats(X_train, 4)
     F = dir_features(X_train, mean, std, 4)
     F_test = dir_features(X_test, mean, std, 4)
@@ -231,6 +244,8 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
         os.makedirs(out_dir, exist_ok=True)
         np.save(os.path.join(out_dir, "data_4dof_vboc_test.npy"), X_test)
         np.save(os.path.join(out_dir, "data_4dof_vboc_train.npy"), X_train)
+        with open(os.path.join(out_dir, "data_4dof_vboc_train.next_id"), "w") as f:
+            f.write(str(first + num_train))
         torch.save({kk: v.detach().cpu() for kk, v in tr.model.state_dict().items()},
                    os.path.join(out_dir, "model_4dof_vboc"))
         torch.save(mean, os.path.join(out_dir, "mean_4dof_vboc"))
