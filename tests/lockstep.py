@@ -1,0 +1,104 @@
+"""Lockstep comparison of a batched driver on two solver backends (test helper, never imported by the
+product path).
+
+Each problem's generator (vboc_amd.drivers: data_generation_problem / testing_problem / ...) runs twice, once
+per backend, in lockstep: every round, each copy's pending request goes to its own backend (batched), and the
+two answers are compared.  While both copies issue the same kind of request (same horizon for a solve) and get
+answers that agree to rounding, the copies are on the same path.  When they part, the first differing answer
+pair says why:
+  'decision' - every answer so far agreed to rounding (same status; |d cost| <= 1e-6 (1 + |cost|), |d x_0| <=
+               1e-6; twin steps to 1e-9): a tolerance decision of the state machine (the horizon-extension
+               test, the at-limit tests, the stop rule) flipped on a rounding-level difference;
+  'status'   - the two solvers returned different statuses for the same request (a rounding-level difference
+               that changed the SQP path enough to hit max_iter or a QP failure on one side only);
+  'value'    - same status, results differ beyond rounding (a genuine solver disagreement).
+Problems that end on the same path with the same result are 'same'."""
+import numpy as np
+
+from vboc_amd.drivers import Rk4, Solve, _pack
+
+
+def _close_solve(a, b):
+    if a.status != b.status:
+        return "status"
+    if a.status != 0:
+        return "ok"       # failed solves: the iterate is not a result
+    if abs(a.cost - b.cost) > 1e-6 * (1 + abs(b.cost)) or np.abs(a.x[0] - b.x[0]).max() > 1e-6:
+        return "value"
+    return "ok"
+
+
+def _equal_result(a, b, tol=1e-5):
+    if a is None or b is None:
+        return (a is None) == (b is None)
+    if isinstance(a, tuple):
+        return all(_equal_result(x, y, tol) for x, y in zip(a, b))
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    return a.shape == b.shape and (a.size == 0 or np.abs(a - b).max() < tol)
+
+
+def _answers(nq, backend, reqs, nmax):
+    from vboc_amd.drivers import Solution
+    out = {}
+    rk = [i for i, r in reqs.items() if isinstance(r, Rk4)]
+    sv = [i for i, r in reqs.items() if isinstance(r, Solve)]
+    if rk:
+        x1 = backend.rk4(np.stack([reqs[i].x for i in rk]), np.stack([reqs[i].u for i in rk]), reqs[rk[0]].T)
+        for k, i in enumerate(rk):
+            out[i] = x1[k]
+    if sv:
+        rs = [reqs[i] for i in sv]
+        r = backend.solve(_pack(nq, rs, nmax))
+        for k, i in enumerate(sv):
+            n = rs[k].N
+            out[i] = Solution(int(r["status"][k]), r["x"][k, :n + 1], r["u"][k, :n], float(r["cost"][k]))
+    return out
+
+
+def lockstep(nq, make_gen, ids, backend_a, backend_b, nmax=200):
+    """make_gen(pid) -> a fresh generator.  Returns {pid: (kind, detail)} with kind in same / decision /
+    status / value (see the module doc) and the final results of copy A."""
+    ga = {p: make_gen(p) for p in ids}
+    gb = {p: make_gen(p) for p in ids}
+    ra, rb, kind = {}, {}, {}
+    pa, pb = {}, {}
+    for p in ids:
+        pa[p], pb[p] = next(ga[p]), next(gb[p])
+    last = {p: "ok" for p in ids}
+    while pa:
+        for p in list(pa):
+            x, y = pa[p], pb[p]
+            if type(x) is not type(y) or (isinstance(x, Solve) and x.N != y.N):
+                kind[p] = ("decision" if last[p] == "ok" else last[p], "parted")
+                del pa[p], pb[p]
+        if not pa:
+            break
+        # twin steps first, as run_problems does (solves only once no twin step is outstanding)
+        rk = {p: r for p, r in pa.items() if isinstance(r, Rk4)}
+        sel = rk if rk else dict(pa)
+        aa = _answers(nq, backend_a, {p: pa[p] for p in sel}, nmax)
+        ab = _answers(nq, backend_b, {p: pb[p] for p in sel}, nmax)
+        for p in sel:
+            if isinstance(pa[p], Rk4):
+                if np.abs(aa[p] - ab[p]).max() > 1e-9:
+                    last[p] = "value"
+            else:
+                c = _close_solve(aa[p], ab[p])
+                if c != "ok":
+                    last[p] = c
+            done_a = done_b = False
+            try:
+                pa[p] = ga[p].send(aa[p])
+            except StopIteration as e:
+                ra[p], done_a = e.value, True
+            try:
+                pb[p] = gb[p].send(ab[p])
+            except StopIteration as e:
+                rb[p], done_b = e.value, True
+            if done_a or done_b:
+                if done_a and done_b and _equal_result(ra[p], rb[p]):
+                    kind[p] = ("same", "end")
+                else:
+                    kind[p] = ("decision" if last[p] == "ok" else last[p], "end")
+                del pa[p], pb[p]
+    return kind

@@ -149,6 +149,47 @@ def test_testing_driver_on_gpu_matches_reference(nq):
     assert same >= 0.9 * len(g["ids"]), (same, len(g["ids"]))
 
 
+def _gens(nq, law, g):
+    from vboc_amd.drivers import (IC_DRAWS, TEST_STREAM, ProblemRNG, data_generation_problem, testing_problem)
+    from vboc_amd.ics import uniforms
+    ids = np.array(g["ids"])
+    U = uniforms(ids, 3 * nq + 1, g.get("seed", 20250124), stream=0 if law == "dg" else 1)
+    row = {int(p): k for k, p in enumerate(ids)}
+    if law == "dg":
+        return lambda p: data_generation_problem(nq, p, U[row[p]], ProblemRNG(p), g["N_start"])
+    return lambda p: testing_problem(nq, p, U[row[p]], ProblemRNG(p, stream=TEST_STREAM), g["N_start"])
+
+
+def test_lockstep_classifier_on_identical_backends():
+    from lockstep import lockstep
+    g = _golden_test(2)
+    g = dict(g, ids=g["ids"][:12])
+    kinds = lockstep(2, _gens(2, "test", g), [int(p) for p in g["ids"]], OracleBackend(2, g["fail_mod"]),
+                     OracleBackend(2, g["fail_mod"]), nmax=512)
+    assert all(k == "same" for k, _ in kinds.values()), kinds
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq,law", [(3, "dg"), (2, "dg"), (3, "test"), (2, "test"), (1, "test")])
+def test_gpu_driver_mismatches_are_rounding_level_flips(nq, law):
+    """Every problem on which the GPU-backed driver and the oracle-backed driver part is classified in
+    lockstep (tests/lockstep.py): a tolerance decision flipped on rounding-level solver differences
+    ('decision'), or the two solvers returned different statuses for the same request ('status', an SQP
+    path that hits max_iter or a QP failure on one side).  A same-status result that differs beyond
+    rounding ('value') is a defect and fails the test; 'decision' flips stay a minority."""
+    from lockstep import lockstep
+    from vboc_amd.drivers import GpuBackend
+    g = _golden(nq) if law == "dg" else _golden_test(nq)
+    fm = g.get("fail_mod", 0)
+    gpu = GpuBackend(nq) if law == "dg" else _FailingGpu(nq, fm)
+    ora = OracleBackend(nq) if law == "dg" else OracleBackend(nq, fm)
+    kinds = lockstep(nq, _gens(nq, law, g), [int(p) for p in g["ids"]], gpu, ora, nmax=200)
+    counts = {k: sum(v[0] == k for v in kinds.values()) for k in ("same", "decision", "status", "value")}
+    print(nq, law, counts, {p: v for p, v in kinds.items() if v[0] != "same"})
+    assert counts["value"] == 0, kinds
+    assert counts["same"] >= 0.75 * len(kinds), counts
+
+
 @pytest.mark.parametrize("nq,law", [(3, "dg"), (2, "dg"), (3, "test"), (2, "test"), (1, "test")])
 def test_first_solve_equals_batched_ics(nq, law):
     """The bench / parity batches (vboc_amd.ics) are exactly the drivers' first OCP solves."""
