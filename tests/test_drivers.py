@@ -61,8 +61,9 @@ def test_driver_on_gpu_matches_reference(nq):
             same += (a is None) == (b is None)
         elif a.shape == b.shape and np.abs(a - b).max() < 1e-5:
             same += 1
-    # rounding-level solver differences may flip a tolerance decision on a few problems
-    assert same >= 0.8 * len(g["ids"]), (same, len(g["ids"]))
+    # rounding-level solver differences may flip a tolerance decision on a problem (classified in
+    # test_gpu_driver_mismatches_are_rounding_level_flips; measured: none on these fixtures)
+    assert same >= 0.95 * len(g["ids"]), (same, len(g["ids"]))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -145,8 +146,9 @@ def test_testing_driver_on_gpu_matches_reference(nq):
             same += (got is None) == (ref is None)
         elif np.abs(np.asarray(got) - np.asarray(ref)).max() < 1e-5:
             same += 1
-    # a rounding-level cost difference can flip the 3-decimal stop rule on a few problems
-    assert same >= 0.9 * len(g["ids"]), (same, len(g["ids"]))
+    # a rounding-level cost difference can flip the 3-decimal stop rule on a problem (classified in
+    # test_gpu_driver_mismatches_are_rounding_level_flips; measured: none on these fixtures)
+    assert same >= 0.95 * len(g["ids"]), (same, len(g["ids"]))
 
 
 def _gens(nq, law, g):
@@ -187,7 +189,8 @@ def test_gpu_driver_mismatches_are_rounding_level_flips(nq, law):
     counts = {k: sum(v[0] == k for v in kinds.values()) for k in ("same", "decision", "status", "value")}
     print(nq, law, counts, {p: v for p, v in kinds.items() if v[0] != "same"})
     assert counts["value"] == 0, kinds
-    assert counts["same"] >= 0.75 * len(kinds), counts
+    # measured on MI355X (profiles/r02s_pytest_gpu_lockstep_classification.log): every problem 'same'
+    assert counts["same"] >= 0.95 * len(kinds), counts
 
 
 @pytest.mark.parametrize("nq,law", [(3, "dg"), (2, "dg"), (3, "test"), (2, "test"), (1, "test")])
