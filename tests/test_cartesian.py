@@ -7,7 +7,7 @@ Pins:
     an inequality (tests/nlp_reference.py), including a problem where the circle is active;
   * the batched driver on the oracle reproduces the reference's own `testing_test` (AST-extracted, run on
     the drop-in vboc_amd.cartesian class, tests/golden/testing_cartesian.json) bit for bit;
-  * on the GPU (lane-mode kernels with the constraint rows) the solver follows the oracle (the section-3
+  * on the GPU (the wave solver and the lane-mode kernels, each with the constraint rows) the solver follows the oracle (the section-3
     bars of DESIGN.md) and the driver matches the fixture.
 ACADOS-level parity is unpinned, as for every solve; so is the stage-0 treatment of
 the constraint (ACADOS versions differ; here: checked once, status 4 if violated)."""
@@ -90,11 +90,14 @@ def test_cartesian_driver_matches_reference_on_oracle():
 
 
 @pytest.mark.gpu
-def test_gpu_cartesian_parity_with_oracle():
+@pytest.mark.parametrize("mode", ["wave", "lane"])
+def test_gpu_cartesian_parity_with_oracle(mode):
+    """Both GPU paths of the constraint rows: the wave solver (k_wave<2, false, true>, the default) and the
+    lane-per-problem kernels (wave_all = 0)."""
     from vboc_amd import lib
     c = cartesian_constraint()
     b = cartesian_ics(np.arange(96))
-    s = lib.Solver(2, 128, slots=256)
+    s = lib.Solver(2, 128, slots=256, wave_all=1 if mode == "wave" else 0)
     s.set_path_constraint(c)
     g = s.solve_host(b)
     xo, _, r = _oracle(b)

@@ -224,9 +224,17 @@ __device__ unsigned g_dbg_cnt;
 #define SPROF_FLUSH
 #endif
 
-template <int NQ, bool FM = false>
+// HC: the Cartesian path-constraint rows (vboc_set_path_constraint; oracle/vboc_oracle.c hc_*, Lane::hc_*) on
+// stages 1..N-1, pendulum chains with the VALU factorisation only.  No change of the stage-record layout: the
+// rows' state lives in a per-workgroup region `gh` (Lane<NQ>::FHC fields per stage); the Hessian's position
+// block diag(H_q) + sigma c c' travels to the factorisation in the K field of the record (free between
+// prep_pred and the factorisation step that writes K), and the costate's c (lambda_u - lambda_l) term in the
+// B field (free once the QP has finished).
+template <int NQ, bool FM = false, bool HC = false>
 struct Coop {
   using L = WaveLayout<NQ>;
+  using HL = Lane<NQ>;
+  static_assert(!HC || (!FM && NQ >= 2 && NQ <= 3), "path constraint: pendulum chains, VALU factorisation");
   using PF = Par<NQ>;
   static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1, REC = L::REC;
   static constexpr int OA = L::OA, OB = L::OB, OZ = L::OZ, ODZ = L::ODZ, OQL = L::OQL, OQU = L::OQU,
@@ -244,6 +252,7 @@ struct Coop {
   double rs, rd0, e00, mu, nbox;   // interior-point scalars (wave-uniform)
 
   unsigned lds0;    // LDS byte address of s[0] (wave-uniform), for the LDS-DMA's M0
+  gdouble* gh = nullptr;   // HC: this workgroup's path-constraint rows, FHC doubles per stage
 
   __device__ Coop(double* s_, gdouble* g_, const Work& w_, const Opts& o_, int t_)
       : s(s_), g(g_), w(w_), o(o_), t(t_), N(0),
@@ -255,6 +264,33 @@ struct Coop {
   __device__ __forceinline__ void fresh() { asm volatile("" : "+v"(t)); }
 
   __device__ __forceinline__ gdouble& st(int k, int off) const { return g[(long long)k * REC + off]; }
+  __device__ __forceinline__ gdouble& hcr(int k, int f) const { return gh[(long long)k * HL::FHC + f]; }
+  __device__ __forceinline__ bool hc_on(int k) const { return HC && k >= 1 && k < N; }
+  __device__ __forceinline__ double hc_eval(const double* x, double* grad) const {
+    constexpr double l = Chain<NQ>::l;
+    double X = 0.0, Y = 0.0;
+    UNR for (int j = 0; j < NQ; ++j) { X += l * sin(x[j]); Y += l * cos(x[j]); }
+    const double dx = X - o.hxc, dy = Y - o.hyc;
+    if (grad) {
+      UNR for (int j = 0; j < NQ; ++j) grad[j] = 2.0 * dx * (l * cos(x[j])) - 2.0 * dy * (l * sin(x[j]));
+    }
+    return dx * dx + dy * dy;
+  }
+  // Newton directions of the row's slacks / duals from the stage step d (Lane::hc_dir)
+  template <bool CORR>
+  __device__ __forceinline__ void hc_dir(int k, const double* d, double smu, double& dtl, double& dtu, double& dql,
+                                         double& dqu) const {
+    double cd = 0.0;
+    UNR for (int j = 0; j < NQ; ++j) cd += hcr(k, HL::HG + j) * d[j];
+    const double htl = hcr(k, HL::HTL), htu = hcr(k, HL::HTU), hql = hcr(k, HL::HQL), hqu = hcr(k, HL::HQU);
+    const double rl = rs * hcr(k, HL::HR0L), ru = rs * hcr(k, HL::HR0U);
+    const double rcl = CORR ? smu - htl * hql - hcr(k, HL::HATL) * hcr(k, HL::HAQL) : -htl * hql;
+    const double rcu = CORR ? smu - htu * hqu - hcr(k, HL::HATU) * hcr(k, HL::HAQU) : -htu * hqu;
+    dtl = cd + rl;
+    dtu = ru - cd;
+    dql = (rcl - hql * dtl) / htl;
+    dqu = (rcu - hqu * dtu) / htu;
+  }
   __device__ __forceinline__ double& par(int f) const { return s[L::PAR + f]; }
   __device__ __forceinline__ static constexpr int fslot(int slot) { return L::RING + slot * L::RSF; }
   __device__ __forceinline__ static constexpr int vslot(int slot) { return L::RING + slot * L::RSV; }
@@ -477,7 +513,8 @@ struct Coop {
       int i, j;
       tri(u, i, j);
       d2.x1 = OA + i; d2.sx1 = NX; d2.y1 = PA + j; d2.sy1 = NX; d2.rel = RX1;
-      if (i == j) { d2.ini = OD + i; d2.rel |= RINI; }
+      if (HC && i < NQ && j < NQ) { d2.ini = OK + i * NQ + j; d2.rel |= RINI; }   // diag(H_q) + sigma c c'
+      else if (i == j) { d2.ini = OD + i; d2.rel |= RINI; }
       d2.d1 = APA + i * NX + j; d2.d2 = APA + j * NX + i;
     } else if ((u -= TX) < TU) {
       int a, c;
@@ -596,6 +633,10 @@ struct Coop {
     for (int k = t; k <= N; k += 64) {
       UNR for (int i = 0; i < NX; ++i) st(k, OX + i) = xg[(long long)k * NXR + i];
       UNR for (int i = 0; i < NZ; ++i) { st(k, OLL + i) = 0.0; st(k, OLU + i) = 0.0; }
+      if constexpr (HC) {
+        hcr(k, HL::HLL) = 0.0;
+        hcr(k, HL::HLU) = 0.0;
+      }
       if (k < N) {
         UNR for (int a = 0; a < NU; ++a) st(k, OU + a) = ug[(long long)k * NU + a];
         UNR for (int i = 0; i < NX; ++i) { st(k, OPI + i) = 0.0; st(k, OWPI + i) = 0.0; }
@@ -672,11 +713,24 @@ struct Coop {
         } else {
           double pprev[NX];
           UNR for (int i = 0; i < NX; ++i) pprev[i] = st(k - 1, OPI + i);
+          double hg[NQ], hmul = 0.0;
+          if constexpr (HC) {
+            const double hv = hc_eval(xk, hg);
+            hcr(k, HL::HV) = hv;
+            UNR for (int j = 0; j < NQ; ++j) hcr(k, HL::HG + j) = hg[j];
+            const double hll = hcr(k, HL::HLL), hlu = hcr(k, HL::HLU);
+            hmul = hlu - hll;
+            inq = fmax(inq, fmax(o.hlh - hv, hv - o.huh));
+            cp = fmax(cp, fmax(fabs(hll * (hv - o.hlh)), fabs(hlu * (o.huh - hv))));
+          }
           UNR for (int c = 0; c < NZ; ++c) {
             double gr = -rec[OLL + c] + rec[OLU + c];
             if (c < NX) {
               UNR for (int r = 0; r < NX; ++r) gr += rec[OA + r * NX + c] * pik[r];
               gr -= pprev[c];
+              if constexpr (HC) {
+                if (c < NQ) gr += hg[c < NQ ? c : 0] * hmul;
+              }
             } else {
               UNR for (int r = 0; r < NX; ++r) gr += rec[OB + r * NU + (c - NX)] * pik[r];
             }
@@ -735,7 +789,25 @@ struct Coop {
         }
         dz[i] = d0;
         rec[ODZ + i] = d0; rec[OQL + i] = ql; rec[OQU + i] = qu;
-        rd = fmax(rd, fabs(o.lm * d0 + cgrad(k, i) - ql + qu));
+        if (!(HC && i < NQ && k >= 1 && k < N)) rd = fmax(rd, fabs(o.lm * d0 + cgrad(k, i) - ql + qu));
+      }
+      if constexpr (HC) {
+        if (hc_on(k)) {
+          // slacks from the initial c'dz, clipped to ipm_push (Lane::qp_init)
+          double hg[NQ], gd = 0.0;
+          UNR for (int j = 0; j < NQ; ++j) { hg[j] = hcr(k, HL::HG + j); gd += hg[j] * dz[j]; }
+          const double hv = hcr(k, HL::HV), Lh = o.hlh - hv, Uh = o.huh - hv;
+          const double tl = fmax(gd - Lh, o.push), tu = fmax(Uh - gd, o.push);
+          const double ql = o.mu0 / tl, qu = o.mu0 / tu;
+          const double r0l = gd - Lh - tl, r0u = Uh - gd - tu;
+          hcr(k, HL::HTL) = tl; hcr(k, HL::HTU) = tu; hcr(k, HL::HQL) = ql; hcr(k, HL::HQU) = qu;
+          hcr(k, HL::HR0L) = r0l; hcr(k, HL::HR0U) = r0u;
+          musum += tl * ql + tu * qu;
+          nb += 2.0;
+          e0 = fmax(e0, fmax(fabs(r0l), fabs(r0u)));
+          UNR for (int i = 0; i < NQ; ++i)
+            rd = fmax(rd, fabs(o.lm * dz[i] + cgrad(k, i) - rec[OQL + i] + rec[OQU + i] + hg[i] * (qu - ql)));
+        }
       }
       if (k < N) {
         const gdouble* rn = &g[(long long)(k + 1) * REC];
@@ -788,6 +860,20 @@ struct Coop {
         rec[OD + i] = o.lm + (c.bx ? c.ql * c.itl + c.qu * c.itu : 0.0);
         rec[ODA + i] = o.lm * c.dz + cgrad(k, i);
       }
+      if constexpr (HC) {
+        if (hc_on(k)) {
+          const double htl = hcr(k, HL::HTL), htu = hcr(k, HL::HTU), hql = hcr(k, HL::HQL), hqu = hcr(k, HL::HQU);
+          const double sig = hql / htl + hqu / htu;
+          const double gam = hql * (rs * hcr(k, HL::HR0L)) / htl - hqu * (rs * hcr(k, HL::HR0U)) / htu;
+          double hg[NQ];
+          UNR for (int j = 0; j < NQ; ++j) hg[j] = hcr(k, HL::HG + j);
+          UNR for (int i = 0; i < NQ; ++i) {
+            UNR for (int j = 0; j < NQ; ++j)
+              rec[OK + i * NQ + j] = (i == j ? (double)rec[OD + i] : 0.0) + sig * hg[i] * hg[j];
+            rec[ODA + i] += hg[i] * gam;
+          }
+        }
+      }
     }
     __syncthreads();
   }
@@ -810,6 +896,16 @@ struct Coop {
           gg += -c.ql - rl * c.itl + c.qu + ru * c.itu;
         }
         rec[OD + i] = gg;
+      }
+      if constexpr (HC) {
+        if (hc_on(k)) {
+          const double htl = hcr(k, HL::HTL), htu = hcr(k, HL::HTU), hql = hcr(k, HL::HQL), hqu = hcr(k, HL::HQU);
+          const double rl = rs * hcr(k, HL::HR0L), ru = rs * hcr(k, HL::HR0U);
+          const double rcl = smu - htl * hql - hcr(k, HL::HATL) * hcr(k, HL::HAQL);
+          const double rcu = smu - htu * hqu - hcr(k, HL::HATU) * hcr(k, HL::HAQU);
+          const double gam = -hql + hqu - (rcl - hql * rl) / htl + (rcu - hqu * ru) / htu;
+          UNR for (int j = 0; j < NQ; ++j) rec[OD + j] += hcr(k, HL::HG + j) * gam;
+        }
       }
     }
     __syncthreads();
@@ -1392,6 +1488,23 @@ struct Coop {
         mr.add(c.ql, dll);
         mr.add(c.qu, dlu);
       }
+      if constexpr (HC) {
+        if (hc_on(k)) {
+          double dtl, dtu, dql, dqu;
+          hc_dir<CORR>(k, d, smu, dtl, dtu, dql, dqu);
+          const double htl = hcr(k, HL::HTL), htu = hcr(k, HL::HTU), hql = hcr(k, HL::HQL), hqu = hcr(k, HL::HQU);
+          if (!CORR) {
+            hcr(k, HL::HATL) = dtl; hcr(k, HL::HATU) = dtu; hcr(k, HL::HAQL) = dql; hcr(k, HL::HAQU) = dqu;
+            a0 += htl * hql + htu * hqu;
+            a1 += htl * dql + dtl * hql + htu * dqu + dtu * hqu;
+            a2 += dtl * dql + dtu * dqu;
+          }
+          mr.add(htl, dtl);
+          mr.add(htu, dtu);
+          mr.add(hql, dql);
+          mr.add(hqu, dqu);
+        }
+      }
     }
     amax = wmind(mr.value());
     c0 = wsum(a0); c1 = wsum(a1); c2 = wsum(a2);
@@ -1423,6 +1536,16 @@ struct Coop {
         rec[OQU + i] = qun;
         musum += (c.tl + alpha * d) * qln + (c.tu - alpha * d) * qun;
       }
+      if constexpr (HC) {
+        if (hc_on(k)) {
+          double dtl, dtu, dql, dqu;
+          hc_dir<true>(k, dd, smu, dtl, dtu, dql, dqu);
+          const double tl = hcr(k, HL::HTL) + alpha * dtl, tu = hcr(k, HL::HTU) + alpha * dtu;
+          const double ql = hcr(k, HL::HQL) + alpha * dql, qu = hcr(k, HL::HQU) + alpha * dqu;
+          hcr(k, HL::HTL) = tl; hcr(k, HL::HTU) = tu; hcr(k, HL::HQL) = ql; hcr(k, HL::HQU) = qu;
+          musum += tl * ql + tu * qu;
+        }
+      }
     }
     mu = wsum(musum) / nbox;
     __syncthreads();
@@ -1431,6 +1554,14 @@ struct Coop {
   // costate recovery into the DA slot (x part) of stages 0..N-1
   __device__ __forceinline__ bool costate() {
     fresh();
+    if constexpr (HC) {
+      // the rows' c (lambda_u - lambda_l) term of each stage's costate constant -> the B field (free now)
+      for (int k = 1 + t; k < N; k += 64) {
+        const double m = hcr(k, HL::HQU) - hcr(k, HL::HQL);
+        UNR for (int j = 0; j < NQ; ++j) st(k, OB + j) = hcr(k, HL::HG + j) * m;
+      }
+      __syncthreads();
+    }
     bool fin = true;
     if (t < NX) {
       const int i = t;
@@ -1453,6 +1584,7 @@ struct Coop {
     auto cterms = [&](int kb, double (&ac)[NX], double& cc) {
       const int i = t < NX ? t : NX - 1;
       cc = o.lm * s[kb + ODZ + i] - s[kb + OQL + i] + s[kb + OQU + i];
+      if constexpr (HC) cc += i < NQ ? s[kb + OB + (i < NQ ? i : 0)] : 0.0;
       UNR for (int q = 0; q < NX; ++q) ac[q] = s[kb + OA + q * NX + i];
     };
     double ac[NX], cc = 0.0;
@@ -1503,6 +1635,9 @@ struct Coop {
         UNR for (int i = 0; i < NX; ++i) st(k, OWPI + i) = Lane<NQ>::wupd(st(k, OWPI + i), st(k, ODA + i));
       }
       UNR for (int i = 0; i < NZ; ++i) lmax = fmax(lmax, fmax((double)st(k, OQL + i), (double)st(k, OQU + i)));
+      if constexpr (HC) {
+        if (hc_on(k)) lmax = fmax(lmax, fmax((double)hcr(k, HL::HQL), (double)hcr(k, HL::HQU)));
+      }
     }
     lmax = wmaxd(lmax);
     if (t == 0) {
@@ -1536,6 +1671,14 @@ struct Coop {
         if (!box(k, i, lb, ub)) continue;
         const double v = rec[OZ + i] + alpha * rec[ODZ + i];
         acc(viol, fmax(0.0, lb - v) + fmax(0.0, v - ub));
+      }
+      if constexpr (HC) {
+        if (hc_on(k)) {
+          double xq[NQ];
+          UNR for (int j = 0; j < NQ; ++j) xq[j] = rec[OZ + j] + alpha * rec[ODZ + j];
+          const double hv = hc_eval(xq, nullptr);
+          acc(viol, fmax(0.0, o.hlh - hv) + fmax(0.0, hv - o.huh));
+        }
       }
       if (k > 0) {
         const gdouble* rp = &g[(long long)(k - 1) * REC];
@@ -1576,6 +1719,12 @@ struct Coop {
       UNR for (int i = 0; i < NZ; ++i) {
         rec[OLL + i] += alpha * (rec[OQL + i] - rec[OLL + i]);
         rec[OLU + i] += alpha * (rec[OQU + i] - rec[OLU + i]);
+      }
+      if constexpr (HC) {
+        if (hc_on(k)) {
+          hcr(k, HL::HLL) += alpha * (hcr(k, HL::HQL) - hcr(k, HL::HLL));
+          hcr(k, HL::HLU) += alpha * (hcr(k, HL::HQU) - hcr(k, HL::HLU));
+        }
       }
       if (k < N) {
         UNR for (int i = 0; i < NX; ++i) rec[OPI + i] += alpha * (rec[ODA + i] - rec[OPI + i]);
@@ -1707,12 +1856,13 @@ struct WavesPerEu { static constexpr int v = NQ <= 3 ? 2 : 1; };
 
 // one workgroup = one wave = one problem at a time; workgroups pull jobs until none are left
 // FM: the Riccati factorisation on FP64 MFMA (factor_mfma, NQ <= 3) instead of VALU dot-product steps
-template <int NQ, bool FM>
+template <int NQ, bool FM, bool HC = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WavesPerEu<NQ>::v, WavesPerEu<NQ>::v)))
 void k_wave(Work w, Opts o, Inputs in, SlotState ss, WaveJobs jb) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int t = (int)threadIdx.x;
-  Coop<NQ, FM> C(smem, gptr(jb.regions) + (long long)blockIdx.x * jb.region_doubles, w, o, t);
+  Coop<NQ, FM, HC> C(smem, gptr(jb.regions) + (long long)blockIdx.x * jb.region_doubles, w, o, t);
+  if constexpr (HC) C.gh = gptr(jb.hc) + (long long)blockIdx.x * jb.hc_doubles;
   for (;;) {
     unsigned idx = 0;
     if (t == 0) idx = atomicAdd(jb.next, 1u);
@@ -1738,6 +1888,22 @@ void k_wave(Work w, Opts o, Inputs in, SlotState ss, WaveJobs jb) {
           atomicAdd(ss.done, 1u);
         }
         continue;
+      }
+      if constexpr (HC) {
+        // stage 0: positions fixed, h constant - outside [lh, uh]: status 4 without iterating (k_refill)
+        double q0[NQ];
+        UNR for (int j = 0; j < NQ; ++j) q0[j] = in.lbx0[(long long)pid * (2 * NQ + 1) + j];
+        const double h0 = C.hc_eval(q0, nullptr);
+        if (!(h0 >= o.hlh && h0 <= o.huh)) {
+          if (t == 0) {
+            in.status[pid] = 4;
+            in.cost[pid] = NAN;
+            in.sqp_iter[pid] = 0;
+            in.qp_iter[pid] = 0;
+            atomicAdd(ss.done, 1u);
+          }
+          continue;
+        }
       }
       C.from_inputs(in, pid);
     }

@@ -1437,6 +1437,8 @@ struct WaveJobs {
   unsigned* next;          // job counter
   double* regions;         // one stage-record region per workgroup
   long long region_doubles;
+  double* hc = nullptr;    // path-constraint rows, one region per workgroup (k_wave<NQ, false, true>)
+  long long hc_doubles = 0;
 };
 
 }  // namespace vboc
@@ -1506,6 +1508,9 @@ struct vboc_solver {
   bool dg_attr[2] = {false, false};
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
+  double* wave_hc = nullptr;        // path-constraint rows of the wave solver, one region per workgroup
+  long long wave_hc_doubles = 0;
+  bool hc_wave = true;              // constrained problems on the wave solver (k_wave<NQ, false, true>)
   void* dg_spec = nullptr;          // their pool (events, results, control words, queue)
   size_t dg_spec_bytes = 0;
 };
@@ -1640,11 +1645,13 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
       else hipLaunchKernelGGL((k_wave<1, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
       break;
     case 2:
-      if (h->factor_mfma) hipLaunchKernelGGL((k_wave<2, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      if (h->o.hc) hipLaunchKernelGGL((k_wave<2, false, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      else if (h->factor_mfma) hipLaunchKernelGGL((k_wave<2, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
       else hipLaunchKernelGGL((k_wave<2, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
       break;
     case 3:
-      if (h->factor_mfma) hipLaunchKernelGGL((k_wave<3, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      if (h->o.hc) hipLaunchKernelGGL((k_wave<3, false, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      else if (h->factor_mfma) hipLaunchKernelGGL((k_wave<3, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
       else hipLaunchKernelGGL((k_wave<3, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
       break;
     default: hipLaunchKernelGGL((k_wave<4, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
@@ -1773,6 +1780,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->head) (void)hipFree(h->head);
   if (h->ist) (void)hipFree(h->ist);
   if (h->w.HC) (void)hipFree(h->w.HC);
+  if (h->wave_hc) (void)hipFree(h->wave_hc);
   if (h->list) (void)hipFree(h->list);
   if (h->regions) (void)hipFree(h->regions);
   if (h->host_done) (void)hipHostFree(h->host_done);
@@ -1817,6 +1825,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "mall_mib") h->mall_mib = v;
   else if (s == "dg_fail_mod") h->dg_fail_mod = (int)v;
   else if (s == "dg_speculate") h->dg_speculate = v != 0.0;
+  else if (s == "hc_wave") h->hc_wave = v != 0.0;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
     if (h->profile && h->pev.empty()) {
@@ -1851,6 +1860,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "coop_available") *v = h->coop_ok ? 1.0 : 0.0;
   else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
   else if (s == "dg_speculate") *v = h->dg_speculate ? 1.0 : 0.0;
+  else if (s == "hc_wave") *v = h->hc_wave ? 1.0 : 0.0;
   else if (s == "factor_mfma") *v = h->factor_mfma ? 1.0 : 0.0;
   else if (s == "wave_groups") *v = (double)h->n_regions;
   else if (s == "mall_mib") *v = h->mall_mib;
@@ -1875,6 +1885,14 @@ int vboc_set_path_constraint(vboc_handle h, int kind, double x_c, double y_c, do
     if (e != hipSuccess) {
       h->w.HC = nullptr;
       return fail(VBOC_ERR_NOMEM, "vboc_set_path_constraint: hipMalloc constraint rows");
+    }
+  }
+  if (!h->wave_hc && h->coop_ok) {
+    const long long f = h->nq == 2 ? (long long)Lane<2>::FHC : (long long)Lane<3>::FHC;
+    h->wave_hc_doubles = f * (long long)(h->nmax + 1);
+    if (hipMalloc((void**)&h->wave_hc, sizeof(double) * (size_t)h->wave_hc_doubles * (size_t)h->n_regions) != hipSuccess) {
+      h->wave_hc = nullptr;
+      (void)hipGetLastError();
     }
   }
   h->o.hc = 1; h->o.hxc = x_c; h->o.hyc = y_c; h->o.hlh = lh; h->o.huh = uh;
@@ -1912,9 +1930,10 @@ int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
   SlotState ss{h->ist, h->head + 1, h->head + 2, (unsigned long long*)(h->head + 4), h->slots};
   const dim3 grid((unsigned)(lanes / 256)), block(256);
   HIPCHK(hipEventRecord(h->ev0, st));
-  if (h->wave_all && h->coop_ok && !h->o.hc) {
+  const bool hc_ok = !h->o.hc || (h->hc_wave && h->wave_hc);
+  if (h->wave_all && h->coop_ok && hc_ok) {
     // every problem on its own wave, pulled from the input queue (head[0])
-    WaveJobs jb{nullptr, b->B, h->head, h->regions, h->region_doubles};
+    WaveJobs jb{nullptr, b->B, h->head, h->regions, h->region_doubles, h->wave_hc, h->wave_hc_doubles};
     h->launches = 1;
     h->coop_count = b->B;
     HIPCHK(launch_wave(h, jb, (long long)b->B, st, w, in, ss));
