@@ -123,8 +123,8 @@ int vboc_get_option(vboc_handle h, const char* field, double* value);
  *           at stage 0 the positions are fixed, so a problem whose initial position violates it gets
  *           status 4 (QP failure) without iterating;
  *   kind 0: no path constraint (the default).
- * Solves with the constraint run on the wave solver (k_wave with the constraint rows; option "hc_wave" = 0 or
- * wave_all = 0: the lane-per-problem kernels); the free-time solver and vboc_data_generation refuse a handle
+ * Solves with the constraint run on the wave solver for nq = 2 (k_wave with the constraint rows; option
+ * "hc_wave" = 0 or wave_all = 0: the lane-per-problem kernels) and on the lane kernels for nq = 3; the free-time solver and vboc_data_generation refuse a handle
  * that carries one (VBOC_ERR_UNSUPPORTED). */
 int vboc_set_path_constraint(vboc_handle h, int kind, double x_c, double y_c, double lh, double uh);
 

@@ -1650,8 +1650,7 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
       else hipLaunchKernelGGL((k_wave<2, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
       break;
     case 3:
-      if (h->o.hc) hipLaunchKernelGGL((k_wave<3, false, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
-      else if (h->factor_mfma) hipLaunchKernelGGL((k_wave<3, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
+      if (h->factor_mfma) hipLaunchKernelGGL((k_wave<3, true>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
       else hipLaunchKernelGGL((k_wave<3, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb);
       break;
     default: hipLaunchKernelGGL((k_wave<4, false>), grid, block, h->wave_lds, st, w, h->o, in, ss, jb); break;
@@ -1887,8 +1886,11 @@ int vboc_set_path_constraint(vboc_handle h, int kind, double x_c, double y_c, do
       return fail(VBOC_ERR_NOMEM, "vboc_set_path_constraint: hipMalloc constraint rows");
     }
   }
-  if (!h->wave_hc && h->coop_ok) {
-    const long long f = h->nq == 2 ? (long long)Lane<2>::FHC : (long long)Lane<3>::FHC;
+  // the wave solver carries the rows for the double pendulum (the reference's Cartesian system); the triple's
+  // instantiation would spill (140 B of scratch), which the counted ring waits do not tolerate (DESIGN.md
+  // section 5), so a constrained triple runs on the lane kernels
+  if (!h->wave_hc && h->coop_ok && h->nq == 2) {
+    const long long f = (long long)Lane<2>::FHC;
     h->wave_hc_doubles = f * (long long)(h->nmax + 1);
     if (hipMalloc((void**)&h->wave_hc, sizeof(double) * (size_t)h->wave_hc_doubles * (size_t)h->n_regions) != hipSuccess) {
       h->wave_hc = nullptr;
