@@ -1028,22 +1028,26 @@ struct Coop {
       const int kk = N - 1 - j >= 0 ? N - 1 - j : 0;
       UNR for (int part = 0; part < P; ++part) dma(kk, 0, L::W_FAC, fslot(j % L::NSF), part);
     };
-    // loop-invariant per-lane constants
-    int goff[2];
+    // loop-invariant per-lane constants.  A lane without a G / H operand reads the zeroed LDS words (ZERO,
+    // absolute: slot base multiplier 0), never the slot's tail: the tail holds whatever the record's next
+    // fields or an earlier problem left there, and a stale NaN / Inf times a 0 mask is NaN (a problem that
+    // failed with non-finite iterates used to poison the next problem solved on the same workgroup region)
+    int goff[2], gb[2];
     double gm[2];
     UNR for (int q = 0; q < 2; ++q) {
       const int row = 4 * q + g;
-      int off = L::W_FAC;
+      int off = L::ZERO, b = 0;
       double m = 0.0;
       if (row < NX) {
-        if (c < NX) { off = OA + row * NX + c; m = 1.0; }
-        else if (c < CE) { off = OB + row * NU + (c - NX); m = 1.0; }
-        else if (c == CE) { off = OE + row; m = rs; }
+        if (c < NX) { off = OA + row * NX + c; m = 1.0; b = 1; }
+        else if (c < CE) { off = OB + row * NU + (c - NX); m = 1.0; b = 1; }
+        else if (c == CE) { off = OE + row; m = rs; b = 1; }
       }
       goff[q] = off;
+      gb[q] = b;
       gm[q] = m;
     }
-    const int hoff = c < CE ? OD + c : L::W_FAC;
+    const int hoff = c < CE ? OD + c : L::ZERO, hb = c < CE ? 1 : 0;
     double hm[4], cm[4];
     UNR for (int r = 0; r < 4; ++r) {
       const int row = g + 4 * r;
@@ -1075,8 +1079,8 @@ struct Coop {
       fdma(j + 2);
       vmwait<2 * P>();   // loads only, as in factor()
       dbg_check(kb, k, 0, L::W_FAC, 1);
-      double g0 = s[kb + goff[0]] * gm[0], g1 = s[kb + goff[1]] * gm[1];
-      const double hv = s[kb + hoff];
+      double g0 = s[kb * gb[0] + goff[0]] * gm[0], g1 = s[kb * gb[1] + goff[1]] * gm[1];
+      const double hv = s[kb * hb + hoff];
       vreg(g0);
       vreg(g1);
       // P G (rows / columns of D beyond the stage blocks only meet zero rows of G)
