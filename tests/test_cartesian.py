@@ -118,6 +118,31 @@ def test_gpu_cartesian_parity_with_oracle(mode):
 
 
 @pytest.mark.gpu
+def test_gpu_handle_state_does_not_leak_between_problems():
+    """Regression: unconstrained solves on a handle that ran constrained ones equal a fresh handle's, bit for
+    bit (the MFMA factorisation used to read the ring slot's tail under a 0 mask; a NaN left there by an
+    earlier problem on the same workgroup region poisoned the next one: 16 of 2048 spurious QP failures,
+    profiles/r02v_probe_handle_state_after_constrained_solves.log)."""
+    import torch
+    from vboc_amd import lib
+    b = cartesian_ics(np.arange(2048))
+    tb = {k: torch.as_tensor(np.ascontiguousarray(v), device="cuda:0") for k, v in b.items()}
+
+    def run(s):
+        r = s.solve_device(tb)
+        torch.cuda.synchronize()
+        return {k: v.cpu().numpy() for k, v in r.items()}
+    fresh = run(lib.Solver(2, 100, slots=4096))
+    used = lib.Solver(2, 100, slots=4096)
+    used.set_path_constraint(cartesian_constraint())
+    run(used)
+    used.set_path_constraint(None)
+    again = run(used)
+    np.testing.assert_array_equal(again["status"], fresh["status"])
+    np.testing.assert_array_equal(again["x"], fresh["x"])
+
+
+@pytest.mark.gpu
 def test_gpu_cartesian_driver_matches_reference():
     from vboc_amd.drivers import GpuBackend
     g = json.load(open(GOLDEN))
