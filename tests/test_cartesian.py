@@ -172,3 +172,19 @@ def test_capi_refuses_unsupported_constraint_handles():
     from vboc_amd import lib
     lib.load()
     assert "vboc_set_path_constraint" in lib.EXPORTS
+
+
+def test_cartesian_run_on_oracle(tmp_path):
+    """The Cartesian main block end to end on CPU (oracle with the circle, small sets, small minibatch):
+    artefacts in the reference's names and formats, loadable with weights_only=True."""
+    import torch
+    from vboc_amd.pipeline import cartesian_run
+    r = cartesian_run(OracleBackend(2, path_constraint=cartesian_constraint()), num_test=6, num_train=24,
+                      out_dir=str(tmp_path), device="cpu", minibatch=8, hidden=16)
+    assert r["X_train"].shape[1] == 5 and r["X_train"].shape[0] >= 12
+    assert np.all(r["X_train"][:, 4] == 1e-2)
+    assert np.isfinite(r["rmse_train"]) and np.isfinite(r["rmse_test"])
+    sd = torch.load(tmp_path / "model_2dof_vboc_10_16", weights_only=True)
+    assert sd["linear_relu_stack.0.weight"].shape == (16, 4)
+    assert np.load(tmp_path / "data_2dof_vboc_10.npy").shape == r["X_train"].shape
+    assert isinstance(torch.load(tmp_path / "mean_2dof_vboc_10_16", weights_only=True), float)

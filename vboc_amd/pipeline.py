@@ -252,3 +252,52 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
         torch.save(std, os.path.join(out_dir, "std_4dof_vboc"))
     return dict(X_test=X_test, X_train=X_train, fit=fit, rmse_train=rmse_train, rmse_test=rmse_test,
                 stats=(st_test, st_train), mean=mean, std=std)
+
+
+def cartesian_run(backend=None, num_test=1000, num_train=100000, out_dir=None, device="cuda", seed=0,
+                  minibatch=4096, hidden=300, log=None):
+    """The main block of VBOC/Cartesian constraints/vboc_multiprocessing.py (double pendulum with the end-effector
+    keep-out circle) on one GPU:
+      test set      `testing_test` over ids [0, num_test) (:557-562)
+      training set  `testing_test` over ids [num_test, + num_train) (:567-585)  -> data_2dof_vboc_10.npy (5 columns,
+                    dt included, as the reference saves X_save)
+      features      [(q - mean) / std, qdot / |qdot|] -> |qdot| with the scalar position mean / std of the training
+                    set (:600-615)
+      fit           NeuralNetRegression(4, 300, 1) (same layers as NeuralNetDIR), Adam lr 1e-3, minibatch 4096,
+                    EMA beta 0.95, stop at val <= 1e-3 or it_max = 100 * int(n * 100 / 4096) steps (:617-660), on
+                    the HIP-graph trainer
+      RMSE          on the training and the test data (:662-690); artefacts model_/mean_/std_2dof_vboc_10_300.
+    backend: a drivers backend carrying the circle (default: GpuBackend(2, path_constraint=...)).  Returns
+    dict(X_test, X_train, fit, rmse_train, rmse_test, stats)."""
+    import torch
+    from .drivers import GpuBackend, cartesian_testing_batch
+    from .systems import cartesian_constraint
+    log = log or (lambda *a: None)
+    backend = backend or GpuBackend(2, nmax=200, path_constraint=cartesian_constraint())
+    rows = lambda res: np.array([r for t in res if t is not None for r in t], dtype=np.float64).reshape(-1, 5)
+    t0 = time.time()
+    res, st_test = cartesian_testing_batch(np.arange(num_test), backend)
+    X_test = rows(res)
+    log(f"test set: {X_test.shape[0]} rows of {num_test} in {time.time() - t0:.1f} s")
+    t1 = time.time()
+    res, st_train = cartesian_testing_batch(np.arange(num_test, num_test + num_train), backend)
+    X_train = rows(res)
+    log(f"training set: {X_train.shape[0]} rows of {num_train} in {time.time() - t1:.1f} s")
+    mean, std = position_stats(X_train, 2)
+    F = dir_features(X_train, mean, std, 2)
+    F_test = dir_features(X_test, mean, std, 2)
+    k = min(minibatch, F.shape[0])
+    tr = DirTrainer(2, device=device, hidden=hidden, minibatch=k, beta=0.95, stop_val=1e-3, seed=seed)
+    B = int(F.shape[0] * 100 / k)
+    fit = tr.fit(F, it_max=max(1, B * 100))
+    rmse_train, rmse_test = tr.rmse(F), tr.rmse(F_test)
+    log(f"fit {fit}  RMSE train {rmse_train:.4g} test {rmse_test:.4g}")
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        tag = f"2dof_vboc_10_{hidden}"
+        np.save(os.path.join(out_dir, "data_2dof_vboc_10.npy"), X_train)
+        torch.save({kk: v.detach().cpu() for kk, v in tr.model.state_dict().items()}, os.path.join(out_dir, "model_" + tag))
+        torch.save(mean, os.path.join(out_dir, "mean_" + tag))
+        torch.save(std, os.path.join(out_dir, "std_" + tag))
+    return dict(X_test=X_test, X_train=X_train, fit=fit, rmse_train=rmse_train, rmse_test=rmse_test,
+                stats=(st_test, st_train), mean=mean, std=std)
