@@ -168,10 +168,29 @@ def test_gpu_cartesian_driver_matches_reference():
     assert same >= 0.9 * n, (same, n)
 
 
-def test_capi_refuses_unsupported_constraint_handles():
+def test_capi_path_constraint_argument_errors():
+    """No GPU needed: a NULL handle is an argument error, reported through vboc_last_error."""
     from vboc_amd import lib
-    lib.load()
-    assert "vboc_set_path_constraint" in lib.EXPORTS
+    so = lib.load()
+    assert so.vboc_set_path_constraint(None, 1, 0.0, -1.2, 0.04, 1e6) == -1
+    assert b"NULL" in so.vboc_last_error()
+
+
+@pytest.mark.gpu
+def test_gpu_path_constraint_unsupported_structures():
+    """The circle is the chains' tip: refused for the pendulum (nq = 1); the free-time solver and the device
+    data-generation loop refuse a handle carrying it; kind 0 removes it."""
+    from vboc_amd import lib
+    with pytest.raises(lib.VbocError):
+        lib.Solver(1, 60, slots=256).set_path_constraint(cartesian_constraint())
+    s = lib.Solver(2, 120, slots=256)
+    s.set_path_constraint(cartesian_constraint())
+    import torch
+    with pytest.raises(lib.VbocError):
+        s.data_generation_device(torch.arange(4, dtype=torch.int64, device="cuda:0"), N_start=100)
+    s.set_path_constraint(None)
+    out = s.data_generation_device(torch.arange(4, dtype=torch.int64, device="cuda:0"), N_start=100)
+    assert out["row_cnt"].shape[0] == 4
 
 
 def test_cartesian_run_on_oracle(tmp_path):
