@@ -165,7 +165,8 @@ def test_gpu_cartesian_driver_matches_reference():
             same += a is None
         elif a is not None:
             same += bool(np.allclose(a[0], e[0], atol=1e-5))
-    assert same >= 0.9 * n, (same, n)
+    # measured on MI355X: every problem agrees (profiles/r02y_gpu_driver_agreement.log)
+    assert same >= 0.95 * n, (same, n)
 
 
 def test_capi_path_constraint_argument_errors():

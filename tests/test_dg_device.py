@@ -71,7 +71,8 @@ def test_device_loop_matches_reference_fixture(nq):
     res, _ = data_generation_device(nq, np.array(g["ids"]), lib.Solver(nq, g["N_start"] + 20),
                                     N_start=g["N_start"], seed=g["seed"])
     same, _ = _compare(nq, res, g["results"], 1e-5)
-    assert same >= 0.8 * len(g["ids"]), (same, len(g["ids"]))
+    # measured on MI355X: 12 / 12 (triple), 24 / 24 (double), profiles/r02y_gpu_driver_agreement.log
+    assert same >= 0.95 * len(g["ids"]), (same, len(g["ids"]))
 
 
 @pytest.mark.gpu

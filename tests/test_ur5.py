@@ -292,7 +292,8 @@ def test_ur5_driver_on_gpu_matches_reference():
             same += (got is None) == (ref is None)
         elif np.abs(np.asarray(got) - np.asarray(ref)).max() < 1e-5:
             same += 1
-    assert same >= 0.9 * n, (same, n)
+    # measured on MI355X: every problem agrees (profiles/r02y_gpu_driver_agreement.log)
+    assert same >= 0.95 * n, (same, n)
 
 
 @pytest.mark.gpu
