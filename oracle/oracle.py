@@ -116,6 +116,30 @@ def solve_batch(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe
     return x_out, u_out, res
 
 
+def solve_mult(nq, b, i, opts=None):
+    """Problem i of batch b (ics.Batch layout) with the NLP multipliers at the final iterate
+    (vboc_oracle_solve_mult): returns dict(x [N+1, 2nq], u [N, nq], status, cost, res_stat, pi [N, 2nq],
+    lam_l / lam_u [N+1, 3nq] in the stage layout z_0 = (s, u_0), z_k = (x_k, u_k), z_N = x_N, nu [nq], s)."""
+    N = int(b["N"][i])
+    nx, nz, nxr = 2 * nq, 3 * nq, 2 * nq + 1
+    arrs = [np.ascontiguousarray(b[k][i], dtype=np.float64) for k in
+            ("x_guess", "u_guess", "p", "lbx", "ubx", "lbu", "ubu", "lbx0", "ubx0", "lbxe", "ubxe")]
+    x_out, u_out = np.zeros((N + 1, nxr)), np.zeros((N, nq))
+    row = nx + 2 * nz
+    mult = np.zeros((N + 1) * row + nq + 1)
+    res = np.zeros(1, dtype=RESULT_DTYPE)
+    o = opts if opts is not None else default_opts(**({"lm": 1e-2} if nq == 4 else {}))
+    rc = lib().vboc_oracle_solve_mult(nq, N, *[_p(a) for a in arrs], ctypes.byref(o), _p(x_out), _p(u_out),
+                                      _p(res), _p(mult))
+    if rc != 0:
+        raise RuntimeError(f"oracle solve_mult failed rc={rc}")
+    m = mult[:(N + 1) * row].reshape(N + 1, row)
+    return dict(x=x_out[:, :nx], u=u_out, status=int(res["status"][0]), cost=float(res["cost"][0]),
+                res_stat=float(res["res_stat"][0]), sqp_iter=int(res["sqp_iter"][0]), pi=m[:N, :nx],
+                lam_l=m[:, nx:nx + nz], lam_u=m[:, nx + nz:], nu=mult[(N + 1) * row:(N + 1) * row + nq],
+                s=float(mult[(N + 1) * row + nq]))
+
+
 def cartesian_opts():
     """vboc_opts_t fields of the Cartesian double pendulum's keep-out circle (vboc_amd.systems)."""
     from vboc_amd.systems import cartesian_constraint

@@ -1172,10 +1172,36 @@ void vboc_oracle_rk4_sens(int nq, double h, const double* x, const double* u, do
 /* Solve one OCP given in the reference's layout (nx_ref = 2 nq + 1 with the dt column):
  *   x_guess[(N+1) * nx_ref], u_guess[N * nq], p[nq + 1], lbx/ubx (path), lbu/ubu,
  *   lbx_0/ubx_0 (q_init), lbx_e/ubx_e (q_fin).  Outputs x_out[(N+1) nx_ref], u_out[N nq]. */
+static int solve_impl(int nq, int N, const double* x_guess, const double* u_guess, const double* p,
+                      const double* lbx, const double* ubx, const double* lbu, const double* ubu,
+                      const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
+                      const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* mult);
+
 int vboc_oracle_solve(int nq, int N, const double* x_guess, const double* u_guess, const double* p,
                       const double* lbx, const double* ubx, const double* lbu, const double* ubu,
                       const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
                       const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res) {
+  return solve_impl(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe, ubxe, opts, x_out, u_out,
+                    res, NULL);
+}
+
+/* The same solve, also returning the NLP multipliers at the final iterate (for KKT checks recomputed outside
+ * the oracle, tests/test_oracle_kkt.py): per stage k = 0..N a row of 3 (2 nq) + 2 (3 nq) doubles
+ *   [pi_k (2nq; zero at k = N) | lam_l of z_k (3nq) | lam_u of z_k (3nq)]
+ * with z_0 = (s, u_0), z_k = (x_k, u_k), z_N = x_N (unused entries zero), then nu (nq; the terminal
+ * velocity multiplier) and s. */
+int vboc_oracle_solve_mult(int nq, int N, const double* x_guess, const double* u_guess, const double* p,
+                           const double* lbx, const double* ubx, const double* lbu, const double* ubu,
+                           const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
+                           const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* mult) {
+  return solve_impl(nq, N, x_guess, u_guess, p, lbx, ubx, lbu, ubu, lbx0, ubx0, lbxe, ubxe, opts, x_out, u_out,
+                    res, mult);
+}
+
+static int solve_impl(int nq, int N, const double* x_guess, const double* u_guess, const double* p,
+                      const double* lbx, const double* ubx, const double* lbu, const double* ubu,
+                      const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
+                      const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* mult) {
   const int nxr = 2 * nq + 1;
   prob_t P;
   memset(&P, 0, sizeof(P));
@@ -1233,6 +1259,17 @@ int vboc_oracle_solve(int nq, int N, const double* x_guess, const double* u_gues
     for (int i = 0; i < 2 * nq; ++i) x_out[k * nxr + i] = P.st[k].x[i];
     x_out[k * nxr + 2 * nq] = P.h;
     if (k < N) for (int a = 0; a < nq; ++a) u_out[k * nq + a] = P.st[k].u[a];
+  }
+  if (mult) {
+    const int nx = 2 * nq, nz = 3 * nq, row = nx + 2 * nz;
+    for (int k = 0; k <= N; ++k) {
+      double* m = mult + (size_t)k * row;
+      for (int i = 0; i < row; ++i) m[i] = 0.0;
+      if (k < N) for (int i = 0; i < nx; ++i) m[i] = P.st[k].pi[i];
+      for (int i = 0; i < nz_of(&P, k); ++i) { m[nx + i] = P.st[k].ll[i]; m[nx + nz + i] = P.st[k].lu[i]; }
+    }
+    for (int j = 0; j < nq; ++j) mult[(size_t)(N + 1) * row + j] = P.nu[j];
+    mult[(size_t)(N + 1) * row + nq] = P.s;
   }
   free(P.st);
   return 0;

@@ -33,6 +33,10 @@ int vboc_oracle_solve(int nq, int N, const double* x_guess, const double* u_gues
                       const double* lbx, const double* ubx, const double* lbu, const double* ubu,
                       const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
                       const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res);
+int vboc_oracle_solve_mult(int nq, int N, const double* x_guess, const double* u_guess, const double* p,
+                           const double* lbx, const double* ubx, const double* lbu, const double* ubu,
+                           const double* lbx0, const double* ubx0, const double* lbxe, const double* ubxe,
+                           const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* mult);
 int vboc_oracle_solve_batch(int nq, int B, int Nmax, const int* N, const double* x_guess,
                             const double* u_guess, const double* p, const double* lbx, const double* ubx,
                             const double* lbu, const double* ubu, const double* lbx0, const double* ubx0,

@@ -10,8 +10,8 @@ from scipy.optimize import minimize
 import oracle
 
 
-def slsqp(nq, b, i, maxiter=500, hc=None):
-    """hc: optional (x_c, y_c, lh, uh) - the Cartesian keep-out circle lh <= |tip(x_k) - c|^2 <= uh on
+def slsqp(nq, b, i, maxiter=500, hc=None, start=None):
+    """start: optional (x [N+1, >= 2nq], u [N, nq]) initial point instead of the batch's guess.  hc: optional (x_c, y_c, lh, uh) - the Cartesian keep-out circle lh <= |tip(x_k) - c|^2 <= uh on
     stages 1..N-1 (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160), written here
     independently of the oracle as SLSQP inequality constraints with their own Jacobian."""
     N = int(b["N"][i])
@@ -63,7 +63,7 @@ def slsqp(nq, b, i, maxiter=500, hc=None):
                 bounds.append((b["lbx"][i, j], b["ubx"][i, j]))
             else:
                 bounds.append((b["lbxe"][i, j], b["ubxe"][i, j]) if j < nq else (None, None))
-    xg, ug = b["x_guess"][i], b["u_guess"][i]
+    xg, ug = (b["x_guess"][i], b["u_guess"][i]) if start is None else start
     z0 = np.r_[d @ xg[0, nq:2 * nq], ug[:N].ravel(), xg[1:N + 1, :nx].ravel()]
     lo = [bb[0] if bb[0] is not None else -1e9 for bb in bounds]
     hi = [bb[1] if bb[1] is not None else 1e9 for bb in bounds]

@@ -223,6 +223,15 @@ __device__ unsigned g_dbg_cnt;
 #define SPROF(i)
 #define SPROF_FLUSH
 #endif
+// Per-pass traffic / time split (-DVBOC_REPEAT=p, measurement builds only): pass p of the IPM iteration runs
+// twice.  Every repeatable pass is idempotent (it recomputes its outputs from inputs it does not write), so
+// results are unchanged and (bytes, time) of the build minus the product build's are those of pass p
+// (tools/pass_split.py).  1 prep_pred, 2 factor, 3 acl, 4 vec (predictor), 5 fwd (predictor), 6 prep_corr,
+// 7 vec (corrector), 8 fwd (corrector).
+#ifndef VBOC_REPEAT
+#define VBOC_REPEAT 0
+#endif
+#define VREP(id, stmt) do { stmt; if constexpr (VBOC_REPEAT == (id)) { stmt; } } while (0)
 
 // HC: the Cartesian path-constraint rows (vboc_set_path_constraint; oracle/vboc_oracle.c hc_*, Lane::hc_*) on
 // stages 1..N-1, pendulum chains with the VALU factorisation only.  No change of the stage-record layout: the
@@ -1791,29 +1800,32 @@ struct Coop {
         int q = qp_check();
         if (q == 1 && qcur >= o.qp_max_iter) q = 2;
         if (q != 1) { qst = q; break; }
-        prep_pred();
+        VREP(1, prep_pred());
         CPROF(2)
         bool okf;
-        if constexpr (FM) okf = factor_mfma();
-        else okf = factor();
-        acl_pass();
+        if constexpr (FM) VREP(2, okf = factor_mfma());
+        else VREP(2, okf = factor());
+        VREP(3, acl_pass());
         CPROF(3)
-        const bool okv = vec(ODA, w0, nun);
+        bool okv;
+        VREP(4, okv = vec(ODA, w0, nun));
         CPROF(4)
         if (!(okf && okv)) { qst = -1; break; }
         double aa, c0, c1, c2;
-        fwd<false>(w0, nun, 0.0, aa, c0, c1, c2);
+        VREP(5, fwd<false>(w0, nun, 0.0, aa, c0, c1, c2));
         CPROF(5)
         const double muaff = (c0 + aa * (c1 + aa * c2)) / nbox;
         double sig = muaff / mu;
         sig = fmin(1.0, sig * sig * sig);
         const double smu = sig * mu;
-        prep_corr(smu);
+        VREP(6, prep_corr(smu));
         CPROF(2)
-        if (!vec(OD, w0, nun)) { qst = -1; break; }
+        bool okc;
+        VREP(7, okc = vec(OD, w0, nun));
+        if (!okc) { qst = -1; break; }
         CPROF(4)
         double amax;
-        fwd<true>(w0, nun, smu, amax, c0, c1, c2);
+        VREP(8, fwd<true>(w0, nun, smu, amax, c0, c1, c2));
         CPROF(5)
         const double alpha = fmin(1.0, o.tau * amax);
         update(alpha, smu);

@@ -141,6 +141,12 @@ __device__ __forceinline__ void st_flag(int* p, int v) {
 __device__ __forceinline__ int ld_flag(const int* p) {
   return __hip_atomic_load((int*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Reader side, once per taken result / job (never per poll): a compiler-level barrier after the flag load
+// has returned, so no data load of the published block can be scheduled above the poll loop.  The hardware
+// side needs nothing more: the data loads are issued only after the flag value is in a register (the loop
+// exit depends on it), and the sc1 loads bypass the stale per-XCD L2 state.  A real acquire fence
+// (buffer_inv sc1) would invalidate the whole XCD L2 and evict every other wave's stage records there.
+__device__ __forceinline__ void after_flag() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
 
 template <int NQ>
 struct Dg {
@@ -467,6 +473,7 @@ struct Dg {
   __device__ __forceinline__ void take_result(int ev, int j, int N) {
     const int* dn = &J.spec_done[ev * (DG_SPEC_JOBS + 1) + j];
     while (ld_flag(dn) == 0) __builtin_amdgcn_s_sleep(8);
+    after_flag();
     const double* r = spec_res(ev, j);
     for (int e = t; e < (N + 1) * NXR; e += 64) ((double*)in.xo)[row(0) * NXR + e] = ld_coh(r + 4 + e);
     for (int e = t; e < N * NU; e += 64)
@@ -861,6 +868,7 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
           int e;
           while ((e = ld_flag(&J->spec_q[h])) == 0) __builtin_amdgcn_s_sleep(2);
+          after_flag();
           got = e - 1;
         }
       }
@@ -872,6 +880,7 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
         if (t == 0 && ld_flag(&J->spec_cancel[ev]) == 0)
           ok = atomicCAS(&J->spec_claim[ev * (DG_SPEC_JOBS + 1) + jj], 0, 1) == 0 ? 1 : 0;
         if (!dg_bcast(ok)) continue;
+        after_flag();
         dg_spec_prepare<NQ>(J, inp, wg, t, ev, jj);
         mode = 2;
         code = 1;
