@@ -12,11 +12,18 @@ Workloads (--workload):
                W*B / K*B problems: a launch is bound by throughput plus its single slowest problem (the
                critical problem, reported under loop.tail), which a launch per step would pay K times.
                Default B = 20k (the driver's 5 + 20 steps then cover configs[2]'s 100k states five times).
+               The warmup launch (W * B problems; 5 x 20k = 100k = one configs[2] round at the driver's
+               command) is timed too and reported as loop.configs2_round: a single round pays its own tail.
   first-solve  one step = the first OCP solve of data_generation for B problems (IC law, straight-line
                guess, N = 100) on the wave solver, inputs resident in HBM, then (N > 1) the all-gather of
-               the boundary states x0.
-Problem ids are a global counter (Philox per id): rank r takes ids [(step * world + r) * B, ... + B), so
+               the boundary states x0.  The inputs of `--max-batches` distinct batches (ids of steps
+               0 .. max_batches - 1) are built before timing; step s solves batch s mod max_batches.
+dg-loop problem ids are a global counter (Philox per id): rank r takes ids [(step * world + r) * B, ... + B), so
 per-GPU work is fixed as N grows (weak scaling).
+`value` counts OCP solves: for the dg-loop every solve the loop issues (its first, horizon-extension and
+verification solves, ~4.4 per problem for the triple - `value_counts` in the line says so), for first-solve
+one per problem; loop.boundary_problems_per_s is the per-problem rate.  The two workloads' values are not
+comparable with each other.
 
 Output: ONE JSON line on rank 0 (contract in the task statement), with
   roofline     the dominant kernel (k_dg / k_wave: the whole step is one launch): algorithmic FP64 flops of
@@ -269,7 +276,13 @@ def run(args, engine_factory=None):
         if count == 0:
             return
         ids = np.concatenate([shard_ids(first + k, world, rank, B) for k in range(count)])
+        tw = time.perf_counter()
         out = engine.dg(ids)
+        if not timed:   # the warmup launch: one round of count * B problems, reported apart (loop.configs2_round)
+            engine.sync()
+            st = out["stats"].cpu().numpy()
+            rec["round"] = dict(problems=int(count * B), wall_s=time.perf_counter() - tw, kernel_ms=engine.kernel_ms(),
+                                solves=float(st[:, 0].sum()), stats=st)
         for k in range(count):
             sl = slice(k * B, (k + 1) * B)
             X = order_rows(dict(row_cnt=out["row_cnt"][sl], row_off=out["row_off"][sl], rows_all=out["rows_all"]))
@@ -351,6 +364,11 @@ def run(args, engine_factory=None):
                     "unit": "TFLOP/s", "frac": round(tf / FP64_PEAK_TFLOPS, 5) if tf else None,
                     "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
                     "traffic_source": src,
+                    "bound_note": "'mfma' names the roofline that applies (FP64 compute: ~3.6 kflop per algorithmic "
+                                  "byte, far right of the ridge), not what binds: the SQ counters show a latency-bound "
+                                  "kernel (waves 31 % parked in s_waitcnt, 31 % dependency-stalled, 38 % issuing, "
+                                  "VALU 23 %; MFMA ~1 % busy) whose resident problems are capped by the 256 MiB MALL "
+                                  "(DESIGN.md section 5; profiles/r03_*)",
                     "pipes": "FP64: Riccati factorisation on v_mfma_f64_16x16x4f64 (factor_mfma), the rest FP64 VALU; "
                              "peak = FP64 dense (vector = matrix on MI355X); latency-bound dependent recursions",
                     "algorithmic": "FP64 flops per launch, SURVEY.md 8(d): sum over solves of "
@@ -400,6 +418,8 @@ def run(args, engine_factory=None):
                    "sqp_iter_max": round(float(sqp.max()), 1)},
     }
     if dgl:
+        line["value_counts"] = ("loop solves: every OCP solve the data-generation loop issues (first, horizon-extension "
+                                "and verification solves)")
         line["loop"] = {"boundary_problems_per_s": round(problems / elapsed, 2),
                         "solves_per_problem": round(solves / problems, 3),
                         "samples": int(rows), "samples_per_s": round(rows / elapsed, 1), "tail": tail,
@@ -409,6 +429,20 @@ def run(args, engine_factory=None):
                                                          "chains run ahead on waves the problem queue no longer "
                                                          "feeds; only used ones are in value (as the problem's "
                                                          "own solves)"}}
+        rd = rec.get("round")
+        if rd is not None and rank == 0:
+            from vboc_amd.lib import DG_CLOCK_HZ
+            st = rd["stats"]
+            ms = 1e3 / DG_CLOCK_HZ
+            line["loop"]["configs2_round"] = {
+                "problems": rd["problems"], "solves": int(rd["solves"]),
+                "solves_per_s": round(rd["solves"] / rd["wall_s"], 2),
+                "boundary_problems_per_s": round(rd["problems"] / rd["wall_s"], 2),
+                "wall_s": round(rd["wall_s"], 2), "kernel_ms": round(rd["kernel_ms"], 1),
+                "critical_problem_ms": round(float((st[:, 6] - st[:, 5]).max()) * ms, 1),
+                "queue_drained_ms": round(float(st[:, 5].max() - st[:, 5].min()) * ms, 1),
+                "note": "the warmup launch: W x B problems as ONE round (5 x 20k = configs[2]'s 100k states at the "
+                        "driver's command), wall time incl. the first launch; rank 0's shard"}
     if world > 1:
         dist.destroy_process_group()
     return line

@@ -24,6 +24,8 @@ def main():
     nq = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 16384
     s = lib.Solver(nq, 100, device=0)
+    if os.environ.get("VBOC_GROUPS"):   # resident problems (default: the MALL budget)
+        s.set_option("wave_groups", int(os.environ["VBOC_GROUPS"]))
     tb = make_batch(nq, np.arange(B), "cuda:0")
     out = s.solve_device(tb)
     torch.cuda.synchronize()
@@ -35,6 +37,7 @@ def main():
     for k in ("status", "sqp_iter", "qp_iter", "cost", "x"):
         h.update(out[k].cpu().numpy().tobytes())
     print(json.dumps({"lib": os.path.basename(os.environ.get("VBOC_LIB") or "libvboc_amd.so"), "nq": nq, "B": B,
+                      "groups": s.get_option("wave_groups"),
                       "kernel_ms": ms, "qp_iter": int(qp.sum()), "sqp_iter": int(sqp.sum()),
                       "stage_ipm_iters": int((N * qp).sum()), "stage_sqp_iters": int((N * sqp).sum()),
                       "digest": h.hexdigest()}), flush=True)
