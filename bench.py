@@ -171,30 +171,39 @@ class GpuEngine:
 
 def cpu_baseline(nq, workload, B, seconds, threads):
     """Oracle (CPU FP64 restatement, oracle/) on the first problems of the same workload for ~`seconds`:
-    first-solve - batches of first solves, one problem per OpenMP thread; dg-loop - the batched
-    data_generation driver (vboc_amd.drivers, the restatement pinned against the reference's own
-    function) with the oracle as its solver and twin integrator."""
+    first-solve - batches of first solves, one problem per OpenMP thread; dg-loop - the reference's loop at
+    full speed: oracle/vboc_dg.c, the C restatement of data_generation (pinned bit for bit to the reference's
+    own function), one problem per OpenMP thread with no rounds - as the reference's Pool.map runs it - first
+    on 4 problems per thread to size the sample, then on as many as fill the remaining time."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     from vboc_amd.ics import data_generation_ics, ur5_ics
+    if workload == "dg-loop":
+        n, start, solves, t_total = 4 * threads, 0, 0, 0.0
+        for _ in range(2):
+            t0 = time.time()
+            _, st = oracle.data_generation(nq, np.arange(start, start + n), nthreads=threads)
+            t_total += time.time() - t0
+            solves += st["solves"]
+            start += n
+            left = seconds - t_total
+            if left <= 0.1 * seconds:
+                break
+            n = max(threads, int(start / t_total * left))
+        return solves / t_total, start, solves, t_total
     done, solves, t_total, start = 0, 0, 0.0, 0
     n = max(threads, 8)
     while t_total < seconds and start < B:
         ids = np.arange(start, start + n)
         t0 = time.time()
-        if workload == "dg-loop":
-            from vboc_amd.drivers import data_generation_batch
-            _, st = data_generation_batch(nq, ids, oracle.DriverBackend(nq, threads))
-            solves += st["solves"]
-        else:
-            b = ur5_ics(ids) if nq == 4 else data_generation_ics(nq, ids)
-            oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
-                               b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], nthreads=threads)
-            solves += n
+        b = ur5_ics(ids) if nq == 4 else data_generation_ics(nq, ids)
+        oracle.solve_batch(nq, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                           b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], nthreads=threads)
+        solves += n
         t_total += time.time() - t0
         done += n
         start += n
-        n = min(4 * n, max(threads, 8) * (16 if workload == "dg-loop" else 64))
+        n = min(4 * n, max(threads, 8) * 64)
     return solves / t_total, done, solves, t_total
 
 
@@ -339,7 +348,7 @@ def run(args, engine_factory=None):
         threads = len(os.sched_getaffinity(0))
         threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
         v, n, ns, t = cpu_baseline(nq, args.workload, B, args.cpu_seconds, threads)
-        what = ("the batched data_generation driver on the oracle (oracle/vboc_oracle.c, OpenMP)" if dgl
+        what = ("data_generation in C (oracle/vboc_dg.c + vboc_oracle.c), one problem per OpenMP thread" if dgl
                 else "first solves on oracle/vboc_oracle.c (OpenMP)")
         cpu = {"value": round(v, 2), "unit": "solves/s", "cores": threads, "kind": "port",
                "sample": f"first {n} problems of the same workload ({ns} OCP solves), {what}, {t:.1f} s"}

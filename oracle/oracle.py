@@ -156,6 +156,44 @@ def hc_value(x):
     return (X - c.x_c) ** 2 + (Y - c.y_c) ** 2
 
 
+def data_generation(nq, ids, N_start=None, seed=None, fail_mod=0, nthreads=None):
+    """The reference's data_generation(v) for every problem id (vboc_dg.c: the C restatement, one problem per
+    OpenMP thread, the oracle as solver and twin integrator).  Returns (results, stats) in the format of
+    vboc_amd.drivers.data_generation_batch: results[i] = list of saved rows or None (triple), the 3-tuple
+    (samples | None, ic | None, ic | None) (double); stats = dict(solves, rk4, sqp_iter, per_problem [B, 3])."""
+    from vboc_amd.ics import SEED
+    from vboc_amd.systems import system
+    sd = system(nq)
+    N_start = int(N_start or sd.N)
+    seed = SEED if seed is None else int(seed)
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    B, nx = ids.shape[0], 2 * nq
+    max_rows = 2 * (N_start + 16) + 2
+    m = (list(sd.m) + [0.0, 0.0])[:2]
+    l = (list(sd.l) + [0.0, 0.0])[:2]
+    params = np.array([sd.q_min, sd.q_max, sd.v_max, sd.u_max, sd.dt, sd.tol, sd.eps, sd.g, l[0], l[1], m[0], m[1]])
+    rows = np.zeros((B, max_rows, nx))
+    cnt = np.zeros(B, np.int32)
+    ic = np.zeros((B, 4))
+    slot = np.zeros(B, np.int32)
+    st = np.zeros((B, 3), np.int64)
+    rc = lib().vboc_oracle_data_generation(nq, B, _p(ids), ctypes.c_ulonglong(seed), N_start, _p(params), int(fail_mod),
+                                          int(nthreads or os.cpu_count()), max_rows, _p(rows), _p(cnt), _p(ic),
+                                          _p(slot), _p(st))
+    if rc != 0 or (cnt > max_rows).any():
+        raise RuntimeError(f"oracle data_generation failed rc={rc}")
+    results = []
+    for b in range(B):
+        samples = None if cnt[b] < 0 else [r.tolist() for r in rows[b, :cnt[b]]]
+        if nq == 2:
+            icb = [int(ic[b, 0])] + ic[b, 1:].tolist()
+            results.append((samples, icb, None) if slot[b] == 1 else (None, None, icb))
+        else:
+            results.append(samples)
+    return results, dict(solves=int(st[:, 0].sum()), rk4=int(st[:, 1].sum()), sqp_iter=int(st[:, 2].sum()),
+                         per_problem=st)
+
+
 class DriverBackend:
     """The oracle behind the batched drivers' backend interface (vboc_amd.drivers: solve(batch),
     rk4(x, u, T)) - the CPU baseline of bench.py's dg-loop leg and the tests' reference runs."""

@@ -53,6 +53,10 @@ int vboc_oracle_ft_solve_batch(int nq, int B, int Nmax, const int* N, const doub
                                const double* lbu, const double* ubu, const double* lbx0, const double* ubx0,
                                const double* lbxe, const double* ubxe, const vboc_opts_t* opts, int nthreads,
                                double* x_out, double* u_out, vboc_result_t* res);
+/* data_generation of the triple / double pendulum, one problem per OpenMP thread (vboc_dg.c) */
+int vboc_oracle_data_generation(int nq, int B, const long long* ids, unsigned long long seed, int N_start,
+                                const double* params, int fail_mod, int nthreads, int max_rows, double* rows,
+                                int* row_cnt, double* ic, int* ic_slot, long long* stats);
 #ifdef __cplusplus
 }
 #endif
