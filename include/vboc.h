@@ -199,6 +199,40 @@ typedef struct {
   long long spec_used;     /* OUT: of them, taken by their problem (the rest is extra work, never counted) */
 } vboc_dg_batch_t;
 int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* batch, void* stream);
+/* The same launch, returning once it is queued on `stream` (the VBOC loop's streaming producer,
+ * vboc_amd/pipeline.py): done_flag[B] (device ints, zeroed by the caller; may be NULL) gets 1 for each problem
+ * once its rows, row_off, row_cnt, ic and stats are in memory - a system-scope release, so a copy or kernel on
+ * another stream may read that problem's results while the launch runs; cancel (a device int, may be NULL),
+ * set by the caller while the launch runs, makes the problems not yet started return at once with
+ * row_cnt -3.  vboc_data_generation_wait ends the launch (synchronises `stream`, fills rows_used and the
+ * speculation counts, reports pool overflow).  No other call may use the handle in between.
+ * Replaces the reference's synchronous Pool(30).map per VBOC iteration (VBOC/triplependulum_vboc.py:493-506)
+ * by one producer over every iteration's problems. */
+int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* batch, int* done_flag, const int* cancel,
+                               void* stream);
+int vboc_data_generation_wait(vboc_handle h, vboc_dg_batch_t* batch, void* stream);
+
+/* The HJR one-step OCP, OCP<sys>.compute_problem(x0) of HJR/<sys>_hjr_class.py (triplependulum_hjr_class.py:
+ * 117-134 with the model and options of :7-115), for every x0 of a batch, one problem per GPU lane (hjr.h):
+ * x0 fixed, N = 1, h = 1e-2, u0 in [-u_max, u_max], terminal cost = logit 0 of NeuralNetCLS(2nq, hidden, 2)
+ * ((x - mean) / std, Linear, ReLU, Linear, ReLU, Linear; my_nn.py:4-18, built by nn_decisionfunction :135-152),
+ * the classes' SQP options (ACADOS default tolerances).  Device pointers; asynchronous on `stream`.
+ *   x0[B][2nq]; W0[hidden][2nq], b0[hidden], W1[hidden][hidden], b1[hidden], W2[2][hidden], b2[2] (FP64 copies of
+ *   model.parameters()); status[B] (compute_problem returns status == 0), cost[B] (get_cost: the network's
+ *   logit 0 at x1), u[B][nq], x1[B][2nq], sqp_iter[B], qp_iter[B].  hidden must be 100 (the reference's). */
+typedef struct {
+  int B, hidden;
+  const double* x0;
+  const double *W0, *b0, *W1, *b1, *W2, *b2;
+  double mean, std, u_max;
+  int* status;
+  double* cost;
+  double* u;
+  double* x1;
+  int* sqp_iter;
+  int* qp_iter;
+} vboc_hjr_batch_t;
+int vboc_hjr_solve_batch(vboc_handle h, const vboc_hjr_batch_t* batch, void* stream);
 
 /* Device time of the last vboc_solve_batch* call's solver kernel in milliseconds (HIP events on
  * the call's stream) and the number of kernel launches it used. */

@@ -140,6 +140,32 @@ def solve_mult(nq, b, i, opts=None):
                 s=float(mult[(N + 1) * row + nq]))
 
 
+def hjr_solve_batch(nq, x0, weights, mean, std, u_max=None, opts=None, nthreads=None):
+    """The HJR one-step OCP (compute_problem of HJR/<sys>_hjr_class.py) for every row of x0 [B, 2nq]
+    (vboc_oracle_hjr.c).  weights: the NeuralNetCLS parameters in model.parameters() order (W0, b0, W1, b1, W2,
+    b2).  Returns dict(status, cost, sqp_iter, qp_iter, res_stat, u [B, nq], x1 [B, 2nq], pi, lam_l, lam_u)."""
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    B = x0.shape[0]
+    W = [np.ascontiguousarray(np.asarray(w, dtype=np.float64)) for w in weights]
+    h = W[0].shape[0]
+    if opts is None:
+        opts = Opts()
+        lib().vboc_oracle_hjr_default_opts(nq, ctypes.byref(opts))
+    u_max = float(u_max if u_max is not None else (3.0 if nq == 1 else 10.0))
+    u, x1 = np.zeros((B, nq)), np.zeros((B, 2 * nq))
+    mult = np.zeros((B, 2 * nq + 2 * nq))
+    res = np.zeros(B, dtype=RESULT_DTYPE)
+    rc = lib().vboc_oracle_hjr_solve_batch(nq, B, _p(x0), h, *[_p(w) for w in W], ctypes.c_double(mean),
+                                           ctypes.c_double(std), ctypes.c_double(u_max), ctypes.byref(opts),
+                                           int(nthreads or os.cpu_count()), _p(u), _p(x1), _p(mult), _p(res))
+    if rc != 0:
+        raise RuntimeError(f"oracle hjr_solve_batch failed rc={rc}")
+    nx = 2 * nq
+    return dict(status=np.array(res["status"]), cost=np.array(res["cost"]), sqp_iter=np.array(res["sqp_iter"]),
+                qp_iter=np.array(res["qp_iter"]), res_stat=np.array(res["res_stat"]), u=u, x1=x1, pi=mult[:, :nx],
+                lam_l=mult[:, nx:nx + nq], lam_u=mult[:, nx + nq:])
+
+
 def cartesian_opts():
     """vboc_opts_t fields of the Cartesian double pendulum's keep-out circle (vboc_amd.systems)."""
     from vboc_amd.systems import cartesian_constraint

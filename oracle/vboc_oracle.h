@@ -53,6 +53,12 @@ int vboc_oracle_ft_solve_batch(int nq, int B, int Nmax, const int* N, const doub
                                const double* lbu, const double* ubu, const double* lbx0, const double* ubx0,
                                const double* lbxe, const double* ubxe, const vboc_opts_t* opts, int nthreads,
                                double* x_out, double* u_out, vboc_result_t* res);
+/* HJR one-step OCP (vboc_oracle_hjr.c): x0 fixed, N = 1, terminal cost = logit 0 of NeuralNetCLS */
+void vboc_oracle_hjr_default_opts(int nq, vboc_opts_t* o);
+int vboc_oracle_hjr_solve_batch(int nq, int B, const double* x0, int h, const double* W0, const double* b0,
+                                const double* W1, const double* b1, const double* W2, const double* b2, double mean,
+                                double std, double u_max, const vboc_opts_t* opts, int nthreads, double* u_out,
+                                double* x1_out, double* mult_out, vboc_result_t* res);
 /* data_generation of the triple / double pendulum, one problem per OpenMP thread (vboc_dg.c) */
 int vboc_oracle_data_generation(int nq, int B, const long long* ids, unsigned long long seed, int N_start,
                                 const double* params, int fail_mod, int nthreads, int max_rows, double* rows,

@@ -32,9 +32,12 @@ out for its test and training sets) is extracted the same way and run against th
 The Cartesian double pendulum's `testing_test` (VBOC/Cartesian constraints/vboc_multiprocessing.py:19-129) is
 run the same way on the drop-in vboc_amd.cartesian.OCPdoublependulumINIT (keep-out circle on the oracle).
 
-Usage: python tests/golden/make_driver_golden.py [dg|test|pend|ur5|cart]
+The HJR labelling function data_generation(v) (HJR/triplependulum_hjr.py:21-40) is run the same way on a fake
+`ocp` whose compute_problem solves the HJR one-step OCP on the oracle (vboc_oracle_hjr.c).
+
+Usage: python tests/golden/make_driver_golden.py [dg|test|pend|ur5|cart|hjr]
   ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json, tests/golden/driver_1.json,
-      tests/golden/testing_ur5.json, tests/golden/testing_cartesian.json
+      tests/golden/testing_ur5.json, tests/golden/testing_cartesian.json, tests/golden/hjr_3.json (+ hjr_net_3.npz)
 """
 import ast
 import json
@@ -295,8 +298,53 @@ def main_cartesian():
                    "results": out}, f)
 
 
+def main_hjr():
+    """The HJR labelling function data_generation(v) of HJR/triplependulum_hjr.py:21-40, AST-extracted and run
+    over 96 candidate states with injected globals: Xu_iter / y_pred (candidates and a classifier prediction),
+    the state box, and `ocp` = an object with compute_problem(x0) / ocp_solver.get_cost() solving the HJR one-step
+    OCP on the oracle (vboc_oracle_hjr.c).  The network: NeuralNetCLS(6, 100, 2) with seeded torch initialisation,
+    stored beside the fixture (tests/golden/hjr_net_3.npz; mean 1.5, std 4.5)."""
+    import oracle
+    import torch
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(6, 100), torch.nn.ReLU(), torch.nn.Linear(100, 100), torch.nn.ReLU(),
+                              torch.nn.Linear(100, 2))
+    W = [p.detach().numpy().astype(np.float64) for p in net.parameters()]
+    np.savez(os.path.join(HERE, "hjr_net_3.npz"), *W)
+    mean, std = 1.5, 4.5
+    rng = np.random.default_rng(3)
+    X = np.c_[rng.uniform(3 * np.pi / 4 - 0.1, 5 * np.pi / 4 + 0.1, (96, 3)), rng.uniform(-11, 11, (96, 3))]
+    pred = (rng.random(96) < 0.7).astype(np.int64)
+
+    class Solver:
+        cost = None
+
+        def get_cost(self):
+            return self.cost
+
+    class HjrOcp:
+        ocp_solver = Solver()
+
+        def compute_problem(self, x0):
+            r = oracle.hjr_solve_batch(3, np.asarray(x0)[None], W, mean, std, nthreads=1)
+            self.ocp_solver.cost = float(r["cost"][0])
+            return 1 if r["status"][0] == 0 else 0
+
+    code = extract(os.path.join(os.path.dirname(REF), "HJR", "triplependulum_hjr.py"))
+    g = dict(np=np, ocp=HjrOcp(), Xu_iter=X, y_pred=pred, q_max=np.pi / 4 + np.pi, q_min=-np.pi / 4 + np.pi,
+             v_max=10.0, v_min=-10.0)
+    exec(code, g)
+    out = [g["data_generation"](v) for v in range(X.shape[0])]
+    json.dump({"nq": 3, "mean": mean, "std": std, "X": X.tolist(), "y_pred": pred.tolist(),
+               "results": [[None if s is None else np.asarray(s).tolist(), o] for s, o in out]},
+              open(os.path.join(HERE, "hjr_3.json"), "w"))
+    print("hjr_3.json", sum(o is not None and o[0] == 0 for _, o in out), "labelled viable of", len(out))
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("hjr", "all"):
+        main_hjr()
     if what in ("dg", "all"):
         main()
     if what in ("test", "all"):

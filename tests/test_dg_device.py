@@ -173,3 +173,33 @@ def test_speculative_restarts_change_nothing():
     oa, ob = a["row_off"].cpu().numpy(), b["row_off"].cpu().numpy()
     for i in np.flatnonzero(cnt > 0):
         np.testing.assert_array_equal(ra[oa[i]:oa[i] + cnt[i]], rb[ob[i]:ob[i] + cnt[i]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq", [3, 2])
+def test_streamed_rounds_equal_one_synchronous_launch(nq):
+    """The VBOC loop's streaming producer (pipeline.StreamedRounds: one vboc_data_generation_async launch over
+    several iterations' ids, each iteration taken as soon as its problems' done flags are released) returns per
+    iteration exactly what a synchronous launch over the same ids returns; cancelling after the second
+    iteration skips the rest (row_cnt -3) and the launch ends."""
+    from vboc_amd import lib
+    from vboc_amd.drivers import data_generation_device
+    from vboc_amd.pipeline import StreamedRounds
+    n, R = 96, 5
+    s = lib.Solver(nq, 120)
+    prod = StreamedRounds(nq, s, R, n, first_id=5000)
+    got = [prod.round(r)[0] for r in range(2)]
+    prod.cancel()
+    info = prod.close()
+    assert info["seconds"] > 0
+    cnt = prod.out["row_cnt"].cpu().numpy()
+    assert (cnt[:2 * n] >= -1).all() and (cnt >= -3).all()
+    ref, _ = data_generation_device(nq, np.arange(5000, 5000 + 2 * n), lib.Solver(nq, 120))
+    for r in range(2):
+        for a, b in zip(got[r], ref[r * n:(r + 1) * n]):
+            if nq == 2:
+                assert a[1:] == b[1:]
+                a, b = a[0], b[0]
+            assert (a is None) == (b is None)
+            if a is not None:
+                np.testing.assert_array_equal(np.asarray(a), np.asarray(b))

@@ -186,6 +186,21 @@ def test_gather_samples_ragged_two_ranks():
         np.testing.assert_array_equal(got[r], exp)
 
 
+def test_chunked_sampler_is_the_single_topk_subset():
+    """A range longer than TOPK_CHUNK is sampled as the top-k of per-chunk top-k candidates: the same index set
+    as one top-k over all keys, distinct and inside [lo, hi)."""
+    from vboc_amd.learn import DirTrainer
+    tr = DirTrainer(3, "cpu", graphs=False)
+    for chunk, n, k in [(1000, 5500, 64), (1000, 4000, 1000), (4096, 4097, 2048)]:
+        tr.TOPK_CHUNK = chunk
+        tr.gen.manual_seed(5)
+        idx = tr._sample(10, 10 + n, k)
+        g = torch.Generator()
+        g.manual_seed(5)
+        ref = torch.topk(torch.rand(n, generator=g), k).indices + 10
+        assert sorted(idx.tolist()) == sorted(ref.tolist())
+
+
 @pytest.mark.gpu
 def test_trainer_graph_replay_equals_eager_on_gpu():
     """HIP-graph replay (poll every 64 steps, gated updates) == eager per-step loop, on cuda:0."""
@@ -217,3 +232,21 @@ def test_vboc_loop_on_gpu(tmp_path):
     assert all(np.isfinite(out["rmse"]))
     art = load_artifacts(str(tmp_path), nq, device="cuda")
     np.testing.assert_array_equal(art["rmse"], out["rmse"])
+
+
+@pytest.mark.gpu
+def test_large_refit_with_graphs_on_gpu():
+    """A refit at configs[2]'s scale (1.5M old + 1.5M new feature rows, HIP-graph replay) runs and samples inside
+    each half: the 1.5M-key top-k this replaced faulted the GPU (profiles/r03f_vboc_loop_fault.log)."""
+    from vboc_amd.learn import DirTrainer
+    nq = 3
+    n = 3_000_000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    F = torch.rand((n, 2 * nq + 1), device="cuda", generator=g)
+    tr = DirTrainer(nq, "cuda", seed=2, graphs=True, poll=64)
+    tr.it_max = 10**9
+    r = tr.fit(F, n_new=n // 2, it_max=256)
+    assert r["iterations"] == 255 and np.isfinite(r["val"])
+    idx = tr._sample(n // 2, n, 2048)
+    assert idx.min().item() >= n // 2 and idx.max().item() < n and torch.unique(idx).numel() == 2048

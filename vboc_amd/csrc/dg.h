@@ -53,6 +53,12 @@ struct DgJobs {
   unsigned long long* rows_next;
   unsigned* err;               // [0] pool overflow, [1] horizon > nmax
   unsigned* done;
+  // streaming consumers (vboc_data_generation_async): done_flag[job] = 1 once the job's results (rows, row_off,
+  // row_cnt, ic, stats) are in memory - a system-scope release store, so a host copy or a kernel on another
+  // stream sees them while the launch runs; cancel: a host-written word, set = the jobs not yet started are
+  // skipped (row_cnt -3).  Either may be nullptr.
+  int* done_flag;
+  const int* cancel;
   // speculative restarts (see "Speculative restarts" below); spec_events == 0 switches them off
   int spec_events, spec_stride;   // events in the pool, doubles per event
   double* spec;                   // [spec_events][spec_stride]: snapshot header, then DG_SPEC_JOBS results
@@ -785,6 +791,27 @@ struct Dg {
       st[DG_T1] = (double)__builtin_amdgcn_s_memrealtime();
       st[DG_ST1] = s->st1;
       st[DG_IT1] = s->it1;
+    }
+    publish(job);
+  }
+  // a job skipped after the host cancelled the launch: no work, row_cnt -3
+  __device__ __forceinline__ void skip(int job_) {
+    job = job_;
+    if (t == 0) {
+      J.row_off[job] = 0;
+      J.row_cnt[job] = -3;
+      if (J.ic) J.ic_slot[job] = 0;
+      double* st = J.stats + (long long)job * DG_NSTAT;
+      for (int c = 0; c < DG_NSTAT; ++c) st[c] = 0.0;
+    }
+    publish(job);
+  }
+  // every lane's result stores complete (the barrier drains them into L2), then one system-scope release
+  // store of the job's done flag (written back past the non-coherent per-XCD L2s), then the finished count
+  __device__ __forceinline__ void publish(int job_) {
+    __syncthreads();
+    if (t == 0) {
+      if (J.done_flag) __hip_atomic_store(&J.done_flag[job_], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       atomicAdd(J.done, 1u);
     }
   }
@@ -810,6 +837,11 @@ template <int NQ>
 __device__ __forceinline__ void dg_finish(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
   Dg<NQ> D(*J, *in, wg, t);
   D.finish(job);
+}
+template <int NQ>
+__device__ __forceinline__ void dg_skip(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Dg<NQ> D(*J, *in, wg, t);
+  D.skip(job);
 }
 template <int NQ>
 __device__ __forceinline__ void dg_spec_prepare(const DgJobs* J, const Inputs* in, int wg, int t, int ev, int j) {
@@ -850,6 +882,13 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
         if (i < (unsigned)count) got = (int)i;
       }
       got = dg_bcast(got);
+      int cancelled = 0;
+      if (got >= 0 && J->cancel && t == 0)
+        cancelled = __hip_atomic_load(J->cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (got >= 0 && dg_bcast(cancelled)) {
+        dg_skip<NQ>(J, inp, wg, t, got);
+        continue;
+      }
       if (got >= 0) {
         idx = got;
         mode = 1;

@@ -1446,6 +1446,7 @@ struct WaveJobs {
 #include "coop.h"
 #include "ft.h"
 #include "dg.h"
+#include "hjr.h"
 
 // =================================================================================================
 // C ABI
@@ -2137,7 +2138,21 @@ static int solve_host(vboc_handle h, const vboc_batch_t* b, bool ft) {
 int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, false); }
 int vboc_solve_batch_ft_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, true); }
 
+static int dg_wait(vboc_handle h, vboc_dg_batch_t* b, hipStream_t st);
+
 int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
+  const int rc = vboc_data_generation_async(h, b, nullptr, nullptr, stream);
+  if (rc != VBOC_OK || !b || b->B == 0) return rc;
+  return dg_wait(h, b, (hipStream_t)stream);
+}
+
+int vboc_data_generation_wait(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_data_generation_wait: NULL argument");
+  if (b->B == 0) return VBOC_OK;
+  return dg_wait(h, b, (hipStream_t)stream);
+}
+
+int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const int* cancel, void* stream) {
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_data_generation: NULL argument");
   if (h->nq != 2 && h->nq != 3)
     return fail(VBOC_ERR_UNSUPPORTED, "vboc_data_generation: defined for the double (nq = 2) and triple (nq = 3) pendulum");
@@ -2205,6 +2220,7 @@ int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
   J.eps = b->eps; J.g = b->g; J.l1 = b->l1; J.l2 = b->l2; J.m1 = b->m1; J.m2 = b->m2;
   J.rows = b->rows; J.rows_cap = b->rows_cap; J.row_off = b->row_off; J.row_cnt = b->row_cnt;
   J.ic = h->nq == 2 ? b->ic : nullptr; J.ic_slot = h->nq == 2 ? b->ic_slot : nullptr; J.stats = b->stats;
+  J.done_flag = done_flag; J.cancel = cancel;
   // counters: [0] job queue, [1] finished problems, [2..3] error flags, [4..5] rows used (u64),
   // [6] speculation events, [7] / [8] restart-job queue tail / head, [10..13] speculative solves run / used (u64)
   J.next = h->head; J.done = h->head + 1; J.err = h->head + 2; J.rows_next = (unsigned long long*)(h->head + 4);
@@ -2246,6 +2262,12 @@ int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
   HIPCHK(hipEventRecord(h->ev1, st));
   h->launches = 1;
   h->coop_count = b->B;
+  return VBOC_OK;
+}
+
+// the end of a data-generation launch: its counters, the pool and horizon checks
+static int dg_wait(vboc_handle h, vboc_dg_batch_t* b, hipStream_t st) {
+  HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipMemcpyAsync(h->host_done, h->head, 14 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   const unsigned* c = h->host_done;
@@ -2255,6 +2277,41 @@ int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
   if (c[2]) return fail(VBOC_ERR_NOMEM, "vboc_data_generation: the row pool (rows_cap) overflowed");
   if (c[3]) return fail(VBOC_ERR_HIP, "vboc_data_generation: a horizon exceeded nmax (internal error)");
   if (c[1] != (unsigned)b->B) return fail(VBOC_ERR_HIP, "vboc_data_generation: not every problem finished");
+  return VBOC_OK;
+}
+
+int vboc_hjr_solve_batch(vboc_handle h, const vboc_hjr_batch_t* b, void* stream) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_hjr_solve_batch: NULL argument");
+  if (h->nq > 3) return fail(VBOC_ERR_UNSUPPORTED, "vboc_hjr_solve_batch: defined for the pendulum chains (nq 1-3)");
+  if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_hjr_solve_batch: B < 0");
+  if (b->B == 0) return VBOC_OK;
+  if (b->hidden != 100)
+    return fail(VBOC_ERR_UNSUPPORTED, "vboc_hjr_solve_batch: NeuralNetCLS hidden size 100 (the reference's) only");
+  if (!b->x0 || !b->W0 || !b->b0 || !b->W1 || !b->b1 || !b->W2 || !b->b2 || !b->status || !b->cost || !b->u ||
+      !b->x1 || !b->sqp_iter || !b->qp_iter)
+    return fail(VBOC_ERR_ARG, "vboc_hjr_solve_batch: NULL array");
+  if (!(b->std > 0.0) || !(b->u_max > 0.0)) return fail(VBOC_ERR_ARG, "vboc_hjr_solve_batch: std and u_max must be > 0");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  // the HJR classes' options (HJR/triplependulum_hjr_class.py:98-108): the VBOC SQP / merit settings, the ACADOS
+  // default tolerances (no tol_stat / qp_solver_tol_stat set), levenberg_marquardt 1e-5 (pendulum 1e-2)
+  Opts o;
+  default_opts(o);
+  o.tol_stat = 1e-6;
+  o.qp_tol_stat = 1e-8;
+  o.lm = h->nq == 1 ? 1e-2 : 1e-5;
+  HjrNet net{b->W0, b->b0, b->W1, b->b1, b->W2, b->b2, b->mean, b->std};
+  HjrJobs J{b->B, b->x0, b->u_max, b->status, b->cost, b->u, b->x1, b->sqp_iter, b->qp_iter};
+  const dim3 grid((unsigned)((b->B + 63) / 64)), block(64);
+  HIPCHK(hipEventRecord(h->ev0, st));
+  switch (h->nq) {
+    case 1: hipLaunchKernelGGL((k_hjr<1, 100>), grid, block, 0, st, net, o, J); break;
+    case 2: hipLaunchKernelGGL((k_hjr<2, 100>), grid, block, 0, st, net, o, J); break;
+    default: hipLaunchKernelGGL((k_hjr<3, 100>), grid, block, 0, st, net, o, J); break;
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(h->ev1, st));
+  h->launches = 1;
   return VBOC_OK;
 }
 

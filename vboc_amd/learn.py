@@ -126,9 +126,24 @@ class DirTrainer:
         self.total_steps = 0
 
     # -- one gated step, written with device tensors only (capturable) ---------------------------------
+    # top-k slices are kept at most this long: a uniform k-subset of a long range is the top-k of the per-chunk
+    # top-k candidates (exactly the same index set as one top-k over all keys).  A refit of the triple's VBOC loop
+    # at configs[2]'s scale (3M feature rows, 1.5M per slice) faulted the GPU inside one 1.5M-key top-k replayed
+    # from a HIP graph (profiles/r03f_vboc_loop_fault.log); slices up to 1M had run in the same loop.
+    TOPK_CHUNK = 1 << 18
+
     def _sample(self, lo, hi, k):
-        keys = torch.rand(hi - lo, device=self.device, generator=self.gen)
-        return torch.topk(keys, k, sorted=False).indices + lo
+        n = hi - lo
+        keys = torch.rand(n, device=self.device, generator=self.gen)
+        if n <= self.TOPK_CHUNK:
+            return torch.topk(keys, k, sorted=False).indices + lo
+        c = self.TOPK_CHUNK
+        m = (n + c - 1) // c
+        pad = torch.full((m * c - n,), -1.0, device=self.device)        # keys are in [0, 1): pads never win
+        part = torch.topk(torch.cat([keys, pad]).view(m, c), k, dim=1, sorted=False)
+        cand = part.indices + (torch.arange(m, device=self.device) * c).unsqueeze(1)
+        best = torch.topk(part.values.reshape(-1), k, sorted=False).indices
+        return cand.reshape(-1).index_select(0, best) + lo
 
     def _step(self, F, X, y, n, n_new):
         if n_new:

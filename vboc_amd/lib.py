@@ -20,7 +20,8 @@ SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
            "vboc_solve_batch_host", "vboc_solve_batch_ft", "vboc_solve_batch_ft_host", "vboc_rk4_batch", "vboc_rk4_batch_host",
            "vboc_rk4_sens_batch_host", "vboc_last_kernel_ms",
-           "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_set_path_constraint",
+           "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_data_generation_async",
+           "vboc_data_generation_wait", "vboc_hjr_solve_batch", "vboc_set_path_constraint",
            "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
@@ -50,6 +51,14 @@ class DgBatch(ctypes.Structure):
                 ("row_cnt", ctypes.c_void_p), ("ic", ctypes.c_void_p), ("ic_slot", ctypes.c_void_p),
                 ("stats", ctypes.c_void_p), ("rows_used", ctypes.c_longlong), ("spec_solves", ctypes.c_longlong),
                 ("spec_used", ctypes.c_longlong)]
+
+
+class HjrBatch(ctypes.Structure):
+    """vboc_hjr_batch_t (include/vboc.h): the HJR one-step OCP batch."""
+    _fields_ = [("B", ctypes.c_int), ("hidden", ctypes.c_int), ("x0", ctypes.c_void_p)] + \
+               [(n, ctypes.c_void_p) for n in ("W0", "b0", "W1", "b1", "W2", "b2")] + \
+               [(n, ctypes.c_double) for n in ("mean", "std", "u_max")] + \
+               [(n, ctypes.c_void_p) for n in ("status", "cost", "u", "x1", "sqp_iter", "qp_iter")]
 
 
 # per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
@@ -100,6 +109,10 @@ def load():
                                         ctypes.POINTER(ctypes.c_int)]
     lib.vboc_debug_counters.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
     lib.vboc_data_generation.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_void_p]
+    lib.vboc_data_generation_async.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_void_p,
+                                               ctypes.c_void_p, ctypes.c_void_p]
+    lib.vboc_data_generation_wait.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_void_p]
+    lib.vboc_hjr_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(HjrBatch), ctypes.c_void_p]
     lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
@@ -207,10 +220,14 @@ class Solver:
         return out
 
     # -- device data generation (the whole data_generation state machine per problem on the GPU) ----
-    def data_generation_device(self, ids, N_start=None, seed=None, rows_cap=None, stream=None):
+    def data_generation_device(self, ids, N_start=None, seed=None, rows_cap=None, stream=None, done_flag=None,
+                               cancel=None, wait=True):
         """`data_generation(v)` for every problem id of the int64 cuda tensor `ids` (vboc_data_generation,
         dg.h).  Returns a dict of device tensors: rows [rows_used, 2nq] (blocks per problem), row_off,
-        row_cnt (-1: None), ic / ic_slot (double pendulum), stats [B, 5] (DG_STATS)."""
+        row_cnt (-1: None), ic / ic_slot (double pendulum), stats [B, 5] (DG_STATS).
+        wait=False (vboc_data_generation_async): returns once the launch is queued; done_flag (int32 cuda
+        tensor [B], zeroed) gets 1 per finished problem, cancel (int32 cuda tensor [1]) skips the problems not
+        yet started once set; finish with data_generation_wait(out)."""
         import torch
         from .ics import SEED
         from .systems import system
@@ -236,10 +253,48 @@ class Solver:
                     ic_slot=out["ic_slot"].data_ptr(), stats=out["stats"].data_ptr(), rows_used=0, spec_solves=0,
                     spec_used=0)
         st = stream if stream is not None else torch.cuda.current_stream(dev)
+        out["rows_all"] = rows
+        if not wait:
+            for t in (done_flag, cancel):
+                assert t is None or (t.is_cuda and t.dtype == torch.int32 and t.is_contiguous())
+            _check(self.lib.vboc_data_generation_async(
+                self.h, ctypes.byref(b), ctypes.c_void_p(done_flag.data_ptr() if done_flag is not None else 0),
+                ctypes.c_void_p(cancel.data_ptr() if cancel is not None else 0), ctypes.c_void_p(st.cuda_stream)))
+            out["_batch"], out["_stream"], out["_keep"] = b, st, (ids, done_flag, cancel)
+            return out
         _check(self.lib.vboc_data_generation(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
         out["rows"] = rows[:b.rows_used]
-        out["rows_all"] = rows
         out["spec_solves"], out["spec_used"] = b.spec_solves, b.spec_used
+        return out
+
+    def data_generation_wait(self, out):
+        """End a launch started with data_generation_device(wait=False)."""
+        b, st = out.pop("_batch"), out.pop("_stream")
+        out.pop("_keep", None)
+        _check(self.lib.vboc_data_generation_wait(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        out["rows"] = out["rows_all"][:b.rows_used]
+        out["spec_solves"], out["spec_used"] = b.spec_solves, b.spec_used
+        return out
+
+    def hjr_solve_device(self, x0, weights, mean, std, u_max, stream=None):
+        """The HJR one-step OCP (vboc_hjr_solve_batch, hjr.h) for every row of the float64 cuda tensor x0 [B, 2nq]:
+        weights = the six NeuralNetCLS parameter tensors (float64, cuda, model.parameters() order).  Returns a
+        dict of device tensors: status, cost, u, x1, sqp_iter, qp_iter."""
+        import torch
+        assert x0.is_cuda and x0.dtype == torch.float64 and x0.is_contiguous()
+        W = [w.contiguous() for w in weights]
+        for w in W:
+            assert w.is_cuda and w.dtype == torch.float64
+        B, dev = x0.shape[0], x0.device
+        out = dict(status=torch.empty(B, dtype=torch.int32, device=dev), cost=torch.empty(B, dtype=torch.float64, device=dev),
+                   u=torch.empty((B, self.nq), dtype=torch.float64, device=dev), x1=torch.empty_like(x0),
+                   sqp_iter=torch.empty(B, dtype=torch.int32, device=dev), qp_iter=torch.empty(B, dtype=torch.int32, device=dev))
+        b = HjrBatch(B=B, hidden=W[0].shape[0], x0=x0.data_ptr(), mean=float(mean), std=float(std), u_max=float(u_max),
+                     **{n: w.data_ptr() for n, w in zip(("W0", "b0", "W1", "b1", "W2", "b2"), W)},
+                     **{k: out[k].data_ptr() for k in ("status", "cost", "u", "x1", "sqp_iter", "qp_iter")})
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        _check(self.lib.vboc_hjr_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        out["_keep"] = W
         return out
 
     def kernel_stats(self):

@@ -107,6 +107,93 @@ def _round(nq, backend, iteration, num_prob, N_start, seed):
     return samples_array(nq, res), stats
 
 
+class StreamedRounds:
+    """The data generation of many VBOC iterations as ONE persistent device launch (vboc_data_generation_async).
+
+    The reference regenerates num_prob problems per iteration with a synchronous Pool.map and refits in
+    between (VBOC/triplependulum_vboc.py:493-568); `data_generation` never reads the model, so the ids of every
+    iteration are known up front.  One producer launch on its own stream works through the ids of `rounds`
+    iterations in order, and the host takes iteration r once all of its problems are finished (per-problem done
+    flags, released to memory by the kernel, polled on a side stream) - while iteration r is being fitted on
+    the default stream, the GPU keeps generating r + 1, r + 2, ...; no round pays its own tail.  `cancel()` skips
+    the problems not yet started (the time budget is spent); `close()` ends the launch."""
+
+    def __init__(self, nq, solver, rounds, num_prob, first_id=0, N_start=None, seed=SEED, rows_per_problem=None,
+                 poll_s=0.005):
+        import torch
+        self.torch, self.nq, self.num_prob, self.poll_s = torch, nq, num_prob, poll_s
+        self.solver = solver
+        dev = torch.device("cuda", solver.device)
+        B = rounds * num_prob
+        N_start = int(N_start or system(nq).N)
+        # row pool: at most 2 N + 2 rows per problem (quirk A.3 included); typical is ~25, so a long producer is
+        # sized by rows_per_problem (an overflow is reported by close(), never written out of bounds)
+        rpp = rows_per_problem or (2 * (N_start + 12) + 2 if B <= 50_000 else 100)
+        self.ids = torch.arange(first_id, first_id + B, dtype=torch.int64, device=dev)
+        self.flags = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.cancel_word = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.producer = torch.cuda.Stream(dev)
+        self.side = torch.cuda.Stream(dev)
+        self.host_flags = torch.zeros(num_prob, dtype=torch.int32).pin_memory()
+        torch.cuda.synchronize(dev)
+        self.t_start = time.time()
+        self.out = solver.data_generation_device(self.ids, N_start=N_start, seed=seed, rows_cap=B * rpp,
+                                                 stream=self.producer, done_flag=self.flags, cancel=self.cancel_word,
+                                                 wait=False)
+        self.waited = 0.0
+
+    def round(self, r):
+        """Results of iteration r in problem order (drivers.data_generation_batch's format) and its stats."""
+        torch, n = self.torch, self.num_prob
+        sl = slice(r * n, (r + 1) * n)
+        t = time.time()
+        while True:
+            with torch.cuda.stream(self.side):
+                self.host_flags.copy_(self.flags[sl], non_blocking=True)
+            self.side.synchronize()
+            if bool(self.host_flags.all()):
+                break
+            time.sleep(self.poll_s)
+        self.waited += time.time() - t
+        out = self.out
+        with torch.cuda.stream(self.side):
+            cnt = out["row_cnt"][sl].to("cpu", non_blocking=True)
+            off = out["row_off"][sl].to("cpu", non_blocking=True)
+            st = out["stats"][sl].to("cpu", non_blocking=True)
+            ic, slot = out["ic"][sl].to("cpu", non_blocking=True), out["ic_slot"][sl].to("cpu", non_blocking=True)
+        self.side.synchronize()
+        cnt, off, st, ic, slot = cnt.numpy(), off.numpy(), st.numpy(), ic.numpy(), slot.numpy()
+        if (cnt < -1).any():
+            raise RuntimeError(f"iteration {r}: row pool overflow or cancelled problems")
+        used = cnt > 0
+        lo = int(off[used].min()) if used.any() else 0
+        hi = int((off + np.maximum(cnt, 0))[used].max()) if used.any() else 0
+        with torch.cuda.stream(self.side):
+            block = out["rows_all"][lo:hi].to("cpu", non_blocking=True)   # the round's blocks (released)
+        self.side.synchronize()
+        block = block.numpy()
+        results = []
+        for b in range(n):
+            samples = None if cnt[b] < 0 else block[off[b] - lo:off[b] - lo + cnt[b]].tolist()
+            if self.nq == 2:
+                icb = [int(ic[b, 0])] + ic[b, 1:].tolist()
+                results.append((samples, icb, None) if slot[b] == 1 else (None, None, icb))
+            else:
+                results.append(samples)
+        return results, dict(solves=int(st[:, 0].sum()), rk4=int(st[:, 1].sum()), sqp_iter=int(st[:, 2].sum()),
+                             rounds=1, per_problem=st)
+
+    def cancel(self):
+        with self.torch.cuda.stream(self.side):
+            self.cancel_word.fill_(1)
+        self.side.synchronize()
+
+    def close(self):
+        out = self.solver.data_generation_wait(self.out)
+        return dict(seconds=time.time() - self.t_start, spec_solves=out["spec_solves"], spec_used=out["spec_used"],
+                    waited_s=self.waited)
+
+
 def _agree(flag):
     """Rank 0's decision on every rank (the time budget must not split the ranks' loop counts)."""
     import torch
@@ -121,8 +208,12 @@ def _agree(flag):
 
 
 def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None, N_start=None, seed=SEED,
-             out_dir=None, device=None, trainer_kw=None, triple_refit_quirk=True, log=None):
-    """Run the VBOC loop; returns dict(X_save, mean, std, trainer, times, rmse, stats)."""
+             out_dir=None, device=None, trainer_kw=None, triple_refit_quirk=True, log=None, stream=None,
+             stream_rounds=None):
+    """Run the VBOC loop; returns dict(X_save, mean, std, trainer, times, rmse, stats).
+    stream (default: on the GPU backend in a single process): the iterations' data generation runs as one
+    producer launch ahead of the fits (StreamedRounds) over max_iterations + 1 iterations (or stream_rounds;
+    problems not reached when the time budget is spent are cancelled)."""
     import torch
     import torch.distributed as dist
     if nq not in (2, 3):
@@ -133,7 +224,23 @@ def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None,
     device = device or ("cuda" if torch.cuda.is_available() else "cpu")
     t0 = time.time()
     iteration = 0
-    X_save, st = _round(nq, backend, iteration, num_prob, N_start, seed)
+    solver = getattr(backend, "solver", None)
+    distributed = dist.is_available() and dist.is_initialized()
+    if stream is None:
+        stream = (solver is not None and hasattr(solver, "data_generation_device") and not distributed and
+                  solver.nmax >= (N_start or system(nq).N) + 12)
+    producer = None
+    if stream:
+        R = stream_rounds or ((max_iterations + 1) if max_iterations is not None else 64)
+        producer = StreamedRounds(nq, solver, R, num_prob, N_start=N_start, seed=seed)
+        get_round = lambda it: (lambda r: (samples_array(nq, r[0]), r[1]))(producer.round(it))
+        if max_iterations is None:
+            max_iterations = R - 1
+        else:
+            max_iterations = min(max_iterations, R - 1)
+    else:
+        get_round = lambda it: _round(nq, backend, it, num_prob, N_start, seed)
+    X_save, st = get_round(iteration)
     stats = [st]
     log(f"iteration 0: {X_save.shape[0]} rows")
     mean, std = position_stats(X_save, nq)
@@ -148,7 +255,7 @@ def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None,
         log(f"fit: {fits[-1]}  rmse {rmse[-1]:.4g}")
     while _agree(time.time() - t0 < stop_time and (max_iterations is None or iteration < max_iterations)):
         iteration += 1
-        X_new, st = _round(nq, backend, iteration, num_prob, N_start, seed)
+        X_new, st = get_round(iteration)
         stats.append(st)
         X_save = np.concatenate((X_save, X_new))
         if rank0:
@@ -159,9 +266,14 @@ def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None,
             times.append(time.time() - t0)
             rmse.append(trainer.rmse(F_test))
             log(f"iteration {iteration}: {X_save.shape[0]} rows, fit {fits[-1]}, rmse {rmse[-1]:.4g}")
+    producer_info = None
+    if producer is not None:
+        producer.cancel()
+        producer_info = producer.close()
     if rank0 and out_dir is not None:
         save_artifacts(out_dir, nq, X_save, mean, std, trainer.model, times, rmse)
-    return dict(X_save=X_save, mean=mean, std=std, trainer=trainer, times=times, rmse=rmse, stats=stats, fits=fits)
+    return dict(X_save=X_save, mean=mean, std=std, trainer=trainer, times=times, rmse=rmse, stats=stats, fits=fits,
+                producer=producer_info)
 
 
 def pendulum_vboc_run(out_dir=None, device="cuda", seed=0, backend=None, it_max=None):
