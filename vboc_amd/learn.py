@@ -110,7 +110,8 @@ class DirTrainer:
         self.nin = 2 * nq
         self.device = torch.device(device)
         torch.manual_seed(seed)
-        self.model = NeuralNetDIR(self.nin, hidden or HIDDEN[nq], 1).to(self.device)
+        self.hidden = hidden or HIDDEN[nq]
+        self.model = NeuralNetDIR(self.nin, self.hidden, 1).to(self.device)
         self.k = minibatch or MINIBATCH[nq]
         self.lr, self.beta, self.stop_val = lr, beta, stop_val
         self.b1, self.b2, self.eps = 0.9, 0.999, 1e-8       # torch.optim.Adam defaults (:44)
@@ -128,8 +129,8 @@ class DirTrainer:
     # -- one gated step, written with device tensors only (capturable) ---------------------------------
     # top-k slices are kept at most this long: a uniform k-subset of a long range is the top-k of the per-chunk
     # top-k candidates (exactly the same index set as one top-k over all keys).  A refit of the triple's VBOC loop
-    # at configs[2]'s scale (3M feature rows, 1.5M per slice) faulted the GPU inside one 1.5M-key top-k replayed
-    # from a HIP graph (profiles/r03f_vboc_loop_fault.log); slices up to 1M had run in the same loop.
+    # at configs[2]'s scale faulted the GPU (illegal address, profiles/r03f_vboc_loop_fault.log) in the first fit
+    # whose halves exceeded 2^20 rows; the fits before it (halves of 0.5M rows) had run in the same process.
     TOPK_CHUNK = 1 << 18
 
     def _sample(self, lo, hi, k):
@@ -238,3 +239,106 @@ class DirTrainer:
             else F.to(self.device, torch.float32)
         out = self.predict(F[:, :self.nin])
         return math.sqrt(torch.mean((out - F[:, self.nin:self.nin + 1]) ** 2).item())
+
+
+class HipTrainer(DirTrainer):
+    """DirTrainer's fit on the device kernels of csrc/fit.hip (libvboc_fit.so, include/vboc_fit.h): sampling,
+    forward, backward, Adam and the stop rule of VBOC/triplependulum_vboc.py:446-466 / :526-556 in four kernels
+    per step, `poll` steps per HIP graph.  The torch module stays the source of truth between fits (its
+    parameters are packed into the trainer before a fit and written back after it); Adam's moments and step count
+    live in the trainer across fits, as the reference's one optimizer does.  Differences from DirTrainer: the
+    minibatch draws (Philox, random.sample's redraw-on-repeat set method, instead of the top-k of uniform keys)
+    and val, kept in float64 as the reference's Python float."""
+
+    def __init__(self, nq, device="cuda", hidden=None, minibatch=None, lr=1e-3, beta=0.95, stop_val=1e-3, seed=0,
+                 graphs=True, poll=64):
+        import ctypes
+        from . import fitlib
+        super().__init__(nq, device, hidden=hidden, minibatch=minibatch, lr=lr, beta=beta, stop_val=stop_val,
+                         seed=seed, graphs=False, poll=poll)
+        if self.device.type != "cuda":
+            raise ValueError("HipTrainer runs on a GPU (use DirTrainer on the CPU)")
+        self._fl = fitlib
+        self._lib = fitlib.load()
+        h = ctypes.c_void_p()
+        fitlib.check(self._lib.vboc_fit_create(self.nin, self.hidden, self.k, seed, ctypes.byref(h)))
+        self._h = h
+        self.use_graphs = graphs
+        self.last = None
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.vboc_fit_destroy(h)
+            self._h = None
+
+    def _param_ptrs(self):
+        st = self.model.linear_relu_stack
+        ps = [st[0].weight, st[0].bias, st[2].weight, st[2].bias, st[4].weight, st[4].bias]
+        for p in ps:
+            if not p.is_contiguous() or p.dtype != torch.float32 or not p.is_cuda:
+                raise ValueError("model parameters must be contiguous float32 tensors on the trainer's device")
+        return [p.data_ptr() for p in ps]
+
+    def fit(self, F, n_new=0, it_max=None):
+        import ctypes
+        fl = self._fl
+        if torch.is_tensor(F):
+            Ft = F.to(self.device, torch.float32).contiguous()
+            val0 = float(Ft[:, self.nin].max())
+        else:
+            Fn = np.asarray(F)
+            val0 = float(np.max(Fn[:, self.nin]))          # :446, over the float64 features
+            Ft = torch.as_tensor(Fn, dtype=torch.float32).to(self.device).contiguous()
+        n = Ft.shape[0]
+        if self.it_max is None:
+            self.it_max = int(n * 100 / self.k) * 10
+        it_max = it_max or self.it_max
+        if n_new and (n_new < self.k // 2 or n - n_new < self.k // 2):
+            raise ValueError("a refit needs at least minibatch/2 old and new rows")
+        if not n_new and n < self.k:
+            raise ValueError(f"need at least {self.k} rows (random.sample of a minibatch)")
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        ptrs = self._param_ptrs()
+        fl.check(self._lib.vboc_fit_set_params(self._h, *ptrs, stream))
+        its, val, launched, ms = ctypes.c_longlong(), ctypes.c_double(), ctypes.c_longlong(), ctypes.c_double()
+        run = fl.FitRun(F=Ft.data_ptr(), n=n, n_new=n_new, ld=Ft.shape[1], it_max=it_max, val0=val0,
+                        stop_val=self.stop_val, beta=self.beta, lr=self.lr, poll=self.poll,
+                        graphs=int(self.use_graphs), iterations=ctypes.addressof(its), val=ctypes.addressof(val),
+                        launched=ctypes.addressof(launched), kernel_ms=ctypes.addressof(ms))
+        fl.check(self._lib.vboc_fit_train(self._h, ctypes.byref(run), stream))
+        fl.check(self._lib.vboc_fit_get_params(self._h, 0, *ptrs, stream))
+        self.total_steps += launched.value
+        self.last = dict(iterations=its.value, val=val.value, launched=launched.value, fit_ms=ms.value)
+        return dict(iterations=its.value, val=val.value, launched=launched.value)
+
+    def moments(self):
+        """Adam's (exp_avg, exp_avg_sq) as lists of tensors in the model's parameter order (test hook)."""
+        out = []
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        for which in (1, 2):
+            ts = [torch.empty_like(p) for p in self.model.parameters()]
+            self._fl.check(self._lib.vboc_fit_get_params(self._h, which, *[t.data_ptr() for t in ts], stream))
+            out.append(ts)
+        return out
+
+    def sample(self, n, n_new=0, steps=1):
+        """The sampler's next `steps` minibatches ([steps, k] int32 row indices; test hook)."""
+        out = torch.empty((steps, self.k), dtype=torch.int32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        self._fl.check(self._lib.vboc_fit_sample(self._h, n, n_new, steps, out.data_ptr(), stream))
+        return out
+
+
+def make_trainer(nq, device="cpu", **kw):
+    """The fit of the VBOC loop: the native device trainer (HipTrainer) on a GPU for the shapes it implements
+    (triple 6-500, double / Cartesian 4-300, pendulum 2-100, minibatch <= 4096), else DirTrainer (PyTorch; the CPU
+    tests and the UR5's 8-1000 / 32768 fit)."""
+    from . import fitlib
+    dev = torch.device(device)
+    hidden = kw.get("hidden") or HIDDEN.get(nq, 0)
+    k = kw.get("minibatch") or MINIBATCH.get(nq, 0)
+    if dev.type == "cuda" and fitlib.supported(2 * nq, hidden, k):
+        return HipTrainer(nq, device, **kw)
+    return DirTrainer(nq, device, **kw)
+

@@ -26,7 +26,7 @@ import numpy as np
 
 from .drivers import data_generation_batch, heldout_set, testing_batch
 from .ics import SEED
-from .learn import DirTrainer, dir_features, position_stats
+from .learn import dir_features, make_trainer, position_stats
 from .systems import system
 
 
@@ -246,7 +246,7 @@ def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None,
     mean, std = position_stats(X_save, nq)
     F = dir_features(X_save, mean, std, nq)
     F_test = dir_features(X_test, mean, std, nq)
-    trainer = DirTrainer(nq, device, **(trainer_kw or {})) if rank0 else None
+    trainer = make_trainer(nq, device, **(trainer_kw or {})) if rank0 else None
     times, rmse, fits = [], [], []
     if rank0:
         fits.append(trainer.fit(F))
@@ -290,7 +290,7 @@ def pendulum_vboc_run(out_dir=None, device="cuda", seed=0, backend=None, it_max=
     X, stats = pendulum_data_generation(backend)
     mean, std = position_stats(X, 1)
     F = dir_features(X, mean, std, 1)
-    tr = DirTrainer(1, device=device, beta=0.8, stop_val=1e-4, seed=seed)
+    tr = make_trainer(1, device=device, beta=0.8, stop_val=1e-4, seed=seed)
     B = int(X.shape[0] * 100 / tr.k)
     # the reference counts it from 0 (`while val > 1e-4 and it < it_max`), the trainer from 1
     fit = tr.fit(F, it_max=(it_max or B * 100) + 1)
@@ -347,7 +347,7 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
     F = dir_features(X_train, mean, std, 4)
     F_test = dir_features(X_test, mean, std, 4)
     k = min(minibatch, F.shape[0])
-    tr = DirTrainer(4, device=device, hidden=hidden, minibatch=k, beta=0.95, stop_val=1e-3, seed=seed)
+    tr = make_trainer(4, device=device, hidden=hidden, minibatch=k, beta=0.95, stop_val=1e-3, seed=seed)
     B = int(F.shape[0] * 100 / k)
     fit = tr.fit(F, it_max=max(1, B * 20))
     rmse_train, rmse_test = tr.rmse(F), tr.rmse(F_test)
@@ -399,7 +399,7 @@ def cartesian_run(backend=None, num_test=1000, num_train=100000, out_dir=None, d
     F = dir_features(X_train, mean, std, 2)
     F_test = dir_features(X_test, mean, std, 2)
     k = min(minibatch, F.shape[0])
-    tr = DirTrainer(2, device=device, hidden=hidden, minibatch=k, beta=0.95, stop_val=1e-3, seed=seed)
+    tr = make_trainer(2, device=device, hidden=hidden, minibatch=k, beta=0.95, stop_val=1e-3, seed=seed)
     B = int(F.shape[0] * 100 / k)
     fit = tr.fit(F, it_max=max(1, B * 100))
     rmse_train, rmse_test = tr.rmse(F), tr.rmse(F_test)
