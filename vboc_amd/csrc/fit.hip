@@ -7,13 +7,17 @@
 // there as ~40 small kernels per step (plus a host sync on loss.item()) is here:
 //
 //   k_sample    one workgroup: the step's gate (val > stop && it < it_max), a uniform k-subset of each row range
-//               (Philox draws with rejection of repeats: random.sample's set method), the gathered minibatch
-//   k_fwd_bwd   16 minibatch rows per workgroup: H1 = relu(x W0' + b0), H2 = relu(H1 W1' + b1) and
+//               (Philox draws with rejection of repeats: random.sample's set method)
+//   k_fwd_bwd   16 minibatch rows per workgroup (gathered from the feature rows): H1 = relu(x W0' + b0),
+//               H2 = relu(H1 W1' + b1) and
 //               dH1 = (dH2 W1) * [H1 > 0] on v_mfma_f32_16x16x4_f32 (exact f32, as the f32 GEMMs of PyTorch),
 //               the output layer, the MSE gradient, per-workgroup partial gradients of every small parameter
 //   k_dw1       dW1 = dH2' H1 (split over minibatch rows), plus the EMA / counter update of the reference's loop
 //   k_adam      the partial sums reduced in a fixed order, torch.optim.Adam's update (single-tensor path),
-//               W1' rewritten for the next step's backward product
+//               W1 rewritten as the packed MFMA fragments of the next step's two products
+//
+// Every operand streamed from L2 / MALL (W1 twice, H1 and dH2 for dW1) is stored fragment-packed (pk()): a wave's
+// B (or A) fragment of one 16 x 16 block is 1 KB contiguous, so each load instruction moves whole 256-B lines.
 //
 // Every reduction has a fixed order, so a HIP-graph replay equals the eager launch sequence bit for bit; a step
 // whose gate is 0 changes nothing, so running up to `poll - 1` steps past the stop is exact.  Parameters are kept
@@ -47,12 +51,11 @@ struct Args {
   float* P;                   // parameters: [W0 (HP x NIN) | b0 | b1 | w2 (HP each) | b2 (4) | W1 (HP x HP)]
   float* M;                   // Adam exp_avg, same layout
   float* V;                   // Adam exp_avg_sq
-  float* W1T;                 // W1 transposed [HP][HP]
-  float* xb;                  // minibatch inputs [Bt][NIN]
-  float* yb;                  // minibatch targets [Bt]
+  float* Wf;                  // W1 packed as the forward product's B fragments: pk(j, k, HP / 16)
+  float* Wb;                  // W1 packed as the backward product's B fragments: element W1[j][c] at pk(c, j, HP / 16)
   int* idx;                   // minibatch row indices [Bt]
-  float* H1T;                 // [HP][Bt]
-  float* dH2T;                // [HP][Bt]
+  float* H1p;                 // H1 packed as dW1's B fragments: element H1[r][c] at pk(c, r, Bt / 16)
+  float* dH2p;                // dH2 packed as dW1's A fragments: element dH2[r][j] at pk(j, r, Bt / 16)
   float* part;                // per-workgroup partials [Bt / R2][REC]
   float* dW1p;                // split partials of dW1 [S][HP][HP]
   State* st;
@@ -72,6 +75,12 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Fragment-packed storage: the 16 x 16 block (RB, CB) of a matrix read as MFMA fragments "lane (lr, lq) takes
+// [16 RB + lr][16 CB + 4 lq + s], s = 0..3" is 1 KB, lane-major: one wave-instruction loads it whole.
+__host__ __device__ __forceinline__ size_t pk(int R, int C, int ncb) {
+  return ((size_t)((R >> 4) * ncb + (C >> 4)) * 64 + (R & 15) + 16 * ((C & 15) >> 2)) * 4 + (C & 3);
+}
+
 __device__ __forceinline__ void philox(unsigned (&c)[4], unsigned k0, unsigned k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -86,25 +95,6 @@ __device__ __forceinline__ void philox(unsigned (&c)[4], unsigned k0, unsigned k
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
   }
-}
-
-// uniform integer in [0, n) from draw `round` of sample slot `p`: Lemire's multiply-shift with rejection over the
-// four words of one Philox block (all four rejected has probability < (n / 2^32)^4; the last one is then kept)
-__device__ __forceinline__ unsigned draw_below(unsigned n, unsigned thr, unsigned long long step, unsigned p,
-                                               unsigned round, unsigned long long seed, unsigned range) {
-  unsigned c[4] = {(unsigned)step, (unsigned)(step >> 32), p, round};
-  philox(c, (unsigned)seed, (unsigned)(seed >> 32) ^ (0x2545F491u + range));
-  unsigned v = 0;
-  bool got = false;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const unsigned long long m = (unsigned long long)c[q] * n;
-    if (!got && ((unsigned)m >= thr || q == 3)) {
-      v = (unsigned)(m >> 32);
-      got = true;
-    }
-  }
-  return v;
 }
 
 __device__ __forceinline__ unsigned hslot(unsigned v) { return (v * 2654435761u) >> 19; }
@@ -163,14 +153,26 @@ __device__ __forceinline__ void sample_set(SampLds& L, unsigned n, int kk, unsig
     slot[u] = 0;
   }
   int any = 1;
+  const unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32) ^ (0x2545F491u + range);
   for (unsigned r = 0; r < ROUNDS && any; ++r) {
+    // one Philox block per thread and round: word u is slot tid + 1024 u's draw (Lemire: a word below thr is
+    // rejected and the slot simply stays pending)
+    bool drew[4] = {false, false, false, false};
+    if (pend[0] || pend[1] || pend[2] || pend[3]) {
+      unsigned c[4] = {(unsigned)step, (unsigned)(step >> 32), (unsigned)tid, r};
+      philox(c, k0, k1);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (pend[u]) {
-        const unsigned p = tid + 1024 * u;
-        vals[u] = draw_below(n, thr, step, p, r, seed, range);
-        slot[u] = tbl_insert(L.keys, vals[u]);
-        atomicMin(&L.own[slot[u]], (r << 12) | p);
+      for (int u = 0; u < 4; ++u) {
+        if (pend[u]) {
+          const unsigned long long m = (unsigned long long)c[u] * n;
+          if ((unsigned)m >= thr) {
+            const unsigned p = tid + 1024 * u;
+            vals[u] = (unsigned)(m >> 32);
+            slot[u] = tbl_insert(L.keys, vals[u]);
+            atomicMin(&L.own[slot[u]], (r << 12) | p);
+            drew[u] = true;
+          }
+        }
       }
     }
     __syncthreads();
@@ -179,7 +181,7 @@ __device__ __forceinline__ void sample_set(SampLds& L, unsigned n, int kk, unsig
     for (int u = 0; u < 4; ++u) {
       if (pend[u]) {
         const unsigned p = tid + 1024 * u;
-        if (L.own[slot[u]] == ((r << 12) | p)) pend[u] = false;
+        if (drew[u] && L.own[slot[u]] == ((r << 12) | p)) pend[u] = false;
         else mine = 1;
       }
     }
@@ -270,13 +272,47 @@ __global__ __launch_bounds__(1024) void k_sample(Args a) {
     sample_range(L, a, 0, (unsigned)n_old, a.Bt / 2, 0, step, 1u);
     sample_range(L, a, n_old, (unsigned)a.n_new, a.Bt / 2, a.Bt / 2, step, 2u);
   }
-  for (int p = threadIdx.x; p < a.Bt; p += 1024) {
-    const float* row = a.F + (size_t)a.idx[p] * a.ldF;
-#pragma unroll
-    for (int i = 0; i < NIN; ++i) a.xb[p * NIN + i] = row[i];
-    a.yb[p] = row[NIN];
-  }
   if (threadIdx.x == 0) st->draws = step + 1;
+}
+
+// acc[u] += A[16 rows][HP] (LDS, row stride LD) x B' for the column tile 16 (w + 4u) .. +15, B [HP][HP] given
+// fragment-packed (pk(j, k, HP / 16), row j = output column j).  MFMA step s of group t sums k = 16t + 4 lq + s.  Two register sets
+// of B fragments alternate (group t + 1's loads are in flight while group t's MFMAs issue); no copies between
+// them, so the compiler's waits stay one group behind the loads.
+template <int NT, int LD>
+__device__ __forceinline__ void mfma_group(const float* A, int t, int lr, int lq, const f4 (&bv)[NT],
+                                           f4 (&acc)[NT]) {
+  const f4 av = *(const f4*)&A[lr * LD + 16 * t + 4 * lq];
+#pragma unroll
+  for (int u = 0; u < NT; ++u) {
+    acc[u] = mfma(av.x, bv[u].x, acc[u]);
+    acc[u] = mfma(av.y, bv[u].y, acc[u]);
+    acc[u] = mfma(av.z, bv[u].z, acc[u]);
+    acc[u] = mfma(av.w, bv[u].w, acc[u]);
+  }
+}
+
+template <int HP, int NT, int LD>
+__device__ __forceinline__ void gemm_rows(const float* A, const float* B, int w, int lane, int lr, int lq,
+                                          f4 (&acc)[NT]) {
+  constexpr int TG = HP / 16;   // even for every instantiation (HP a multiple of 64)
+  const float* bp[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u) bp[u] = B + ((size_t)(w + 4 * u) * TG * 64 + lane) * 4;
+  f4 b0[NT], b1[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u) b0[u] = *(const f4*)bp[u];
+  static_assert(TG % 2 == 0, "column groups come in pairs");
+  for (int t = 0; t < TG; t += 2) {
+#pragma unroll
+    for (int u = 0; u < NT; ++u) b1[u] = *(const f4*)(bp[u] + 256 * (t + 1));
+    mfma_group<NT, LD>(A, t, lr, lq, b0, acc);
+    if (t + 2 < TG) {
+#pragma unroll
+      for (int u = 0; u < NT; ++u) b0[u] = *(const f4*)(bp[u] + 256 * (t + 2));
+    }
+    mfma_group<NT, LD>(A, t + 1, lr, lq, b1, acc);
+  }
 }
 
 template <int NIN, int HP>
@@ -291,8 +327,13 @@ __global__ __launch_bounds__(256) void k_fwd_bwd(Args a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lq = lane >> 4;
   const int row0 = blockIdx.x * R2;
   const float* P = a.P;
-  if (tid < R2 * NIN) xs[tid] = a.xb[row0 * NIN + tid];
-  if (tid < R2) ys[tid] = a.yb[row0 + tid];
+  // the workgroup's minibatch rows, gathered from the feature matrix
+  if (tid < R2 * (NIN + 1)) {
+    const int r = tid / (NIN + 1), i = tid % (NIN + 1);
+    const float v = a.F[(size_t)a.idx[row0 + r] * a.ldF + i];
+    if (i < NIN) xs[r * NIN + i] = v;
+    else ys[r] = v;
+  }
   __syncthreads();
 
   // H1 = relu(x W0' + b0), kept in LDS and written transposed for dW1
@@ -310,30 +351,17 @@ __global__ __launch_bounds__(256) void k_fwd_bwd(Args a) {
       h[r] = fmaxf(s + bc, 0.f);
       H1[r * LD + c] = h[r];
     }
-    f4* dst = (f4*)(a.H1T + (size_t)c * a.Bt + row0);
+    f4* dst = (f4*)(a.H1p + pk(c, row0, a.Bt / 16));
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = f4{h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]};
+    for (int q = 0; q < 4; ++q) dst[16 * q] = f4{h[4 * q], h[4 * q + 1], h[4 * q + 2], h[4 * q + 3]};
   }
   __syncthreads();
 
   // A2 = H1 W1' on MFMA: wave w owns column tiles w, w + 4, ...; MFMA step s of group t sums k = 16t + 4 lq + s
-  const float* W1 = P + Ly::W1;
   f4 acc[NT];
 #pragma unroll
   for (int u = 0; u < NT; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < HP / 16; ++t) {
-    const f4 av = *(const f4*)&H1[lr * LD + 16 * t + 4 * lq];
-    f4 bv[NT];
-#pragma unroll
-    for (int u = 0; u < NT; ++u) bv[u] = *(const f4*)(W1 + (size_t)(16 * (w + 4 * u) + lr) * HP + 16 * t + 4 * lq);
-#pragma unroll
-    for (int u = 0; u < NT; ++u) {
-      acc[u] = mfma(av.x, bv[u].x, acc[u]);
-      acc[u] = mfma(av.y, bv[u].y, acc[u]);
-      acc[u] = mfma(av.z, bv[u].z, acc[u]);
-      acc[u] = mfma(av.w, bv[u].w, acc[u]);
-    }
-  }
+  gemm_rows<HP, NT, LD>(H1, a.Wf, w, lane, lr, lq, acc);
   // acc[u][g] = A2[row 4 lq + g][col 16 (w + 4u) + lr]; H2 = relu(A2 + b1); output partial sums
   float op[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -384,7 +412,7 @@ __global__ __launch_bounds__(256) void k_fwd_bwd(Args a) {
       sw = fmaf(dr[g], h, sw);
       G2[(4 * lq + g) * LD + j] = gv[g];
     }
-    *(f4*)(a.dH2T + (size_t)j * a.Bt + row0 + 4 * lq) = f4{gv[0], gv[1], gv[2], gv[3]};
+    *(f4*)(a.dH2p + pk(j, row0 + 4 * lq, a.Bt / 16)) = f4{gv[0], gv[1], gv[2], gv[3]};
     sb += __shfl_xor(sb, 16);
     sb += __shfl_xor(sb, 32);
     sw += __shfl_xor(sw, 16);
@@ -408,23 +436,10 @@ __global__ __launch_bounds__(256) void k_fwd_bwd(Args a) {
   }
   __syncthreads();
 
-  // dH1 = dH2 W1 [H1 > 0] on MFMA (B operand W1[j][c] = W1T[c][j]); db0 and dW0 partials
-  const float* W1T = a.W1T;
+  // dH1 = dH2 W1 [H1 > 0] on MFMA (B operand W1[j][c], packed in Wb); db0 and dW0 partials
 #pragma unroll
   for (int u = 0; u < NT; ++u) acc[u] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < HP / 16; ++t) {
-    const f4 av = *(const f4*)&G2[lr * LD + 16 * t + 4 * lq];
-    f4 bv[NT];
-#pragma unroll
-    for (int u = 0; u < NT; ++u) bv[u] = *(const f4*)(W1T + (size_t)(16 * (w + 4 * u) + lr) * HP + 16 * t + 4 * lq);
-#pragma unroll
-    for (int u = 0; u < NT; ++u) {
-      acc[u] = mfma(av.x, bv[u].x, acc[u]);
-      acc[u] = mfma(av.y, bv[u].y, acc[u]);
-      acc[u] = mfma(av.z, bv[u].z, acc[u]);
-      acc[u] = mfma(av.w, bv[u].w, acc[u]);
-    }
-  }
+  gemm_rows<HP, NT, LD>(G2, a.Wb, w, lane, lr, lq, acc);
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
     const int c = 16 * (w + 4 * u) + lr;
@@ -471,13 +486,12 @@ __global__ __launch_bounds__(256) void k_dw1(Args a) {
   for (int x = 0; x < 2; ++x)
 #pragma unroll
     for (int y = 0; y < 2; ++y) acc[x][y] = f4{0.f, 0.f, 0.f, 0.f};
-  const float* A0 = a.dH2T + (size_t)(j0 + lr) * a.Bt + r0 + 4 * lq;
-  const float* A1 = A0 + (size_t)16 * a.Bt;
-  const float* B0 = a.H1T + (size_t)(c0 + lr) * a.Bt + r0 + 4 * lq;
-  const float* B1 = B0 + (size_t)16 * a.Bt;
-  for (int t = 0; t < KC / 16; ++t) {
-    const f4 av[2] = {*(const f4*)(A0 + 16 * t), *(const f4*)(A1 + 16 * t)};
-    const f4 bv[2] = {*(const f4*)(B0 + 16 * t), *(const f4*)(B1 + 16 * t)};
+  const int RG = a.Bt / 16;
+  const float* A0 = a.dH2p + ((size_t)((j0 >> 4) * RG + (r0 >> 4)) * 64 + lane) * 4;
+  const float* A1 = A0 + (size_t)RG * 256;
+  const float* B0 = a.H1p + ((size_t)((c0 >> 4) * RG + (r0 >> 4)) * 64 + lane) * 4;
+  const float* B1 = B0 + (size_t)RG * 256;
+  auto group = [&](const f4 (&av)[2], const f4 (&bv)[2]) {
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -487,6 +501,28 @@ __global__ __launch_bounds__(256) void k_dw1(Args a) {
         acc[x][y] = mfma(av[x].z, bv[y].z, acc[x][y]);
         acc[x][y] = mfma(av[x].w, bv[y].w, acc[x][y]);
       }
+  };
+  // ping-pong register sets, as gemm_rows
+  f4 a0[2] = {*(const f4*)A0, *(const f4*)A1}, b0[2] = {*(const f4*)B0, *(const f4*)B1};
+  f4 a1[2], b1[2];
+  const int T = KC / 16;
+  for (int t = 0; t < T; t += 2) {
+    const int o1 = 256 * (t + 1), o2 = 256 * (t + 2);
+    const bool odd = t + 1 < T;
+    if (odd) {
+      a1[0] = *(const f4*)(A0 + o1);
+      a1[1] = *(const f4*)(A1 + o1);
+      b1[0] = *(const f4*)(B0 + o1);
+      b1[1] = *(const f4*)(B1 + o1);
+    }
+    group(a0, b0);
+    if (t + 2 < T) {
+      a0[0] = *(const f4*)(A0 + o2);
+      a0[1] = *(const f4*)(A1 + o2);
+      b0[0] = *(const f4*)(B0 + o2);
+      b0[1] = *(const f4*)(B1 + o2);
+    }
+    if (odd) group(a1, b1);
   }
   float* out = a.dW1p + (size_t)s * HP * HP;
 #pragma unroll
@@ -552,10 +588,16 @@ __global__ __launch_bounds__(256) void k_adam(Args a) {
       tile[rj][rc] = p;
     }
     __syncthreads();
+    // the new W1 tile as the packed B fragments of both products: 4 blocks of 16 x 16 = 4 KB each, lane-major
+    constexpr int TG = HP / 16;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int e = tid + 256 * q, rc = e >> 5, rj = e & 31;
-      a.W1T[(size_t)(tc * 32 + rc) * HP + tj * 32 + rj] = tile[rj][rc];
+      const int e = tid + 256 * q, bi = e >> 8, L = (e >> 2) & 63, sx = e & 3;
+      const int b_r = bi >> 1, b_c = bi & 1, lr = L & 15, lq = L >> 4;
+      // forward: rows j (output columns), k along the fragment
+      a.Wf[(((size_t)(tj * 2 + b_r) * TG + tc * 2 + b_c) * 64 + L) * 4 + sx] = tile[16 * b_r + lr][16 * b_c + 4 * lq + sx];
+      // backward: rows c, k = j along the fragment
+      a.Wb[(((size_t)(tc * 2 + b_r) * TG + tj * 2 + b_c) * 64 + L) * 4 + sx] = tile[16 * b_c + 4 * lq + sx][16 * b_r + lr];
     }
     return;
   }
@@ -580,8 +622,8 @@ __global__ __launch_bounds__(256) void k_adam(Args a) {
 
 // torch layouts <-> padded buffers
 template <int NIN, int HP>
-__global__ void k_pack(float* P, float* W1T, float* W0, float* b0, float* W1, float* b1, float* W2, float* b2, int H,
-                       int unpack) {
+__global__ void k_pack(float* P, float* Wf, float* Wb, float* W0, float* b0, float* W1, float* b1, float* W2,
+                       float* b2, int H, int unpack) {
   using Ly = Lay<NIN, HP>;
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < (long long)HP * HP) {
@@ -591,7 +633,8 @@ __global__ void k_pack(float* P, float* W1T, float* W0, float* b0, float* W1, fl
     } else {
       const float v = (j < H && c < H) ? W1[j * H + c] : 0.f;
       P[Ly::W1 + i] = v;
-      W1T[(size_t)c * HP + j] = v;
+      Wf[pk(j, c, HP / 16)] = v;
+      Wb[pk(c, j, HP / 16)] = v;
     }
   }
   if (i < HP) {
@@ -622,8 +665,8 @@ __global__ void k_pack(float* P, float* W1T, float* W0, float* b0, float* W1, fl
 struct vboc_fit {
   int nin, hidden, hp, bt, S;
   int total, rec;
-  float *P = nullptr, *M = nullptr, *V = nullptr, *W1T = nullptr, *xb = nullptr, *yb = nullptr;
-  float *H1T = nullptr, *dH2T = nullptr, *part = nullptr, *dW1p = nullptr;
+  float *P = nullptr, *M = nullptr, *V = nullptr, *Wf = nullptr, *Wb = nullptr;
+  float *H1p = nullptr, *dH2p = nullptr, *part = nullptr, *dW1p = nullptr;
   int* idx = nullptr;
   State* st = nullptr;
   State* st_host = nullptr;           // pinned
@@ -676,9 +719,9 @@ static void pack(vboc_fit* h, float* W0, float* b0, float* W1, float* b1, float*
                  float* src) {
   const int nthr = h->hp * h->hp;
   dim3 g((nthr + 255) / 256), b(256);
-  if (h->nin == 6) hipLaunchKernelGGL((k_pack<6, 512>), g, b, 0, h->stream, src, h->W1T, W0, b0, W1, b1, W2, b2, h->hidden, unpack);
-  else if (h->nin == 4) hipLaunchKernelGGL((k_pack<4, 320>), g, b, 0, h->stream, src, h->W1T, W0, b0, W1, b1, W2, b2, h->hidden, unpack);
-  else hipLaunchKernelGGL((k_pack<2, 128>), g, b, 0, h->stream, src, h->W1T, W0, b0, W1, b1, W2, b2, h->hidden, unpack);
+  if (h->nin == 6) hipLaunchKernelGGL((k_pack<6, 512>), g, b, 0, h->stream, src, h->Wf, h->Wb, W0, b0, W1, b1, W2, b2, h->hidden, unpack);
+  else if (h->nin == 4) hipLaunchKernelGGL((k_pack<4, 320>), g, b, 0, h->stream, src, h->Wf, h->Wb, W0, b0, W1, b1, W2, b2, h->hidden, unpack);
+  else hipLaunchKernelGGL((k_pack<2, 128>), g, b, 0, h->stream, src, h->Wf, h->Wb, W0, b0, W1, b1, W2, b2, h->hidden, unpack);
 }
 
 extern "C" {
@@ -699,10 +742,10 @@ int vboc_fit_create(int nin, int hidden, int minibatch, unsigned long long seed,
   h->hidden = hidden;
   h->hp = hp;
   h->bt = minibatch;
-  // split of the dW1 rows: about 256 workgroups, each split a multiple of 16 rows
+  // split of the dW1 rows: about 256 workgroups, each split a multiple of 32 rows
   const int blocks = (hp / 64) * (hp / 64);
   int S = 1;
-  while (blocks * S * 2 <= 256 && minibatch / (S * 2) >= 16 && (minibatch / (S * 2)) % 16 == 0) S *= 2;
+  while (blocks * S * 2 <= 256 && (minibatch / (S * 2)) % 32 == 0) S *= 2;
   h->S = S;
   if (nin == 6) { h->total = total_of<6, 512>(); h->rec = rec_of<6, 512>(); }
   else if (nin == 4) { h->total = total_of<4, 320>(); h->rec = rec_of<4, 320>(); }
@@ -717,12 +760,11 @@ int vboc_fit_create(int nin, int hidden, int minibatch, unsigned long long seed,
   FALLOC(h->P, sizeof(float) * h->total);
   FALLOC(h->M, sizeof(float) * h->total);
   FALLOC(h->V, sizeof(float) * h->total);
-  FALLOC(h->W1T, sizeof(float) * hp * hp);
-  FALLOC(h->xb, sizeof(float) * minibatch * nin);
-  FALLOC(h->yb, sizeof(float) * minibatch);
+  FALLOC(h->Wf, sizeof(float) * hp * hp);
+  FALLOC(h->Wb, sizeof(float) * hp * hp);
   FALLOC(h->idx, sizeof(int) * minibatch);
-  FALLOC(h->H1T, sizeof(float) * (size_t)hp * minibatch);
-  FALLOC(h->dH2T, sizeof(float) * (size_t)hp * minibatch);
+  FALLOC(h->H1p, sizeof(float) * (size_t)hp * minibatch);
+  FALLOC(h->dH2p, sizeof(float) * (size_t)hp * minibatch);
   FALLOC(h->part, sizeof(float) * (size_t)(minibatch / R2) * h->rec);
   FALLOC(h->dW1p, sizeof(float) * (size_t)S * hp * hp);
   FALLOC(h->st, sizeof(State));
@@ -736,7 +778,8 @@ int vboc_fit_create(int nin, int hidden, int minibatch, unsigned long long seed,
   (void)hipMemsetAsync(h->P, 0, sizeof(float) * h->total, h->stream);
   (void)hipMemsetAsync(h->M, 0, sizeof(float) * h->total, h->stream);
   (void)hipMemsetAsync(h->V, 0, sizeof(float) * h->total, h->stream);
-  (void)hipMemsetAsync(h->W1T, 0, sizeof(float) * hp * hp, h->stream);
+  (void)hipMemsetAsync(h->Wf, 0, sizeof(float) * hp * hp, h->stream);
+  (void)hipMemsetAsync(h->Wb, 0, sizeof(float) * hp * hp, h->stream);
   State s{};
   s.seed = seed;
   *h->st_host = s;
@@ -750,7 +793,7 @@ int vboc_fit_destroy(vboc_fit_handle h) {
   if (!h) return 0;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->exec) (void)hipGraphExecDestroy(h->exec);
-  float* bufs[] = {h->P, h->M, h->V, h->W1T, h->xb, h->yb, h->H1T, h->dH2T, h->part, h->dW1p};
+  float* bufs[] = {h->P, h->M, h->V, h->Wf, h->Wb, h->H1p, h->dH2p, h->part, h->dW1p};
   for (float* b : bufs)
     if (b) (void)hipFree(b);
   if (h->idx) (void)hipFree(h->idx);
@@ -802,8 +845,8 @@ int vboc_fit_train(vboc_fit_handle h, const vboc_fit_run_t* r, void* stream) {
   const int poll = r->poll > 0 ? r->poll : 1;
   Args a;
   memset(&a, 0, sizeof a);
-  a.P = h->P; a.M = h->M; a.V = h->V; a.W1T = h->W1T; a.xb = h->xb; a.yb = h->yb; a.idx = h->idx;
-  a.H1T = h->H1T; a.dH2T = h->dH2T; a.part = h->part; a.dW1p = h->dW1p; a.st = h->st;
+  a.P = h->P; a.M = h->M; a.V = h->V; a.Wf = h->Wf; a.Wb = h->Wb; a.idx = h->idx;
+  a.H1p = h->H1p; a.dH2p = h->dH2p; a.part = h->part; a.dW1p = h->dW1p; a.st = h->st;
   a.F = r->F; a.n = r->n; a.n_new = r->n_new; a.ldF = r->ld; a.Bt = h->bt; a.S = h->S; a.lr = (float)r->lr;
   // loop state of the reference: it = 1, val = max |qdot| of the training rows (given by the caller in f64)
   FCHK(hipStreamSynchronize(h->stream));
@@ -884,8 +927,7 @@ int vboc_fit_sample(vboc_fit_handle h, long long n, long long n_new, int steps, 
   FCHK(hipMemcpyAsync(h->st, s, sizeof(State), hipMemcpyHostToDevice, h->stream));
   Args a;
   memset(&a, 0, sizeof a);
-  a.xb = h->xb; a.yb = h->yb; a.idx = h->idx; a.st = h->st;
-  a.F = h->xb;          // gather reads row 0 of the minibatch buffer for every index (ld 0): in bounds
+  a.idx = h->idx; a.st = h->st;
   a.n = n; a.n_new = n_new; a.ldF = 0; a.Bt = h->bt; a.S = h->S;
   for (int i = 0; i < steps; ++i) {
     if (h->nin == 6) hipLaunchKernelGGL(k_sample<6>, dim3(1), dim3(1024), 0, h->stream, a);
