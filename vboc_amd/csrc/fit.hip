@@ -6,9 +6,10 @@
 // rows + 2048 from the new ones), my_nn.py:20-34 (the model), the double / pendulum twins.  What PyTorch runs
 // there as ~40 small kernels per step (plus a host sync on loss.item()) is here:
 //
-//   k_sample    one workgroup: the step's gate (val > stop && it < it_max), a uniform k-subset of each row range
-//               (Philox draws with rejection of repeats: random.sample's set method)
-//   k_fwd_bwd   16 minibatch rows per workgroup (gathered from the feature rows): H1 = relu(x W0' + b0),
+//   k_sample    one workgroup: the NEXT step's minibatch, a uniform k-subset of each row range (Philox draws with
+//               rejection of repeats: random.sample's set method), on a second stream beside dW1 / Adam
+//   k_fwd_bwd   the step's gate (val > stop && it < it_max); 16 minibatch rows per workgroup (gathered from the
+//               feature rows): H1 = relu(x W0' + b0),
 //               H2 = relu(H1 W1' + b1) and
 //               dH1 = (dH2 W1) * [H1 > 0] on v_mfma_f32_16x16x4_f32 (exact f32, as the f32 GEMMs of PyTorch),
 //               the output layer, the MSE gradient, per-workgroup partial gradients of every small parameter
@@ -256,15 +257,14 @@ __device__ void sample_range(SampLds& L, const Args& a, long long lo, unsigned n
   __syncthreads();
 }
 
+// The minibatch of the next step, into a.idx (one of two buffers): draw number st->draws of the sampler's stream.
+// It reads nothing the training kernels write, so it runs beside the previous step's dW1 / Adam kernels.
 template <int NIN>
 __global__ __launch_bounds__(1024) void k_sample(Args a) {
   __shared__ SampLds L;
   State* st = a.st;
-  const int gate = (st->val > st->stop) && (st->it < st->it_lim);
   const unsigned long long step = st->draws;
   __syncthreads();
-  if (threadIdx.x == 0) st->gate = gate;
-  if (!gate) return;
   if (a.n_new == 0) {
     sample_range(L, a, 0, (unsigned)a.n, a.Bt, 0, step, 0u);
   } else {
@@ -323,7 +323,12 @@ __global__ __launch_bounds__(256) void k_fwd_bwd(Args a) {
   __shared__ __attribute__((aligned(16))) float H1[R2 * LD];
   __shared__ __attribute__((aligned(16))) float G2[R2 * LD];
   __shared__ float xs[R2 * NIN], ys[R2], dout[R2], sq[R2], red[4][R2];
-  if (!a.st->gate) return;
+  // the step's gate (the reference's `while val > stop and it < it_max`), from the state the previous step left;
+  // block 0 publishes it for this step's dW1 / Adam kernels and the host's poll
+  const State* sc = a.st;
+  const int gate = (sc->val > sc->stop) && (sc->it < sc->it_lim);
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.st->gate = gate;
+  if (!gate) return;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lq = lane >> 4;
   const int row0 = blockIdx.x * R2;
   const float* P = a.P;
@@ -667,11 +672,11 @@ struct vboc_fit {
   int total, rec;
   float *P = nullptr, *M = nullptr, *V = nullptr, *Wf = nullptr, *Wb = nullptr;
   float *H1p = nullptr, *dH2p = nullptr, *part = nullptr, *dW1p = nullptr;
-  int* idx = nullptr;
+  int* idx[2] = {nullptr, nullptr};
   State* st = nullptr;
   State* st_host = nullptr;           // pinned
-  hipStream_t stream = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr, t0 = nullptr, t1 = nullptr;
+  hipStream_t stream = nullptr, stream2 = nullptr;   // training kernels; the sampler beside them
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, t0 = nullptr, t1 = nullptr, ev_f = nullptr, ev_s = nullptr;
   hipGraphExec_t exec = nullptr;
   Args key{};
   int key_poll = 0;
@@ -690,20 +695,51 @@ static int ffail(int code, const std::string& m) {
     if (e_ != hipSuccess) return ffail(VBOC_FIT_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
 
-template <int NIN, int HP>
-static void launch_step(const vboc_fit* h, const Args& a, hipStream_t s) {
-  constexpr int NW1 = (HP / 32) * (HP / 32);
-  const int nsmall = (Lay<NIN, HP>::SMALL + 15) / 16;
-  hipLaunchKernelGGL(k_sample<NIN>, dim3(1), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL((k_fwd_bwd<NIN, HP>), dim3(h->bt / R2), dim3(256), 0, s, a);
-  hipLaunchKernelGGL((k_dw1<NIN, HP>), dim3((HP / 64) * (HP / 64) * h->S), dim3(256), 0, s, a);
-  hipLaunchKernelGGL((k_adam<NIN, HP>), dim3(NW1 + nsmall), dim3(256), 0, s, a);
+static void launch_sample(const vboc_fit* h, const Args& a, hipStream_t s) {
+  if (h->nin == 6) hipLaunchKernelGGL(k_sample<6>, dim3(1), dim3(1024), 0, s, a);
+  else if (h->nin == 4) hipLaunchKernelGGL(k_sample<4>, dim3(1), dim3(1024), 0, s, a);
+  else hipLaunchKernelGGL(k_sample<2>, dim3(1), dim3(1024), 0, s, a);
 }
 
-static void step(const vboc_fit* h, const Args& a, hipStream_t s) {
-  if (h->nin == 6 && h->hp == 512) launch_step<6, 512>(h, a, s);
-  else if (h->nin == 4 && h->hp == 320) launch_step<4, 320>(h, a, s);
-  else launch_step<2, 128>(h, a, s);
+template <int NIN, int HP>
+static void launch_train(const vboc_fit* h, const Args& a, hipStream_t s, bool fwd) {
+  constexpr int NW1 = (HP / 32) * (HP / 32);
+  const int nsmall = (Lay<NIN, HP>::SMALL + 15) / 16;
+  if (fwd) {
+    hipLaunchKernelGGL((k_fwd_bwd<NIN, HP>), dim3(h->bt / R2), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((k_dw1<NIN, HP>), dim3((HP / 64) * (HP / 64) * h->S), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_adam<NIN, HP>), dim3(NW1 + nsmall), dim3(256), 0, s, a);
+  }
+}
+
+static void train_part(const vboc_fit* h, const Args& a, hipStream_t s, bool fwd) {
+  if (h->nin == 6 && h->hp == 512) launch_train<6, 512>(h, a, s, fwd);
+  else if (h->nin == 4 && h->hp == 320) launch_train<4, 320>(h, a, s, fwd);
+  else launch_train<2, 128>(h, a, s, fwd);
+}
+
+// Step i of a chunk (i = 0 .. steps - 1; the chunk starts with its first minibatch already drawn into
+// idx[parity]; step i uses idx[(parity + i) % 2]): the forward / backward kernel on `s`, then the next minibatch on `s2` (it may overwrite
+// idx[(i + 1) % 2] once step i - 1's forward kernel, which read it, is done: it waits for this step's forward
+// kernel, which stream order puts after that one), dW1 and Adam on `s`; the chunk ends joined on `s`.
+static hipError_t chunk(const vboc_fit* h, const Args& base, int steps, int parity, hipStream_t s, hipStream_t s2,
+                        hipEvent_t ev_f, hipEvent_t ev_s) {
+  hipError_t e;
+  for (int i = 0; i < steps; ++i) {
+    Args a = base;
+    a.idx = h->idx[(parity + i) & 1];
+    Args an = base;
+    an.idx = h->idx[(parity + i + 1) & 1];
+    if (i > 0 && (e = hipStreamWaitEvent(s, ev_s, 0)) != hipSuccess) return e;
+    train_part(h, a, s, true);
+    if ((e = hipEventRecord(ev_f, s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(s2, ev_f, 0)) != hipSuccess) return e;
+    launch_sample(h, an, s2);
+    if ((e = hipEventRecord(ev_s, s2)) != hipSuccess) return e;
+    train_part(h, a, s, false);
+  }
+  return hipStreamWaitEvent(s, ev_s, 0);
 }
 
 static bool supported(int nin, int hp) {
@@ -762,7 +798,8 @@ int vboc_fit_create(int nin, int hidden, int minibatch, unsigned long long seed,
   FALLOC(h->V, sizeof(float) * h->total);
   FALLOC(h->Wf, sizeof(float) * hp * hp);
   FALLOC(h->Wb, sizeof(float) * hp * hp);
-  FALLOC(h->idx, sizeof(int) * minibatch);
+  FALLOC(h->idx[0], sizeof(int) * minibatch);
+  FALLOC(h->idx[1], sizeof(int) * minibatch);
   FALLOC(h->H1p, sizeof(float) * (size_t)hp * minibatch);
   FALLOC(h->dH2p, sizeof(float) * (size_t)hp * minibatch);
   FALLOC(h->part, sizeof(float) * (size_t)(minibatch / R2) * h->rec);
@@ -771,6 +808,9 @@ int vboc_fit_create(int nin, int hidden, int minibatch, unsigned long long seed,
 #undef FALLOC
   if ((e = hipHostMalloc((void**)&h->st_host, sizeof(State))) != hipSuccess) return fail_free(e, "hipHostMalloc");
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail_free(e, "stream");
+  if ((e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess) return fail_free(e, "stream");
+  if ((e = hipEventCreateWithFlags(&h->ev_f, hipEventDisableTiming)) != hipSuccess) return fail_free(e, "event");
+  if ((e = hipEventCreateWithFlags(&h->ev_s, hipEventDisableTiming)) != hipSuccess) return fail_free(e, "event");
   if ((e = hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming)) != hipSuccess) return fail_free(e, "event");
   if ((e = hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming)) != hipSuccess) return fail_free(e, "event");
   if ((e = hipEventCreate(&h->t0)) != hipSuccess) return fail_free(e, "event");
@@ -796,13 +836,18 @@ int vboc_fit_destroy(vboc_fit_handle h) {
   float* bufs[] = {h->P, h->M, h->V, h->Wf, h->Wb, h->H1p, h->dH2p, h->part, h->dW1p};
   for (float* b : bufs)
     if (b) (void)hipFree(b);
-  if (h->idx) (void)hipFree(h->idx);
+  for (int* b : h->idx)
+    if (b) (void)hipFree(b);
   if (h->st) (void)hipFree(h->st);
   if (h->st_host) (void)hipHostFree(h->st_host);
   if (h->ev_in) (void)hipEventDestroy(h->ev_in);
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
   if (h->t0) (void)hipEventDestroy(h->t0);
   if (h->t1) (void)hipEventDestroy(h->t1);
+  if (h->ev_f) (void)hipEventDestroy(h->ev_f);
+  if (h->ev_s) (void)hipEventDestroy(h->ev_s);
+  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+  if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -842,10 +887,11 @@ int vboc_fit_train(vboc_fit_handle h, const vboc_fit_run_t* r, void* stream) {
     return ffail(VBOC_FIT_EARG, "a refit needs at least minibatch/2 old and new rows");
   if (r->n >= (1ll << 31)) return ffail(VBOC_FIT_EARG, "more than 2^31 rows");
   if (r->it_max < 1) return ffail(VBOC_FIT_EARG, "it_max < 1");
-  const int poll = r->poll > 0 ? r->poll : 1;
+  // a graph replays an even number of steps, so every replay starts on idx[0]
+  const int poll = r->graphs ? (r->poll > 2 ? (r->poll + 1) / 2 * 2 : 2) : (r->poll > 0 ? r->poll : 1);
   Args a;
   memset(&a, 0, sizeof a);
-  a.P = h->P; a.M = h->M; a.V = h->V; a.Wf = h->Wf; a.Wb = h->Wb; a.idx = h->idx;
+  a.P = h->P; a.M = h->M; a.V = h->V; a.Wf = h->Wf; a.Wb = h->Wb; a.idx = nullptr;
   a.H1p = h->H1p; a.dH2p = h->dH2p; a.part = h->part; a.dW1p = h->dW1p; a.st = h->st;
   a.F = r->F; a.n = r->n; a.n_new = r->n_new; a.ldF = r->ld; a.Bt = h->bt; a.S = h->S; a.lr = (float)r->lr;
   // loop state of the reference: it = 1, val = max |qdot| of the training rows (given by the caller in f64)
@@ -862,6 +908,12 @@ int vboc_fit_train(vboc_fit_handle h, const vboc_fit_run_t* r, void* stream) {
   FCHK(hipEventRecord(h->ev_in, (hipStream_t)stream));
   FCHK(hipStreamWaitEvent(h->stream, h->ev_in, 0));
   FCHK(hipMemcpyAsync(h->st, s, sizeof(State), hipMemcpyHostToDevice, h->stream));
+  const unsigned long long d0 = s->draws;
+  // the first step's minibatch (draw d0); every later one is drawn beside the step before it
+  Args a0 = a;
+  a0.idx = h->idx[0];
+  launch_sample(h, a0, h->stream);
+  FCHK(hipGetLastError());
   const bool same = h->exec && h->key_poll == poll && memcmp(&h->key, &a, sizeof(Args)) == 0;
   if (r->graphs && !same) {
     if (h->exec) {
@@ -870,8 +922,12 @@ int vboc_fit_train(vboc_fit_handle h, const vboc_fit_run_t* r, void* stream) {
     }
     hipGraph_t g;
     FCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < poll; ++i) step(h, a, h->stream);
+    const hipError_t ec = chunk(h, a, poll, 0, h->stream, h->stream2, h->ev_f, h->ev_s);
     FCHK(hipStreamEndCapture(h->stream, &g));
+    if (ec != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      return ffail(VBOC_FIT_EHIP, std::string("graph capture: ") + hipGetErrorString(ec));
+    }
     hipError_t e = hipGraphInstantiate(&h->exec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (e != hipSuccess) return ffail(VBOC_FIT_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
@@ -882,8 +938,7 @@ int vboc_fit_train(vboc_fit_handle h, const vboc_fit_run_t* r, void* stream) {
   long long launched = 0;
   for (;;) {
     if (r->graphs) FCHK(hipGraphLaunch(h->exec, h->stream));
-    else
-      for (int i = 0; i < poll; ++i) step(h, a, h->stream);
+    else FCHK(chunk(h, a, poll, (int)(launched & 1), h->stream, h->stream2, h->ev_f, h->ev_s));
     FCHK(hipGetLastError());
     launched += poll;
     FCHK(hipMemcpyAsync(&s->gate, &h->st->gate, sizeof(int), hipMemcpyDeviceToHost, h->stream));
@@ -893,6 +948,11 @@ int vboc_fit_train(vboc_fit_handle h, const vboc_fit_run_t* r, void* stream) {
   }
   FCHK(hipEventRecord(h->t1, h->stream));
   FCHK(hipMemcpyAsync(s, h->st, sizeof(State), hipMemcpyDeviceToHost, h->stream));
+  FCHK(hipStreamSynchronize(h->stream));
+  // the sampler stream continues after the steps taken (the ones drawn past the stop are dropped), so the next
+  // fit draws what a step-by-step loop would
+  s->draws = d0 + (unsigned long long)(s->it - 1);
+  FCHK(hipMemcpyAsync(&h->st->draws, &s->draws, sizeof(s->draws), hipMemcpyHostToDevice, h->stream));
   FCHK(hipStreamSynchronize(h->stream));
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, h->t0, h->t1);
@@ -927,14 +987,12 @@ int vboc_fit_sample(vboc_fit_handle h, long long n, long long n_new, int steps, 
   FCHK(hipMemcpyAsync(h->st, s, sizeof(State), hipMemcpyHostToDevice, h->stream));
   Args a;
   memset(&a, 0, sizeof a);
-  a.idx = h->idx; a.st = h->st;
+  a.idx = h->idx[0]; a.st = h->st;
   a.n = n; a.n_new = n_new; a.ldF = 0; a.Bt = h->bt; a.S = h->S;
   for (int i = 0; i < steps; ++i) {
-    if (h->nin == 6) hipLaunchKernelGGL(k_sample<6>, dim3(1), dim3(1024), 0, h->stream, a);
-    else if (h->nin == 4) hipLaunchKernelGGL(k_sample<4>, dim3(1), dim3(1024), 0, h->stream, a);
-    else hipLaunchKernelGGL(k_sample<2>, dim3(1), dim3(1024), 0, h->stream, a);
+    launch_sample(h, a, h->stream);
     FCHK(hipGetLastError());
-    FCHK(hipMemcpyAsync(idx_out + (size_t)i * h->bt, h->idx, sizeof(int) * h->bt, hipMemcpyDeviceToDevice,
+    FCHK(hipMemcpyAsync(idx_out + (size_t)i * h->bt, h->idx[0], sizeof(int) * h->bt, hipMemcpyDeviceToDevice,
                         h->stream));
   }
   FCHK(hipMemcpyAsync(s, h->st, sizeof(State), hipMemcpyDeviceToHost, h->stream));
