@@ -212,6 +212,14 @@ int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* batch, int* done_
                                void* stream);
 int vboc_data_generation_wait(vboc_handle h, vboc_dg_batch_t* batch, void* stream);
 
+/* The held-out set's testing(v) on the device (replaces Pool(...).map(testing, range(P)) over
+ * triplependulum_testdata.py:9-125 / doublependulum_testdata.py:9-121, the a10 driver): one wave per problem runs the
+ * draws (Philox stream 1, restarts stream 3), the horizon extension with the '{:.3f}' / '{:.4f}' rounded stop rule
+ * and the perturbed restarts (at most max_restarts; the reference retries forever).  b: as vboc_data_generation,
+ * with rows_cap >= B; row b of rows is problem b's x0[:2nq] (row_cnt[b] 1), or row_cnt[b] = -1 for None; ic,
+ * ic_slot unused.  Synchronous on `stream`. */
+int vboc_testing(vboc_handle h, vboc_dg_batch_t* b, int max_restarts, void* stream);
+
 /* The HJR one-step OCP, OCP<sys>.compute_problem(x0) of HJR/<sys>_hjr_class.py (triplependulum_hjr_class.py:
  * 117-134 with the model and options of :7-115), for every x0 of a batch, one problem per GPU lane (hjr.h):
  * x0 fixed, N = 1, h = 1e-2, u0 in [-u_max, u_max], terminal cost = logit 0 of NeuralNetCLS(2nq, hidden, 2)

@@ -203,3 +203,69 @@ def test_streamed_rounds_equal_one_synchronous_launch(nq):
             assert (a is None) == (b is None)
             if a is not None:
                 np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+
+
+# ------------------------------------------------------------------------------------------------
+# the held-out set's `testing` on the device (vboc_testing, dg.h k_ts)
+# ------------------------------------------------------------------------------------------------
+def _same_rows(a_res, b_res, tol):
+    same = 0
+    for a, b in zip(a_res, b_res):
+        if a is None or b is None:
+            same += (a is None) == (b is None)
+        else:
+            same += bool(np.abs(np.asarray(a, float) - np.asarray(b, float)).max() <= tol)
+    return same
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq", [3, 2])
+def test_device_testing_matches_reference_fixture(nq):
+    """tests/golden/testing_{nq}.json: the reference's own `testing` (triplependulum_testdata.py:9-125,
+    doublependulum_testdata.py:9-121) on the CPU oracle with the failure injection that drives its restarts;
+    the device state machine with the same injection (solver option dg_fail_mod) at the host driver's GPU bar."""
+    from vboc_amd import lib
+    from vboc_amd.drivers import testing_device
+    g = json.load(open(os.path.join(HERE, "golden", f"testing_{nq}.json")))
+    s = lib.Solver(nq, g["N_start"] + 40)
+    s.set_option("dg_fail_mod", g["fail_mod"])
+    res, st = testing_device(nq, np.array(g["ids"]), s, N_start=g["N_start"], seed=g["seed"])
+    ref = [None if r is None else np.asarray(r, float) for r in g["results"]]
+    same = _same_rows(res, ref, 1e-5)
+    print(f"nq {nq}: {same}/{len(ref)} as the reference function, {st['solves']} solves")
+    assert same >= 0.95 * len(ref), (same, len(ref))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nq", [3, 2])
+def test_device_testing_matches_host_driver_on_gpu(nq):
+    """The device state machine against the host driver on the same wave solver (the same solves in the same
+    order), with and without the failure injection: the same solve count and the same rows."""
+    from vboc_amd import lib
+    from vboc_amd.drivers import testing_batch, testing_device
+    ids = np.arange(2000, 2000 + 96)
+    for fail_mod in (0, 3):
+        host, hst = testing_batch(nq, ids, _FailingGpu(nq, fail_mod), N_start=100)
+        s = lib.Solver(nq, 140)
+        s.set_option("dg_fail_mod", fail_mod)
+        dev, dst = testing_device(nq, ids, s, N_start=100)
+        same = _same_rows(dev, host, 0.0 if nq == 3 else 1e-9)
+        print(f"nq {nq} fail_mod {fail_mod}: {same}/{len(ids)} identical, solves {dst['solves']} vs {hst['solves']}")
+        assert same >= (len(ids) if nq == 3 else 0.95 * len(ids)), (same, len(ids))
+        if nq == 3:
+            assert dst["solves"] == hst["solves"], (dst["solves"], hst["solves"])
+
+
+@pytest.mark.gpu
+def test_device_testing_set_at_scale():
+    """configs[2]'s held-out set in one launch: 10 000 triple problems, every x0 inside the state box and on the
+    stage-0 constraint's line (positions free of the velocity box), no problem hits the restart cap."""
+    from vboc_amd import lib
+    from vboc_amd.drivers import testing_device
+    from vboc_amd.systems import system
+    sysd = system(3)
+    res, st = testing_device(3, np.arange(10**7, 10**7 + 10000), lib.Solver(3, 140), N_start=100)
+    X = np.array([r for r in res if r is not None])
+    assert X.shape[0] >= 0.99 * 10000
+    assert (X[:, :3] >= sysd.q_min - 1e-9).all() and (X[:, :3] <= sysd.q_max + 1e-9).all()
+    assert (np.abs(X[:, 3:]) <= sysd.v_max + 1e-6).all()

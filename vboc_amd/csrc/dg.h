@@ -31,6 +31,8 @@ struct DgJobs {
   int count;
   int N_start, nmax;
   int fail_mod;                // test-only failure injection (solver option dg_fail_mod), 0 = off
+  int max_restarts;            // testing (k_ts): restarts before a problem gives None (the reference: unbounded)
+  double fmt_scale;            // testing (k_ts): 10^d of the stop rule's '{:.df}'.format(cost) (1e3 / 1e4)
   unsigned long long seed;
   // system constants (vboc_amd/systems.py; VBOC/triplependulum_vboc.py:381-393)
   double q_min, q_max, v_max, u_max, dt, tol, eps, g, l1, l2, m1, m2;
@@ -959,6 +961,300 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
       }
     }
     if (mode == 1) dg_finish<NQ>(J, inp, wg, t, idx);
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// The held-out set's `testing(v)` ON THE DEVICE (triplependulum_testdata.py:9-125, doublependulum_testdata.py:9-121;
+// row a10): the same persistent job loop and wave solver as k_dg, with the testing state machine - a random cost
+// direction and initial position, then extend the horizon while the cost still drops (by the stop rule's rounded
+// threshold), restarting from a perturbed start on a failed solve.  A restatement of
+// vboc_amd/drivers.py::testing_problem (pinned against the reference's own function, tests/test_drivers.py) with
+// the same arithmetic: stream 1 for the first draws, stream 3 (TEST_STREAM) for the restarts, Python scalar
+// expressions without contraction.  One row x0[:2nq] per problem (row_cnt 1), or None (row_cnt -1) once
+// max_restarts restarts have failed.
+// ------------------------------------------------------------------------------------------------
+template <int NQ>
+struct TsState {
+  int N, restarts, rng_pos, solves, fail;
+  double cost, sqp, nsqp, nqp, t0, st1, it1;
+  double rans[NQ], qs[NQ];
+};
+
+// float('{:.df}'.format(v)) with scale = 10^d: v scaled exactly (a double-double product), rounded to the
+// nearest integer with ties to even on the exact value (Python's correctly rounded formatting), divided back
+// (the correctly rounded quotient is the double float() parses from the decimal string)
+__device__ __forceinline__ double fmt_round(double v, double scale) {
+#pragma clang fp contract(off)
+  const double m = fabs(v);
+  const double hi = m * scale;
+  const double lo = fma(m, scale, -hi);    // m scale = hi + lo exactly
+  const double k = floor(hi);
+  const double a = hi - k;                 // exact (k <= hi < k + 1), a multiple of ulp(hi) > 2 |lo|
+  double n;
+  if (a > 0.5 || (a == 0.5 && lo > 0.0)) n = k + 1.0;
+  else if (a < 0.5 || (a == 0.5 && lo < 0.0)) n = k;
+  else n = fmod(k, 2.0) == 0.0 ? k : k + 1.0;   // an exact tie: to even
+  const double r = n / scale;
+  return v < 0.0 ? -r : r;
+}
+
+template <int NQ>
+struct Ts {
+  static constexpr int NX = 2 * NQ, NXR = NX + 1, NU = NQ, NP = NQ + 1;
+  static constexpr bool GRAV = NQ == 2;   // double pendulum: gravity-compensation guesses
+  const DgJobs& J;
+  const Inputs& in;
+  const int wg, t;
+  TsState<NQ>* s;
+  long long pid;
+  int job;
+
+  __device__ Ts(const DgJobs& J_, const Inputs& in_, int wg_, int t_) : J(J_), in(in_), wg(wg_), t(t_), pid(0), job(0) {
+    s = (TsState<NQ>*)(J.st + (long long)wg * J.st_doubles);
+  }
+  __device__ __forceinline__ long long row(int r) const { return (long long)wg * (J.nmax + 1) + r; }
+  __device__ __forceinline__ double* xg(int r) const { return (double*)in.xg + row(r) * NXR; }
+  __device__ __forceinline__ double* ug(int r) const { return (double*)in.ug + ((long long)wg * J.nmax + r) * NU; }
+  __device__ __forceinline__ const double* xo(int r) const { return in.xo + row(r) * NXR; }
+  __device__ __forceinline__ const double* uo(int r) const { return in.uo + ((long long)wg * J.nmax + r) * NU; }
+  __device__ __forceinline__ double* pp() const { return (double*)in.p + (long long)wg * NP; }
+  __device__ __forceinline__ double* qlb0() const { return (double*)in.lbx0 + (long long)wg * NXR; }
+  __device__ __forceinline__ double* qub0() const { return (double*)in.ubx0 + (long long)wg * NXR; }
+
+  __device__ __forceinline__ void grav_u(const double* x, double* u) const {
+#pragma clang fp contract(off)
+    if constexpr (GRAV) {
+      u[0] = J.g * J.l1 * (J.m1 + J.m2) * sin(x[0]);
+      u[1] = J.g * J.l2 * J.m2 * sin(x[1]);
+    } else {
+      UNR for (int a = 0; a < NU; ++a) u[a] = 0.0;
+    }
+  }
+  __device__ __forceinline__ double rng_random() {   // ProblemRNG(pid, stream=TEST_STREAM = 3).random()
+    const int i = s->rng_pos;
+    s->rng_pos = i + 1;
+    return philox_uniform(pid, i, J.seed, 3u);
+  }
+  __device__ __forceinline__ double rng_pm1() { return Dg<NQ>::choice_idx(rng_random(), 2) == 0 ? -1.0 : 1.0; }
+
+  __device__ __forceinline__ void request(int N) {
+    if (N > J.nmax) {
+      if (t == 0) atomicOr(J.err + 1, 1u);
+      N = J.nmax;
+    }
+    ((int*)in.N)[wg] = N;
+    s->solves += 1;
+  }
+  __device__ __forceinline__ void set_bounds() {
+    const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max;
+    double* lbx = (double*)in.lbx + (long long)wg * NXR; double* ubx = (double*)in.ubx + (long long)wg * NXR;
+    double* lbxe = (double*)in.lbxe + (long long)wg * NXR; double* ubxe = (double*)in.ubxe + (long long)wg * NXR;
+    double* lbu = (double*)in.lbu + (long long)wg * NU; double* ubu = (double*)in.ubu + (long long)wg * NU;
+    UNR for (int j = 0; j < NQ; ++j) {
+      lbx[j] = q_min; ubx[j] = q_max; lbx[NQ + j] = v_min; ubx[NQ + j] = v_max;
+      lbxe[j] = q_min; ubxe[j] = q_max; lbxe[NQ + j] = 0.0; ubxe[NQ + j] = 0.0;
+      lbu[j] = -J.u_max; ubu[j] = J.u_max;
+    }
+    lbx[NX] = J.dt; ubx[NX] = J.dt; lbxe[NX] = J.dt; ubxe[NX] = J.dt;
+  }
+  // p = direction(rans) (:31-34); start(qs): the stage-0 box and the constant guess (:36-49)
+  __device__ __forceinline__ void setup() {
+#pragma clang fp contract(off)
+    double r[NQ];
+    UNR for (int j = 0; j < NQ; ++j) r[j] = s->rans[j];
+    const double nw = np_norm<NQ>(r);
+    double* P = pp();
+    UNR for (int j = 0; j < NQ; ++j) P[j] = r[j] / nw;
+    P[NQ] = 0.0;
+    double q[NQ];
+    UNR for (int j = 0; j < NQ; ++j) q[j] = s->qs[j];
+    double *lb0 = qlb0(), *ub0 = qub0();
+    UNR for (int j = 0; j < NQ; ++j) {
+      lb0[j] = q[j]; ub0[j] = q[j];
+      lb0[NQ + j] = -J.v_max; ub0[NQ + j] = J.v_max;
+    }
+    lb0[NX] = J.dt; ub0[NX] = J.dt;
+    double x[NXR], u[NU];
+    UNR for (int j = 0; j < NQ; ++j) { x[j] = q[j]; x[NQ + j] = 0.0; }
+    x[NX] = J.dt;
+    grav_u(x, u);
+    const int N = J.N_start;
+    for (int rr = t; rr <= N; rr += 64) {
+      UNR for (int c = 0; c < NXR; ++c) xg(rr)[c] = x[c];
+      if (rr < N) UNR for (int a = 0; a < NU; ++a) ug(rr)[a] = u[a];
+    }
+    s->N = N;
+    s->cost = 1e6;
+    request(N);
+  }
+
+  __device__ __forceinline__ bool start(int job_) {
+#pragma clang fp contract(off)
+    job = job_;
+    pid = J.ids[job];
+    s->t0 = (double)__builtin_amdgcn_s_memrealtime();
+    s->restarts = 0; s->rng_pos = 0; s->solves = 0; s->fail = 0;
+    s->sqp = 0.0; s->nsqp = 0.0; s->nqp = 0.0; s->st1 = 0.0; s->it1 = 0.0;
+    int di = 0;
+    auto draw = [&]() { return philox_uniform(pid, di++, J.seed, 1u); };
+    UNR for (int j = 0; j < NQ; ++j) {
+      const double c = Dg<NQ>::choice_idx(draw(), 2) == 0 ? -1.0 : 1.0;
+      s->rans[j] = c * draw();
+    }
+    UNR for (int j = 0; j < NQ; ++j) s->qs[j] = J.q_min + draw() * (J.q_max - J.q_min);
+    set_bounds();
+    setup();
+    return true;
+  }
+
+  // returns 1 when another solve is requested, 0 when the problem is done
+  __device__ __forceinline__ int feed(int job_) {
+#pragma clang fp contract(off)
+    job = job_;
+    pid = J.ids[job];
+    const int N = in.N[wg];
+    const int it = in.sqp_iter[wg], qit = in.qp_iter[wg];
+    if (s->solves == 1) {
+      s->st1 = (double)in.status[wg];
+      s->it1 = (double)it;
+    }
+    s->sqp += (double)it;
+    s->nsqp += (double)N * (double)it;
+    s->nqp += (double)N * (double)qit;
+    int status = in.status[wg];
+    if (J.fail_mod > 0) {   // tests: status 4 when int(|q_0| 1e6) % fail_mod == 0 (tests/oracle_backend.py)
+      const long long q = (long long)(fabs(qlb0()[0]) * 1e6);
+      if (q % J.fail_mod == 0) status = 4;
+    }
+    if (status == 0) {
+      const double cost_new = in.cost[wg];
+      // `cost_new > float('{:.3f}'.format(cost)) - 1e-3` (triple :65-67; the double: 4 decimals and 1e-4, :80-82)
+      if (cost_new > fmt_round(s->cost, J.fmt_scale) - (GRAV ? 1e-4 : 1e-3)) return 0;
+      if (N + 1 > J.nmax) {   // the extension ran past the handle's horizon capacity: reported to the host
+        if (t == 0) atomicOr(J.err + 1, 1u);
+        s->fail = 1;
+        return 0;
+      }
+      s->cost = cost_new;
+      // the solution becomes the guess of horizon N + 1: rows 0..N, u rows < N, u[N] the gravity guess at x[N]
+      for (int r = t; r <= N + 1; r += 64) {
+        const int rr = r <= N ? r : N;
+        UNR for (int c = 0; c < NXR; ++c) xg(r)[c] = xo(rr)[c];
+        if (r < N) {
+          UNR for (int a = 0; a < NU; ++a) ug(r)[a] = uo(r)[a];
+        } else if (r == N) {
+          double u[NU];
+          grav_u(xo(N), u);
+          UNR for (int a = 0; a < NU; ++a) ug(r)[a] = u[a];
+        }
+      }
+      s->N = N + 1;
+      request(N + 1);
+      return 1;
+    }
+    s->restarts += 1;
+    if (s->restarts > J.max_restarts) {
+      s->fail = 1;
+      return 0;
+    }
+    // a perturbed restart (:41-58): rans, then the initial positions, each by <= 0.01 (stream 3, random()
+    // before choice() in `rans[j] + random.random() * random.choice([-1, 1]) * 0.01`)
+    UNR for (int j = 0; j < NQ; ++j) {
+      const double a = rng_random();
+      const double b = rng_pm1();
+      s->rans[j] = s->rans[j] + a * b * 0.01;
+    }
+    UNR for (int j = 0; j < NQ; ++j) {
+      const double a = rng_random();
+      const double b = rng_pm1();
+      s->qs[j] = s->qs[j] + a * b * 0.01;
+    }
+    setup();
+    return 1;
+  }
+
+  __device__ __forceinline__ void finish(int job_) {
+    job = job_;
+    __syncthreads();
+    long long off = job;   // one row per problem, in problem order
+    if (t == 0) {
+      J.row_off[job] = off;
+      J.row_cnt[job] = s->fail ? -1 : 1;
+      double* st = J.stats + (long long)job * DG_NSTAT;
+      st[DG_SOLVES] = (double)s->solves;
+      st[DG_RK4] = 0.0;
+      st[DG_SQP] = s->sqp;
+      st[DG_NSQP] = s->nsqp;
+      st[DG_NQP] = s->nqp;
+      st[DG_T0] = s->t0;
+      st[DG_T1] = (double)__builtin_amdgcn_s_memrealtime();
+      st[DG_ST1] = s->st1;
+      st[DG_IT1] = s->it1;
+    }
+    if (!s->fail && t < NX) J.rows[off * NX + t] = xo(0)[t];
+    __syncthreads();
+    if (t == 0) {
+      if (J.done_flag) __hip_atomic_store(&J.done_flag[job], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      atomicAdd(J.done, 1u);
+    }
+  }
+};
+
+template <int NQ>
+__device__ __forceinline__ bool ts_start(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Ts<NQ> T(*J, *in, wg, t);
+  return T.start(job);
+}
+template <int NQ>
+__device__ __forceinline__ int ts_feed(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Ts<NQ> T(*J, *in, wg, t);
+  return T.feed(job);
+}
+template <int NQ>
+__device__ __forceinline__ void ts_finish(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Ts<NQ> T(*J, *in, wg, t);
+  T.finish(job);
+}
+
+// one workgroup = one wave = one held-out problem at a time (k_dg's loop without the speculation)
+template <int NQ, bool FM>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WavesPerEu<NQ>::v, WavesPerEu<NQ>::v)))
+void k_ts(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJobs jb) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int t = (int)threadIdx.x;
+  const int wg = (int)blockIdx.x;
+  Coop<NQ, FM> C(smem, gptr(jb.regions) + (long long)wg * jb.region_doubles, w, o, t);
+  const int count = J->count;
+  for (;;) {
+    int got = -1;
+    if (t == 0 && __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)count) {
+      const unsigned i = atomicAdd(jb.next, 1u);
+      if (i < (unsigned)count) got = (int)i;
+    }
+    got = dg_bcast(got);
+    if (got < 0) break;
+    int code = ts_start<NQ>(J, inp, wg, t, got) ? 1 : 0;
+    while (code) {
+      __syncthreads();
+      int it = 0, qit = 0;
+      Lane<NQ> chk(w, o, 0u);
+      if (!chk.supported(in, wg)) {
+        if (t == 0) {
+          in.status[wg] = 5;
+          in.sqp_iter[wg] = 0;
+          in.qp_iter[wg] = 0;
+        }
+      } else {
+        C.from_inputs(in, wg);
+        const int status = C.run(it, qit);
+        C.store(in, wg, status, it, qit);
+      }
+      __syncthreads();
+      code = ts_feed<NQ>(J, inp, wg, t, got);
+    }
+    ts_finish<NQ>(J, inp, wg, t, got);
     __syncthreads();
   }
 }

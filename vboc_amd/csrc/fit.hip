@@ -6,10 +6,10 @@
 // rows + 2048 from the new ones), my_nn.py:20-34 (the model), the double / pendulum twins.  What PyTorch runs
 // there as ~40 small kernels per step (plus a host sync on loss.item()) is here:
 //
-//   k_sample    one workgroup: the NEXT step's minibatch, a uniform k-subset of each row range (Philox draws with
-//               rejection of repeats: random.sample's set method), on a second stream beside dW1 / Adam
-//   k_fwd_bwd   the step's gate (val > stop && it < it_max); 16 minibatch rows per workgroup (gathered from the
-//               feature rows): H1 = relu(x W0' + b0),
+//   k_fwd_bwd   the step's gate (val > stop && it < it_max); one extra workgroup draws the NEXT step's
+//               minibatch, a uniform k-subset of each row range (Philox draws with rejection of repeats:
+//               random.sample's set method; k_sample draws a fit's first one); 16 minibatch rows per other
+//               workgroup (gathered from the feature rows): H1 = relu(x W0' + b0),
 //               H2 = relu(H1 W1' + b1) and
 //               dH1 = (dH2 W1) * [H1 > 0] on v_mfma_f32_16x16x4_f32 (exact f32, as the f32 GEMMs of PyTorch),
 //               the output layer, the MSE gradient, per-workgroup partial gradients of every small parameter
@@ -54,7 +54,8 @@ struct Args {
   float* V;                   // Adam exp_avg_sq
   float* Wf;                  // W1 packed as the forward product's B fragments: pk(j, k, HP / 16)
   float* Wb;                  // W1 packed as the backward product's B fragments: element W1[j][c] at pk(c, j, HP / 16)
-  int* idx;                   // minibatch row indices [Bt]
+  int* idx;                   // this step's minibatch row indices [Bt]
+  int* idx_next;              // the next step's, drawn by the forward kernel's extra workgroup
   float* H1p;                 // H1 packed as dW1's B fragments: element H1[r][c] at pk(c, r, Bt / 16)
   float* dH2p;                // dH2 packed as dW1's A fragments: element dH2[r][j] at pk(j, r, Bt / 16)
   float* part;                // per-workgroup partials [Bt / R2][REC]
@@ -121,158 +122,171 @@ __device__ __forceinline__ bool tbl_has(const unsigned* keys, unsigned v) {
   }
 }
 
+constexpr int SNT = 256;            // sampler threads (one workgroup of the forward kernel's shape)
+constexpr int SL = MAXK / SNT;      // sample slots per thread
+
+// 64 KB: the hash table, then the owners (reused for the sequential completion's values and, in the complement
+// path, the marks and the compaction counts once the owners are no longer needed)
 struct SampLds {
   unsigned keys[TBL];
-  unsigned own[TBL];
-  unsigned pendv[MAXK];
-  unsigned char mark[2 * MAXK];
-  int cnt[1024];
+  union {
+    unsigned own[TBL];
+    unsigned pendv[MAXK];
+    struct {
+      unsigned char mark[2 * MAXK];
+      int cnt[SNT];
+    } c;
+  } u;
   int npend;
 };
 
-// kk <= n / 2 distinct values of [0, n); slot p < kk (thread p % 1024, register p / 1024) gets vals[p / 1024].
+// kk <= n / 2 distinct values of [0, n); slot p < kk (thread p % SNT, register p / SNT) gets vals[p / SNT].
 // Round r: every pending slot draws, inserts, and claims its value with key (r << 12 | p); the smallest key
 // (earliest round, then lowest slot) owns the value and the other claimants draw again - the set of
 // random.sample's "draw, redraw while already selected" loop.  With at most half of [0, n) taken a slot is
 // pending after ROUNDS rounds with probability < 2^-128; such slots then take the smallest free values.
 __device__ __forceinline__ void sample_set(SampLds& L, unsigned n, int kk, unsigned long long step,
-                                           unsigned long long seed, unsigned range, unsigned (&vals)[4]) {
+                                           unsigned long long seed, unsigned range, unsigned (&vals)[SL]) {
   const int tid = threadIdx.x;
-  for (int i = tid; i < TBL; i += 1024) {
+  for (int i = tid; i < TBL; i += SNT) {
     L.keys[i] = 0u;
-    L.own[i] = 0xFFFFFFFFu;
+    L.u.own[i] = 0xFFFFFFFFu;
   }
   if (tid == 0) L.npend = 0;
   __syncthreads();
   const unsigned thr = (0u - n) % n;
-  bool pend[4];
-  int slot[4];
+  unsigned pend = 0u;       // bit u: slot tid + SNT u still needs a value
+  int slot[SL];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    pend[u] = tid + 1024 * u < kk;
+  for (int u = 0; u < SL; ++u) {
+    if (tid + SNT * u < kk) pend |= 1u << u;
     vals[u] = 0u;
     slot[u] = 0;
   }
   int any = 1;
   const unsigned k0 = (unsigned)seed, k1 = (unsigned)(seed >> 32) ^ (0x2545F491u + range);
   for (unsigned r = 0; r < ROUNDS && any; ++r) {
-    // one Philox block per thread and round: word u is slot tid + 1024 u's draw (Lemire: a word below thr is
-    // rejected and the slot simply stays pending)
-    bool drew[4] = {false, false, false, false};
-    if (pend[0] || pend[1] || pend[2] || pend[3]) {
-      unsigned c[4] = {(unsigned)step, (unsigned)(step >> 32), (unsigned)tid, r};
-      philox(c, k0, k1);
+    // one Philox block per four slots and round (Lemire: a word below thr is rejected and the slot simply
+    // stays pending)
+    unsigned drew = 0u;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (pend[u]) {
-          const unsigned long long m = (unsigned long long)c[u] * n;
-          if ((unsigned)m >= thr) {
-            const unsigned p = tid + 1024 * u;
-            vals[u] = (unsigned)(m >> 32);
-            slot[u] = tbl_insert(L.keys, vals[u]);
-            atomicMin(&L.own[slot[u]], (r << 12) | p);
-            drew[u] = true;
+    for (int q = 0; q < SL / 4; ++q) {
+      if ((pend >> (4 * q)) & 15u) {
+        unsigned c[4] = {(unsigned)step, (unsigned)(step >> 32), (unsigned)(tid + SNT * q), r};
+        philox(c, k0, k1);
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const int u = 4 * q + x;
+          if ((pend >> u) & 1u) {
+            const unsigned long long m = (unsigned long long)c[x] * n;
+            if ((unsigned)m >= thr) {
+              vals[u] = (unsigned)(m >> 32);
+              slot[u] = tbl_insert(L.keys, vals[u]);
+              atomicMin(&L.u.own[slot[u]], (r << 12) | (unsigned)(tid + SNT * u));
+              drew |= 1u << u;
+            }
           }
         }
       }
     }
     __syncthreads();
-    int mine = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (pend[u]) {
-        const unsigned p = tid + 1024 * u;
-        if (drew[u] && L.own[slot[u]] == ((r << 12) | p)) pend[u] = false;
-        else mine = 1;
-      }
-    }
-    any = __syncthreads_or(mine);
+    for (int u = 0; u < SL; ++u)
+      if (((drew >> u) & 1u) && L.u.own[slot[u]] == ((r << 12) | (unsigned)(tid + SNT * u))) pend &= ~(1u << u);
+    any = __syncthreads_or(pend != 0u);
   }
   if (!any) return;
-  int q[4];
+  // sequential completion: each still-pending slot gets a ticket (kept in slot[]), thread 0 hands out the
+  // smallest free values in ticket order
 #pragma unroll
-  for (int u = 0; u < 4; ++u) q[u] = pend[u] ? atomicAdd(&L.npend, 1) : -1;
+  for (int u = 0; u < SL; ++u)
+    if ((pend >> u) & 1u) slot[u] = atomicAdd(&L.npend, 1);
   __syncthreads();
   if (tid == 0) {
     unsigned v = 0;
     for (int i = 0; i < L.npend; ++i) {
       while (tbl_has(L.keys, v)) ++v;
       tbl_insert(L.keys, v);
-      L.pendv[i] = v;
+      L.u.pendv[i] = v;
     }
   }
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (q[u] >= 0) vals[u] = L.pendv[q[u]];
+  for (int u = 0; u < SL; ++u)
+    if ((pend >> u) & 1u) vals[u] = L.u.pendv[slot[u]];
   __syncthreads();
 }
 
-// indices of one range [lo, lo + n) into idx[off, off + kk)
-__device__ void sample_range(SampLds& L, const Args& a, long long lo, unsigned n, int kk, int off,
+// indices of one range [lo, lo + n) into out[off, off + kk)
+__device__ void sample_range(SampLds& L, const Args& a, int* out, long long lo, unsigned n, int kk, int off,
                              unsigned long long step, unsigned range) {
   const int tid = threadIdx.x;
   const unsigned long long seed = a.st->seed;
-  unsigned vals[4];
+  unsigned vals[SL];
   if (2 * (long long)kk <= (long long)n) {
     sample_set(L, n, kk, step, seed, range, vals);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int p = tid + 1024 * u;
-      if (p < kk) a.idx[off + p] = (int)(lo + vals[u]);
+    for (int u = 0; u < SL; ++u) {
+      const int p = tid + SNT * u;
+      if (p < kk) out[off + p] = (int)(lo + vals[u]);
     }
     __syncthreads();
     return;
   }
-  // kk > n / 2: draw the n - kk rows left out, keep the others in increasing order
+  // kk > n / 2 (then n <= 2 MAXK): draw the n - kk rows left out, keep the others in increasing order
   const int nc = (int)n - kk;
-  for (int i = tid; i < (int)n; i += 1024) L.mark[i] = 0;
+  if (nc > 0) sample_set(L, n, nc, step, seed, range, vals);
+  __syncthreads();
+  for (int i = tid; i < (int)n; i += SNT) L.u.c.mark[i] = 0;
   __syncthreads();
   if (nc > 0) {
-    sample_set(L, n, nc, step, seed, range, vals);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (tid + 1024 * u < nc) L.mark[vals[u]] = 1;
+    for (int u = 0; u < SL; ++u)
+      if (tid + SNT * u < nc) L.u.c.mark[vals[u]] = 1;
   }
   __syncthreads();
-  // block compaction: thread t owns values [8t, 8t + 8)
+  // block compaction: thread t owns values [VT t, VT t + VT)
+  constexpr int VT = 2 * MAXK / SNT;
   int c = 0;
-  for (int q = 0; q < 8; ++q) {
-    const int v = 8 * tid + q;
-    if (v < (int)n && !L.mark[v]) ++c;
+  for (int q = 0; q < VT; ++q) {
+    const int v = VT * tid + q;
+    if (v < (int)n && !L.u.c.mark[v]) ++c;
   }
-  L.cnt[tid] = c;
+  L.u.c.cnt[tid] = c;
   __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {
-    const int add = tid >= d ? L.cnt[tid - d] : 0;
+  for (int d = 1; d < SNT; d <<= 1) {
+    const int add = tid >= d ? L.u.c.cnt[tid - d] : 0;
     __syncthreads();
-    L.cnt[tid] += add;
+    L.u.c.cnt[tid] += add;
     __syncthreads();
   }
-  int pos = L.cnt[tid] - c;
-  for (int q = 0; q < 8; ++q) {
-    const int v = 8 * tid + q;
-    if (v < (int)n && !L.mark[v]) a.idx[off + pos++] = (int)(lo + v);
+  int pos = L.u.c.cnt[tid] - c;
+  for (int q = 0; q < VT; ++q) {
+    const int v = VT * tid + q;
+    if (v < (int)n && !L.u.c.mark[v]) out[off + pos++] = (int)(lo + v);
   }
   __syncthreads();
 }
 
-// The minibatch of the next step, into a.idx (one of two buffers): draw number st->draws of the sampler's stream.
-// It reads nothing the training kernels write, so it runs beside the previous step's dW1 / Adam kernels.
-template <int NIN>
-__global__ __launch_bounds__(1024) void k_sample(Args a) {
-  __shared__ SampLds L;
+// one minibatch into `out`: draw number st->draws of the sampler's stream (then st->draws + 1)
+__device__ __forceinline__ void sample_minibatch(SampLds& L, const Args& a, int* out) {
   State* st = a.st;
   const unsigned long long step = st->draws;
   __syncthreads();
   if (a.n_new == 0) {
-    sample_range(L, a, 0, (unsigned)a.n, a.Bt, 0, step, 0u);
+    sample_range(L, a, out, 0, (unsigned)a.n, a.Bt, 0, step, 0u);
   } else {
     const long long n_old = a.n - a.n_new;
-    sample_range(L, a, 0, (unsigned)n_old, a.Bt / 2, 0, step, 1u);
-    sample_range(L, a, n_old, (unsigned)a.n_new, a.Bt / 2, a.Bt / 2, step, 2u);
+    sample_range(L, a, out, 0, (unsigned)n_old, a.Bt / 2, 0, step, 1u);
+    sample_range(L, a, out, n_old, (unsigned)a.n_new, a.Bt / 2, a.Bt / 2, step, 2u);
   }
   if (threadIdx.x == 0) st->draws = step + 1;
+}
+
+// the first minibatch of a fit (and the test hook vboc_fit_sample), into a.idx
+__global__ __launch_bounds__(SNT) void k_sample(Args a) {
+  __shared__ SampLds L;
+  sample_minibatch(L, a, a.idx);
 }
 
 // acc[u] += A[16 rows][HP] (LDS, row stride LD) x B' for the column tile 16 (w + 4u) .. +15, B [HP][HP] given
@@ -320,15 +334,33 @@ __global__ __launch_bounds__(256) void k_fwd_bwd(Args a) {
   using Ly = Lay<NIN, HP>;
   constexpr int NT = HP / 64;          // 16-column tiles per wave
   constexpr int LD = HP + 4;
-  __shared__ __attribute__((aligned(16))) float H1[R2 * LD];
-  __shared__ __attribute__((aligned(16))) float G2[R2 * LD];
-  __shared__ float xs[R2 * NIN], ys[R2], dout[R2], sq[R2], red[4][R2];
+  struct FwdLds {
+    float H1[R2 * LD];
+    float G2[R2 * LD];
+    float xs[R2 * NIN], ys[R2], dout[R2], sq[R2], red[4][R2];
+  };
+  __shared__ __attribute__((aligned(16))) union {
+    FwdLds f;
+    SampLds s;
+  } U;
+  float* H1 = U.f.H1;
+  float* G2 = U.f.G2;
+  float* xs = U.f.xs;
+  float* ys = U.f.ys;
+  float* dout = U.f.dout;
+  float* sq = U.f.sq;
+  float (*red)[R2] = U.f.red;
   // the step's gate (the reference's `while val > stop and it < it_max`), from the state the previous step left;
   // block 0 publishes it for this step's dW1 / Adam kernels and the host's poll
   const State* sc = a.st;
   const int gate = (sc->val > sc->stop) && (sc->it < sc->it_lim);
   if (blockIdx.x == 0 && threadIdx.x == 0) a.st->gate = gate;
   if (!gate) return;
+  // the last workgroup draws the next step's minibatch (it reads nothing this step writes)
+  if ((int)blockIdx.x == a.Bt / R2) {
+    sample_minibatch(U.s, a, a.idx_next);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lq = lane >> 4;
   const int row0 = blockIdx.x * R2;
   const float* P = a.P;
@@ -675,8 +707,8 @@ struct vboc_fit {
   int* idx[2] = {nullptr, nullptr};
   State* st = nullptr;
   State* st_host = nullptr;           // pinned
-  hipStream_t stream = nullptr, stream2 = nullptr;   // training kernels; the sampler beside them
-  hipEvent_t ev_in = nullptr, ev_out = nullptr, t0 = nullptr, t1 = nullptr, ev_f = nullptr, ev_s = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, t0 = nullptr, t1 = nullptr;
   hipGraphExec_t exec = nullptr;
   Args key{};
   int key_poll = 0;
@@ -695,10 +727,8 @@ static int ffail(int code, const std::string& m) {
     if (e_ != hipSuccess) return ffail(VBOC_FIT_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
   } while (0)
 
-static void launch_sample(const vboc_fit* h, const Args& a, hipStream_t s) {
-  if (h->nin == 6) hipLaunchKernelGGL(k_sample<6>, dim3(1), dim3(1024), 0, s, a);
-  else if (h->nin == 4) hipLaunchKernelGGL(k_sample<4>, dim3(1), dim3(1024), 0, s, a);
-  else hipLaunchKernelGGL(k_sample<2>, dim3(1), dim3(1024), 0, s, a);
+static void launch_sample(const vboc_fit*, const Args& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_sample, dim3(1), dim3(SNT), 0, s, a);
 }
 
 template <int NIN, int HP>
@@ -706,7 +736,7 @@ static void launch_train(const vboc_fit* h, const Args& a, hipStream_t s, bool f
   constexpr int NW1 = (HP / 32) * (HP / 32);
   const int nsmall = (Lay<NIN, HP>::SMALL + 15) / 16;
   if (fwd) {
-    hipLaunchKernelGGL((k_fwd_bwd<NIN, HP>), dim3(h->bt / R2), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((k_fwd_bwd<NIN, HP>), dim3(h->bt / R2 + 1), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL((k_dw1<NIN, HP>), dim3((HP / 64) * (HP / 64) * h->S), dim3(256), 0, s, a);
     hipLaunchKernelGGL((k_adam<NIN, HP>), dim3(NW1 + nsmall), dim3(256), 0, s, a);
@@ -719,27 +749,16 @@ static void train_part(const vboc_fit* h, const Args& a, hipStream_t s, bool fwd
   else launch_train<2, 128>(h, a, s, fwd);
 }
 
-// Step i of a chunk (i = 0 .. steps - 1; the chunk starts with its first minibatch already drawn into
-// idx[parity]; step i uses idx[(parity + i) % 2]): the forward / backward kernel on `s`, then the next minibatch on `s2` (it may overwrite
-// idx[(i + 1) % 2] once step i - 1's forward kernel, which read it, is done: it waits for this step's forward
-// kernel, which stream order puts after that one), dW1 and Adam on `s`; the chunk ends joined on `s`.
-static hipError_t chunk(const vboc_fit* h, const Args& base, int steps, int parity, hipStream_t s, hipStream_t s2,
-                        hipEvent_t ev_f, hipEvent_t ev_s) {
-  hipError_t e;
+// Step i of a chunk uses the minibatch in idx[(parity + i) % 2], drawn by the previous step's forward kernel
+// (or by the fit's first k_sample), and its forward kernel draws step i + 1's into the other buffer.
+static void chunk(const vboc_fit* h, const Args& base, int steps, int parity, hipStream_t s) {
   for (int i = 0; i < steps; ++i) {
     Args a = base;
     a.idx = h->idx[(parity + i) & 1];
-    Args an = base;
-    an.idx = h->idx[(parity + i + 1) & 1];
-    if (i > 0 && (e = hipStreamWaitEvent(s, ev_s, 0)) != hipSuccess) return e;
+    a.idx_next = h->idx[(parity + i + 1) & 1];
     train_part(h, a, s, true);
-    if ((e = hipEventRecord(ev_f, s)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(s2, ev_f, 0)) != hipSuccess) return e;
-    launch_sample(h, an, s2);
-    if ((e = hipEventRecord(ev_s, s2)) != hipSuccess) return e;
     train_part(h, a, s, false);
   }
-  return hipStreamWaitEvent(s, ev_s, 0);
 }
 
 static bool supported(int nin, int hp) {
@@ -808,9 +827,6 @@ int vboc_fit_create(int nin, int hidden, int minibatch, unsigned long long seed,
 #undef FALLOC
   if ((e = hipHostMalloc((void**)&h->st_host, sizeof(State))) != hipSuccess) return fail_free(e, "hipHostMalloc");
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail_free(e, "stream");
-  if ((e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess) return fail_free(e, "stream");
-  if ((e = hipEventCreateWithFlags(&h->ev_f, hipEventDisableTiming)) != hipSuccess) return fail_free(e, "event");
-  if ((e = hipEventCreateWithFlags(&h->ev_s, hipEventDisableTiming)) != hipSuccess) return fail_free(e, "event");
   if ((e = hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming)) != hipSuccess) return fail_free(e, "event");
   if ((e = hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming)) != hipSuccess) return fail_free(e, "event");
   if ((e = hipEventCreate(&h->t0)) != hipSuccess) return fail_free(e, "event");
@@ -844,10 +860,6 @@ int vboc_fit_destroy(vboc_fit_handle h) {
   if (h->ev_out) (void)hipEventDestroy(h->ev_out);
   if (h->t0) (void)hipEventDestroy(h->t0);
   if (h->t1) (void)hipEventDestroy(h->t1);
-  if (h->ev_f) (void)hipEventDestroy(h->ev_f);
-  if (h->ev_s) (void)hipEventDestroy(h->ev_s);
-  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
-  if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -922,12 +934,8 @@ int vboc_fit_train(vboc_fit_handle h, const vboc_fit_run_t* r, void* stream) {
     }
     hipGraph_t g;
     FCHK(hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
-    const hipError_t ec = chunk(h, a, poll, 0, h->stream, h->stream2, h->ev_f, h->ev_s);
+    chunk(h, a, poll, 0, h->stream);
     FCHK(hipStreamEndCapture(h->stream, &g));
-    if (ec != hipSuccess) {
-      (void)hipGraphDestroy(g);
-      return ffail(VBOC_FIT_EHIP, std::string("graph capture: ") + hipGetErrorString(ec));
-    }
     hipError_t e = hipGraphInstantiate(&h->exec, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
     if (e != hipSuccess) return ffail(VBOC_FIT_EHIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
@@ -938,7 +946,7 @@ int vboc_fit_train(vboc_fit_handle h, const vboc_fit_run_t* r, void* stream) {
   long long launched = 0;
   for (;;) {
     if (r->graphs) FCHK(hipGraphLaunch(h->exec, h->stream));
-    else FCHK(chunk(h, a, poll, (int)(launched & 1), h->stream, h->stream2, h->ev_f, h->ev_s));
+    else chunk(h, a, poll, (int)(launched & 1), h->stream);
     FCHK(hipGetLastError());
     launched += poll;
     FCHK(hipMemcpyAsync(&s->gate, &h->st->gate, sizeof(int), hipMemcpyDeviceToHost, h->stream));

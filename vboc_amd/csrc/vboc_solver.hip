@@ -1506,7 +1506,7 @@ struct vboc_solver {
   size_t dg_bytes = 0;
   DgJobs* dg_jobs = nullptr;        // device copies of the job descriptor and of the per-workgroup batch
   Inputs* dg_in = nullptr;
-  bool dg_attr[2] = {false, false};
+  bool dg_attr[4] = {false, false, false, false};
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
   double* wave_hc = nullptr;        // path-constraint rows of the wave solver, one region per workgroup
@@ -1661,9 +1661,10 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
 
 // the data-generation kernel (dg.h): one problem's whole state machine per wave, the wave solver inside
 template <int NQ, bool FM>
-static hipError_t launch_dg(vboc_solver* h, const DgJobs& J, const Inputs& in, long long groups, hipStream_t st) {
-  const void* fn = (const void*)k_dg<NQ, FM>;
-  bool& attr = h->dg_attr[FM ? 1 : 0];
+static hipError_t launch_dg(vboc_solver* h, const DgJobs& J, const Inputs& in, long long groups, hipStream_t st,
+                           bool testing = false) {
+  const void* fn = testing ? (const void*)k_ts<NQ, FM> : (const void*)k_dg<NQ, FM>;
+  bool& attr = h->dg_attr[(FM ? 1 : 0) + (testing ? 2 : 0)];
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wave_lds);
     if (e != hipSuccess) return e;
@@ -1674,8 +1675,12 @@ static hipError_t launch_dg(vboc_solver* h, const DgJobs& J, const Inputs& in, l
   if (e == hipSuccess) e = hipMemcpyAsync(h->dg_in, &in, sizeof(Inputs), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);   // J and in live on the host stack
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_dg<NQ, FM>), dim3((unsigned)groups), dim3(64), h->wave_lds, st, h->w, h->o, in,
-                     (const Inputs*)h->dg_in, (const DgJobs*)h->dg_jobs, jb);
+  if (testing)
+    hipLaunchKernelGGL((k_ts<NQ, FM>), dim3((unsigned)groups), dim3(64), h->wave_lds, st, h->w, h->o, in,
+                       (const Inputs*)h->dg_in, (const DgJobs*)h->dg_jobs, jb);
+  else
+    hipLaunchKernelGGL((k_dg<NQ, FM>), dim3((unsigned)groups), dim3(64), h->wave_lds, st, h->w, h->o, in,
+                       (const Inputs*)h->dg_in, (const DgJobs*)h->dg_jobs, jb);
   return hipGetLastError();
 }
 
@@ -2152,23 +2157,28 @@ int vboc_data_generation_wait(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
   return dg_wait(h, b, (hipStream_t)stream);
 }
 
-int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const int* cancel, void* stream) {
-  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_data_generation: NULL argument");
+// the per-workgroup records, job descriptor and counters of a k_dg / k_ts launch (testing: the held-out set's
+// state machine, no speculation, one row per problem)
+static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const int* cancel, hipStream_t st,
+                      bool testing, int max_restarts, const char* who) {
+  const std::string W(who);
   if (h->nq != 2 && h->nq != 3)
-    return fail(VBOC_ERR_UNSUPPORTED, "vboc_data_generation: defined for the double (nq = 2) and triple (nq = 3) pendulum");
+    return fail(VBOC_ERR_UNSUPPORTED, W + ": defined for the double (nq = 2) and triple (nq = 3) pendulum");
   if (h->o.hc)
-    return fail(VBOC_ERR_UNSUPPORTED, "vboc_data_generation: the VBOC data generation has no path constraint (clear it first)");
-  if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_data_generation: B < 0");
+    return fail(VBOC_ERR_UNSUPPORTED, W + ": the boundary OCP of this driver has no path constraint (clear it first)");
+  if (b->B < 0) return fail(VBOC_ERR_ARG, W + ": B < 0");
   b->rows_used = 0;
   if (b->B == 0) return VBOC_OK;
   if (b->N_start < 2 || b->N_start + 12 > h->nmax)
-    return fail(VBOC_ERR_ARG, "vboc_data_generation: needs 2 <= N_start and N_start + 12 <= the handle's nmax "
+    return fail(VBOC_ERR_ARG, W + ": needs 2 <= N_start and N_start + 12 <= the handle's nmax "
                               "(horizon extension +9, verification horizons up to N - 1 + 4)");
-  if (!b->ids || !b->rows || !b->row_off || !b->row_cnt || !b->stats || (h->nq == 2 && (!b->ic || !b->ic_slot)))
-    return fail(VBOC_ERR_ARG, "vboc_data_generation: NULL array");
-  if (!h->coop_ok) return fail(VBOC_ERR_HIP, "vboc_data_generation: wave solver unavailable on this device");
+  if (!b->ids || !b->rows || !b->row_off || !b->row_cnt || !b->stats ||
+      (!testing && h->nq == 2 && (!b->ic || !b->ic_slot)))
+    return fail(VBOC_ERR_ARG, W + ": NULL array");
+  if (testing && b->rows_cap < b->B) return fail(VBOC_ERR_ARG, W + ": rows_cap < B (one row per problem)");
+  if (testing && max_restarts < 0) return fail(VBOC_ERR_ARG, W + ": max_restarts < 0");
+  if (!h->coop_ok) return fail(VBOC_ERR_HIP, W + ": wave solver unavailable on this device");
   HIPCHK(hipSetDevice(h->device));
-  hipStream_t st = (hipStream_t)stream;
   long long groups = b->B < h->n_regions ? b->B : h->n_regions;
   // resident problems: their hot stage records at the horizons data generation uses (N_start .. +12) fit the MALL
   const long long cap = h->group_cap > 0 ? h->group_cap
@@ -2177,7 +2187,9 @@ int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag
   // per-workgroup arrays: the solver's one-problem batch (Inputs layout) + x_sol, u_sol, saved rows, state
   const int nq = h->nq, NXR = 2 * nq + 1, NU = nq, NP = nq + 1, NX = 2 * nq, nm = h->nmax;
   const int vr_cap = 2 * nm + 2;
-  const int st_d = (int)(((nq == 2 ? sizeof(DgState<2>) : sizeof(DgState<3>)) + 15) / 16 * 2);
+  const size_t st_bytes = nq == 2 ? (sizeof(DgState<2>) > sizeof(TsState<2>) ? sizeof(DgState<2>) : sizeof(TsState<2>))
+                                  : (sizeof(DgState<3>) > sizeof(TsState<3>) ? sizeof(DgState<3>) : sizeof(TsState<3>));
+  const int st_d = (int)((st_bytes + 15) / 16 * 2);
   const size_t G = (size_t)groups;
   const size_t dbl = G * ((size_t)(nm + 1) * NXR * 3 + (size_t)nm * NU * 2 + (size_t)(nm + 1) * NU + NP + 6 * NXR +
                           2 * NU + 1 + (size_t)vr_cap * NX + st_d) + 64;
@@ -2187,13 +2199,13 @@ int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag
     h->dg_scratch = nullptr;
     h->dg_bytes = 0;
     if (hipMalloc((void**)&h->dg_scratch, need) != hipSuccess)
-      return fail(VBOC_ERR_NOMEM, "vboc_data_generation: hipMalloc of the state-machine records");
+      return fail(VBOC_ERR_NOMEM, W + ": hipMalloc of the state-machine records");
     h->dg_bytes = need;
   }
   if (!h->dg_jobs && hipMalloc((void**)&h->dg_jobs, sizeof(DgJobs)) != hipSuccess)
-    return fail(VBOC_ERR_NOMEM, "vboc_data_generation: hipMalloc of the job descriptor");
+    return fail(VBOC_ERR_NOMEM, W + ": hipMalloc of the job descriptor");
   if (!h->dg_in && hipMalloc((void**)&h->dg_in, sizeof(Inputs)) != hipSuccess)
-    return fail(VBOC_ERR_NOMEM, "vboc_data_generation: hipMalloc of the batch descriptor");
+    return fail(VBOC_ERR_NOMEM, W + ": hipMalloc of the batch descriptor");
   double* d = h->dg_scratch;
   auto take = [&](size_t n) { double* r = d; d += (n + 1) & ~(size_t)1; return r; };
   Inputs in;
@@ -2213,13 +2225,16 @@ int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag
   in.status = ip; ip += G;
   in.sqp_iter = ip; ip += G;
   in.qp_iter = ip; ip += G;
-  if ((size_t)((char*)ip - (char*)h->dg_scratch) > need) return fail(VBOC_ERR_ARG, "vboc_data_generation: internal size error");
+  if ((size_t)((char*)ip - (char*)h->dg_scratch) > need) return fail(VBOC_ERR_ARG, W + ": internal size error");
   J.ids = b->ids; J.count = b->B; J.N_start = b->N_start; J.nmax = nm; J.seed = b->seed;
   J.fail_mod = h->dg_fail_mod;
+  J.max_restarts = max_restarts;
+  J.fmt_scale = nq == 2 ? 1e4 : 1e3;
   J.q_min = b->q_min; J.q_max = b->q_max; J.v_max = b->v_max; J.u_max = b->u_max; J.dt = b->dt; J.tol = b->tol;
   J.eps = b->eps; J.g = b->g; J.l1 = b->l1; J.l2 = b->l2; J.m1 = b->m1; J.m2 = b->m2;
   J.rows = b->rows; J.rows_cap = b->rows_cap; J.row_off = b->row_off; J.row_cnt = b->row_cnt;
-  J.ic = h->nq == 2 ? b->ic : nullptr; J.ic_slot = h->nq == 2 ? b->ic_slot : nullptr; J.stats = b->stats;
+  J.ic = (!testing && h->nq == 2) ? b->ic : nullptr; J.ic_slot = (!testing && h->nq == 2) ? b->ic_slot : nullptr;
+  J.stats = b->stats;
   J.done_flag = done_flag; J.cancel = cancel;
   // counters: [0] job queue, [1] finished problems, [2..3] error flags, [4..5] rows used (u64),
   // [6] speculation events, [7] / [8] restart-job queue tail / head, [10..13] speculative solves run / used (u64)
@@ -2230,7 +2245,7 @@ int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag
   J.spec_events = 0; J.spec_stride = 0; J.spec = nullptr;
   J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = nullptr;
   size_t spec_ctl = 0;
-  if (h->dg_speculate) {
+  if (h->dg_speculate && !testing) {
     const int E = b->B < 8192 ? b->B : 8192;
     const long long res = 4 + (long long)(nm + 1) * NXR + (long long)nm * NU;
     const long long stride = DG_SPEC_HDR + DG_SPEC_JOBS * res;
@@ -2241,7 +2256,7 @@ int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag
       h->dg_spec = nullptr;
       h->dg_spec_bytes = 0;
       if (hipMalloc(&h->dg_spec, sneed) != hipSuccess)
-        return fail(VBOC_ERR_NOMEM, "vboc_data_generation: hipMalloc of the speculation pool");
+        return fail(VBOC_ERR_NOMEM, W + ": hipMalloc of the speculation pool");
       h->dg_spec_bytes = sneed;
     }
     int* ci = (int*)h->dg_spec;
@@ -2256,13 +2271,27 @@ int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag
   HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
   HIPCHK(hipEventRecord(h->ev0, st));
   hipError_t e;
-  if (h->nq == 2) e = h->factor_mfma ? launch_dg<2, true>(h, J, in, groups, st) : launch_dg<2, false>(h, J, in, groups, st);
-  else e = h->factor_mfma ? launch_dg<3, true>(h, J, in, groups, st) : launch_dg<3, false>(h, J, in, groups, st);
-  if (e != hipSuccess) return fail(VBOC_ERR_HIP, std::string("vboc_data_generation: ") + hipGetErrorString(e));
+  if (h->nq == 2)
+    e = h->factor_mfma ? launch_dg<2, true>(h, J, in, groups, st, testing) : launch_dg<2, false>(h, J, in, groups, st, testing);
+  else
+    e = h->factor_mfma ? launch_dg<3, true>(h, J, in, groups, st, testing) : launch_dg<3, false>(h, J, in, groups, st, testing);
+  if (e != hipSuccess) return fail(VBOC_ERR_HIP, W + ": " + hipGetErrorString(e));
   HIPCHK(hipEventRecord(h->ev1, st));
   h->launches = 1;
   h->coop_count = b->B;
   return VBOC_OK;
+}
+
+int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const int* cancel, void* stream) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_data_generation: NULL argument");
+  return dg_prepare(h, b, done_flag, cancel, (hipStream_t)stream, false, 0, "vboc_data_generation");
+}
+
+int vboc_testing(vboc_handle h, vboc_dg_batch_t* b, int max_restarts, void* stream) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_testing: NULL argument");
+  const int rc = dg_prepare(h, b, nullptr, nullptr, (hipStream_t)stream, true, max_restarts, "vboc_testing");
+  if (rc != VBOC_OK || b->B == 0) return rc;
+  return dg_wait(h, b, (hipStream_t)stream);
 }
 
 // the end of a data-generation launch: its counters, the pool and horizon checks

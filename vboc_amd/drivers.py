@@ -572,6 +572,20 @@ def data_generation_device(nq, ids, solver, N_start=None, seed=SEED):
     return results, stats
 
 
+def testing_device(nq, ids, solver, N_start=None, seed=SEED, max_restarts=MAX_TEST_RESTARTS):
+    """`testing(v)` for every problem id with the whole state machine on the GPU (vboc_testing: one wave per
+    problem runs the draws, the horizon extension and the perturbed restarts, dg.h k_ts).  Same return values
+    as `testing_batch`: results[i] = x_0[:2nq] of ids[i] or None, and stats.  `solver`: a lib.Solver for nq
+    (double or triple) with nmax >= N_start + 12."""
+    import torch
+    ids_t = torch.as_tensor(np.asarray(ids, dtype=np.int64), device=f"cuda:{solver.device}")
+    out = solver.testing_device(ids_t, N_start=N_start, seed=seed, max_restarts=max_restarts)
+    rows, cnt, st = out["rows"].cpu().numpy(), out["row_cnt"].cpu().numpy(), out["stats"].cpu().numpy()
+    results = [rows[b].copy() if cnt[b] == 1 else None for b in range(len(cnt))]
+    stats = dict(solves=int(st[:, 0].sum()), sqp_iter=int(st[:, 2].sum()), rounds=1, per_problem=st)
+    return results, stats
+
+
 def testing_batch(nq, ids, backend, N_start=None, seed=SEED, max_restarts=MAX_TEST_RESTARTS):
     """`testing(v)` for every problem id in `ids`, batched.  Returns (results, stats):
     results[i] is x_0[:2nq] of problem ids[i] (or None)."""

@@ -21,7 +21,7 @@ EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", 
            "vboc_solve_batch_host", "vboc_solve_batch_ft", "vboc_solve_batch_ft_host", "vboc_rk4_batch", "vboc_rk4_batch_host",
            "vboc_rk4_sens_batch_host", "vboc_last_kernel_ms",
            "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_data_generation_async",
-           "vboc_data_generation_wait", "vboc_hjr_solve_batch", "vboc_set_path_constraint",
+           "vboc_data_generation_wait", "vboc_testing", "vboc_hjr_solve_batch", "vboc_set_path_constraint",
            "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
@@ -113,6 +113,7 @@ def load():
                                                ctypes.c_void_p, ctypes.c_void_p]
     lib.vboc_data_generation_wait.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_void_p]
     lib.vboc_hjr_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(HjrBatch), ctypes.c_void_p]
+    lib.vboc_testing.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_int, ctypes.c_void_p]
     lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
@@ -274,6 +275,33 @@ class Solver:
         _check(self.lib.vboc_data_generation_wait(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
         out["rows"] = out["rows_all"][:b.rows_used]
         out["spec_solves"], out["spec_used"] = b.spec_solves, b.spec_used
+        return out
+
+    def testing_device(self, ids, N_start=None, seed=None, max_restarts=100, stream=None):
+        """The held-out set's `testing(v)` for every problem id of the int64 cuda tensor `ids` (vboc_testing,
+        dg.h k_ts).  Returns a dict of device tensors: rows [B, 2nq] (row b = problem b's x0), row_cnt (1, or -1
+        for None), stats [B, len(DG_STATS)]."""
+        import torch
+        from .ics import SEED
+        from .systems import system
+        sysd = system(self.nq)
+        N_start = int(N_start or sysd.N)
+        seed = SEED if seed is None else int(seed)
+        assert ids.is_cuda and ids.dtype == torch.int64 and ids.is_contiguous()
+        B, dev = ids.shape[0], ids.device
+        rows = torch.zeros((max(B, 1), 2 * self.nq), dtype=torch.float64, device=dev)
+        out = dict(row_off=torch.empty(B, dtype=torch.int64, device=dev), row_cnt=torch.empty(B, dtype=torch.int32, device=dev),
+                   stats=torch.empty((B, len(DG_STATS)), dtype=torch.float64, device=dev))
+        m = (list(sysd.m) + [0.0, 0.0])[:2]
+        l = (list(sysd.l) + [0.0, 0.0])[:2]
+        b = DgBatch(B=B, ids=ids.data_ptr(), seed=seed, N_start=N_start, q_min=sysd.q_min, q_max=sysd.q_max,
+                    v_max=sysd.v_max, u_max=sysd.u_max, dt=sysd.dt, tol=sysd.tol, eps=sysd.eps, g=sysd.g,
+                    l1=l[0], l2=l[1], m1=m[0], m2=m[1], rows=rows.data_ptr(), rows_cap=B,
+                    row_off=out["row_off"].data_ptr(), row_cnt=out["row_cnt"].data_ptr(), ic=0, ic_slot=0,
+                    stats=out["stats"].data_ptr(), rows_used=0, spec_solves=0, spec_used=0)
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        _check(self.lib.vboc_testing(self.h, ctypes.byref(b), int(max_restarts), ctypes.c_void_p(st.cuda_stream)))
+        out["rows"] = rows[:B]
         return out
 
     def hjr_solve_device(self, x0, weights, mean, std, u_max, stream=None):
