@@ -220,6 +220,27 @@ int vboc_data_generation_wait(vboc_handle h, vboc_dg_batch_t* batch, void* strea
  * ic_slot unused.  Synchronous on `stream`. */
 int vboc_testing(vboc_handle h, vboc_dg_batch_t* b, int max_restarts, void* stream);
 
+/* testing_test(v) on the device: the UR5 arm's (VBOC/UR5/vboc_multiprocessing_ur5.py:369-466, nq = 4) and the Cartesian
+ * double pendulum's (VBOC/Cartesian constraints/vboc_multiprocessing.py:19-129, nq = 2 on a handle with the keep-out
+ * circle) per-problem driver, the Pool(30).map fan-outs of their main blocks (:487-528; :557-585).  One wave per
+ * problem: draws from Philox stream draw_stream (ids are the keys), p = r_j choice_j / norm, q0 = xlo + u (xhi - xlo),
+ * then the horizon grows from N_start while the cost drops by more than tol; a failed solve gives None. */
+typedef struct {
+  int B;
+  const long long* ids;     /* device, int64 [B] */
+  unsigned long long seed;
+  int N_start;
+  int draw_stream;          /* vboc_amd.ics: UR5 5, Cartesian 6 */
+  double tol, dt;           /* the stop rule's tol (nlp_solver_tol_stat), the pinned time step */
+  double xlo[8], xhi[8];    /* state box [q, qdot] (2nq entries) */
+  double ulim[4];           /* |u| <= ulim (nq entries) */
+  double* rows;             /* device [B][2nq + 1]: x0 with the dt column (row_cnt 1) */
+  int* row_cnt;             /* device [B]: 1, or -1 for None */
+  double* stats;            /* device [B][9]: as vboc_dg_batch_t.stats */
+} vboc_tt_batch_t;
+
+int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream);
+
 /* The HJR one-step OCP, OCP<sys>.compute_problem(x0) of HJR/<sys>_hjr_class.py (triplependulum_hjr_class.py:
  * 117-134 with the model and options of :7-115), for every x0 of a batch, one problem per GPU lane (hjr.h):
  * x0 fixed, N = 1, h = 1e-2, u0 in [-u_max, u_max], terminal cost = logit 0 of NeuralNetCLS(2nq, hidden, 2)

@@ -208,3 +208,49 @@ def test_cartesian_run_on_oracle(tmp_path):
     assert sd["linear_relu_stack.0.weight"].shape == (16, 4)
     assert np.load(tmp_path / "data_2dof_vboc_10.npy").shape == r["X_train"].shape
     assert isinstance(torch.load(tmp_path / "mean_2dof_vboc_10_16", weights_only=True), float)
+
+
+def _same_tt(a_res, b_res, tol):
+    same = 0
+    for a, b in zip(a_res, b_res):
+        if a is None or b is None:
+            same += (a is None) == (b is None)
+        else:
+            same += bool(np.abs(np.asarray(a[0], float) - np.asarray(b[0], float)).max() <= tol)
+    return same
+
+
+@pytest.mark.gpu
+def test_cartesian_device_testing_test_matches_reference():
+    """`testing_test` on the device (vboc_testing_test, dg.h k_tt<2, HC>) against the reference function's
+    fixture (same failure injection) and the host driver on the same wave solver; then 4096 problems in one
+    launch: every returned x0 has its tip outside the circle and inside the state box."""
+    from vboc_amd import lib
+    from vboc_amd.drivers import GpuBackend, cartesian_testing_device
+    from vboc_amd.systems import system
+    g = json.load(open(GOLDEN))
+    s = lib.Solver(2, 200)
+    s.set_path_constraint(cartesian_constraint())
+    s.set_option("dg_fail_mod", g["fail_mod"])
+    res, _ = cartesian_testing_device(np.array(g["ids"]), s, N_start=g["N_start"], seed=g["seed"])
+    ref = [None if r is None else [np.asarray(r[0], float)] for r in g["results"]]
+    same = _same_tt(res, ref, 1e-5)
+    print(f"Cartesian device testing_test: {same}/{len(ref)} as the reference function")
+    assert same >= 0.95 * len(ref), (same, len(ref))
+    ids = np.arange(7000, 7064)
+    host, hst = cartesian_testing_batch(ids, GpuBackend(2, nmax=200, path_constraint=cartesian_constraint()), N_start=100)
+    s2 = lib.Solver(2, 200)
+    s2.set_path_constraint(cartesian_constraint())
+    dev, dst = cartesian_testing_device(ids, s2, N_start=100)
+    same = _same_tt(dev, host, 1e-9)
+    print(f"Cartesian device vs host driver: {same}/64, solves {dst['solves']} vs {hst['solves']}")
+    assert same >= 0.95 * len(ids), (same, len(ids))
+    big, bst = cartesian_testing_device(np.arange(100000, 104096), s2, N_start=100)
+    X = np.array([r[0] for r in big if r is not None])
+    c, sd = cartesian_constraint(), system(2)
+    tip = (sd.l[0] * np.sin(X[:, 0]) + sd.l[1] * np.sin(X[:, 1]) - c.x_c) ** 2 + \
+          (sd.l[0] * np.cos(X[:, 0]) + sd.l[1] * np.cos(X[:, 1]) - c.y_c) ** 2
+    assert X.shape[0] >= 0.5 * 4096 and (tip >= c.lh - 1e-9).all()
+    assert (X[:, :2] >= sd.q_min - 1e-9).all() and (X[:, :2] <= sd.q_max + 1e-9).all()
+    assert (np.abs(X[:, 2:4]) <= sd.v_max + 1e-6).all() and np.allclose(X[:, 4], sd.dt)
+    print(f"Cartesian device testing_test, 4096 problems: {X.shape[0]} rows, {bst['solves']} solves")

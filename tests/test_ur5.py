@@ -345,3 +345,36 @@ def test_ur5_run_on_oracle(tmp_path):
     assert not any((r2["X_train"][n_old:] == row).all(1).any() for row in r["X_train"])
     assert np.load(tmp_path / "data_4dof_vboc_train.npy").shape == r2["X_train"].shape
     assert (tmp_path / "data_4dof_vboc_train.next_id").read_text() == str(8 + 24 + 16)
+
+
+def _same_tt(a_res, b_res, tol):
+    same = 0
+    for a, b in zip(a_res, b_res):
+        if a is None or b is None:
+            same += (a is None) == (b is None)
+        else:
+            same += bool(np.abs(np.asarray(a[0], float)[:8] - np.asarray(b[0], float)[:8]).max() <= tol)
+    return same
+
+
+@pytest.mark.gpu
+def test_ur5_device_testing_test_matches_reference():
+    """`testing_test` with the whole state machine on the device (vboc_testing_test, dg.h k_tt<4>) against the
+    reference function's fixture (same failure injection, solver option dg_fail_mod) and against the host
+    driver on the same wave solver."""
+    from vboc_amd import lib
+    from vboc_amd.drivers import GpuBackend, ur5_testing_batch, ur5_testing_device
+    g = _fixture()
+    s = lib.Solver(4, 200)
+    s.set_option("dg_fail_mod", g["fail_mod"])
+    res, st = ur5_testing_device(np.array(g["ids"]), s, N_start=g["N_start"])
+    ref = [None if r is None else [np.asarray(r[0], float)] for r in g["results"]]
+    same = _same_tt(res, ref, 1e-5)
+    print(f"UR5 device testing_test: {same}/{len(ref)} as the reference function")
+    assert same >= 0.95 * len(ref), (same, len(ref))
+    ids = np.arange(5000, 5064)
+    host, hst = ur5_testing_batch(ids, GpuBackend(4), N_start=100)
+    dev, dst = ur5_testing_device(ids, lib.Solver(4, 200), N_start=100)
+    same = _same_tt(dev, host, 1e-9)
+    print(f"UR5 device vs host driver: {same}/64, solves {dst['solves']} vs {hst['solves']}")
+    assert same >= 0.95 * len(ids), (same, len(ids))

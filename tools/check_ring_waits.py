@@ -2,7 +2,7 @@
 (spill) STORE may sit between a ring DMA (global_load_lds_dwordx4) and the next hand-counted
 `s_waitcnt vmcnt(N)` - a store can complete before an older load and let the wait pass early.  (A spill
 LOAD there only over-waits: loads complete in order.)
-Compiles the device code to assembly (hipcc -S, gfx950, -O3) and scans every k_wave / k_dg / k_ts instantiation.
+Compiles the device code to assembly (hipcc -S, gfx950, -O3) and scans every k_wave / k_dg / k_ts / k_tt instantiation.
 usage: python tools/check_ring_waits.py   (exit status 1 on a violation)"""
 import os
 import re
@@ -21,7 +21,7 @@ def main():
                                SRC, "-o", asm])
         lines = open(asm).read().split("\n")
     bad_total = 0
-    starts = [k for k, l in enumerate(lines) if re.match(r"^_ZN4vboc(6k_wave|4k_dg|4k_ts)I.*:", l)]
+    starts = [k for k, l in enumerate(lines) if re.match(r"^_ZN4vboc(6k_wave|4k_dg|4k_ts|4k_tt)I.*:", l)]
     for i in starts:
         end = next(j for j in range(i, len(lines)) if lines[j].startswith(".Lfunc_end"))
         body = lines[i:end]

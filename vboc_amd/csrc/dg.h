@@ -1259,4 +1259,228 @@ void k_ts(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// `testing_test(v)` ON THE DEVICE: the training / test-set driver of the UR5 arm (VBOC/UR5/vboc_multiprocessing_ur5.py
+// :369-466) and of the Cartesian double pendulum (VBOC/Cartesian constraints/vboc_multiprocessing.py:19-129; the
+// handle carries the keep-out circle).  A random cost direction and initial position, then the horizon grows while
+// the cost still drops by more than tol; a failed solve gives None (no restarts).  Restates
+// vboc_amd/drivers.py::ur5_problem / cartesian_problem (pinned against the reference's own functions): draws from
+// Philox stream `draw_stream` in the reference's order (random() before choice() in `random.random() *
+// random.choice([-1, 1])`), p / norm(p), q0 = lo + random() (hi - lo).  Result: x0 incl. the dt column.
+// ------------------------------------------------------------------------------------------------
+struct TtJobs {
+  const long long* ids;
+  int count, N_start, nmax, draw_stream;
+  int fail_mod;                     // test-only failure injection (solver option dg_fail_mod), 0 = off
+  unsigned long long seed;
+  double tol, dt;
+  double xlo[8], xhi[8], ulim[4];   // state box [q, qdot] and torque limits (2nq / nq entries used)
+  double* st;                       // [groups][st_doubles]
+  int st_doubles;
+  double* rows;                     // [count][2nq + 1]: x0 with the dt column
+  int* row_cnt;                     // 1, or -1 for None
+  double* stats;                    // [count][DG_NSTAT]
+  unsigned* next;
+  unsigned* done;
+  unsigned* err;
+};
+
+template <int NQ>
+struct TtState {
+  int N, solves;
+  double cost, sqp, nsqp, nqp, t0, st1, it1;
+};
+
+template <int NQ>
+struct Tt {
+  static constexpr int NX = 2 * NQ, NXR = NX + 1, NU = NQ, NP = NQ + 1;
+  const TtJobs& J;
+  const Inputs& in;
+  const int wg, t;
+  TtState<NQ>* s;
+
+  __device__ Tt(const TtJobs& J_, const Inputs& in_, int wg_, int t_) : J(J_), in(in_), wg(wg_), t(t_) {
+    s = (TtState<NQ>*)(J.st + (long long)wg * J.st_doubles);
+  }
+  __device__ __forceinline__ long long row(int r) const { return (long long)wg * (J.nmax + 1) + r; }
+  __device__ __forceinline__ double* xg(int r) const { return (double*)in.xg + row(r) * NXR; }
+  __device__ __forceinline__ double* ug(int r) const { return (double*)in.ug + ((long long)wg * J.nmax + r) * NU; }
+  __device__ __forceinline__ const double* xo(int r) const { return in.xo + row(r) * NXR; }
+  __device__ __forceinline__ const double* uo(int r) const { return in.uo + ((long long)wg * J.nmax + r) * NU; }
+
+  __device__ __forceinline__ void request(int N) {
+    ((int*)in.N)[wg] = N;
+    s->solves += 1;
+  }
+
+  __device__ __forceinline__ bool start(int job) {
+#pragma clang fp contract(off)
+    const long long pid = J.ids[job];
+    s->t0 = (double)__builtin_amdgcn_s_memrealtime();
+    s->solves = 0; s->sqp = 0.0; s->nsqp = 0.0; s->nqp = 0.0; s->st1 = 0.0; s->it1 = 0.0;
+    s->cost = 1e6;
+    int di = 0;
+    auto draw = [&]() { return philox_uniform(pid, di++, J.seed, (unsigned)J.draw_stream); };
+    double p[NQ], q0[NQ];
+    UNR for (int j = 0; j < NQ; ++j) {
+      const double r = draw();
+      const double c = Dg<(NQ < 4 ? NQ : 3)>::choice_idx(draw(), 2) == 0 ? -1.0 : 1.0;
+      p[j] = r * c;
+    }
+    const double nw = np_norm<NQ>(p);
+    UNR for (int j = 0; j < NQ; ++j) p[j] = p[j] / nw;
+    UNR for (int j = 0; j < NQ; ++j) q0[j] = J.xlo[j] + draw() * (J.xhi[j] - J.xlo[j]);
+    double* P = (double*)in.p + (long long)wg * NP;
+    UNR for (int j = 0; j < NQ; ++j) P[j] = p[j];
+    P[NQ] = 0.0;
+    double* lbx = (double*)in.lbx + (long long)wg * NXR; double* ubx = (double*)in.ubx + (long long)wg * NXR;
+    double* lbxe = (double*)in.lbxe + (long long)wg * NXR; double* ubxe = (double*)in.ubxe + (long long)wg * NXR;
+    double* lb0 = (double*)in.lbx0 + (long long)wg * NXR; double* ub0 = (double*)in.ubx0 + (long long)wg * NXR;
+    double* lbu = (double*)in.lbu + (long long)wg * NU; double* ubu = (double*)in.ubu + (long long)wg * NU;
+    UNR for (int c = 0; c < NX; ++c) {
+      lbx[c] = J.xlo[c]; ubx[c] = J.xhi[c];
+      lbxe[c] = c < NQ ? J.xlo[c] : 0.0; ubxe[c] = c < NQ ? J.xhi[c] : 0.0;
+      lb0[c] = c < NQ ? q0[c] : J.xlo[c]; ub0[c] = c < NQ ? q0[c] : J.xhi[c];
+    }
+    lbx[NX] = J.dt; ubx[NX] = J.dt; lbxe[NX] = J.dt; ubxe[NX] = J.dt; lb0[NX] = J.dt; ub0[NX] = J.dt;
+    UNR for (int a = 0; a < NU; ++a) { lbu[a] = -J.ulim[a]; ubu[a] = J.ulim[a]; }
+    const int N = J.N_start;
+    for (int r = t; r <= N; r += 64) {
+      UNR for (int c = 0; c < NXR; ++c) xg(r)[c] = c < NQ ? q0[c] : (c == NX ? J.dt : 0.0);
+      if (r < N) UNR for (int a = 0; a < NU; ++a) ug(r)[a] = 0.0;
+    }
+    s->N = N;
+    request(N);
+    return true;
+  }
+
+  // 1: another solve is requested; 0: done (row written by finish)
+  __device__ __forceinline__ int feed(int job, int& ok) {
+#pragma clang fp contract(off)
+    const int N = in.N[wg];
+    const int it = in.sqp_iter[wg], qit = in.qp_iter[wg];
+    if (s->solves == 1) {
+      s->st1 = (double)in.status[wg];
+      s->it1 = (double)it;
+    }
+    s->sqp += (double)it;
+    s->nsqp += (double)N * (double)it;
+    s->nqp += (double)N * (double)qit;
+    int status = in.status[wg];
+    if (J.fail_mod > 0) {   // tests: status 4 when int(|q_0| 1e6) % fail_mod == 0 (tests/oracle_backend.py)
+      const long long q = (long long)(fabs(in.lbx0[(long long)wg * NXR]) * 1e6);
+      if (q % J.fail_mod == 0) status = 4;
+    }
+    if (status != 0) { ok = 0; return 0; }
+    const double cost = in.cost[wg];
+    if (cost > s->cost - J.tol) { ok = 1; return 0; }
+    if (N + 1 > J.nmax) {
+      if (t == 0) atomicOr(J.err + 1, 1u);
+      ok = 0;
+      return 0;
+    }
+    s->cost = cost;
+    for (int r = t; r <= N + 1; r += 64) {
+      const int rr = r <= N ? r : N;
+      UNR for (int c = 0; c < NXR; ++c) xg(r)[c] = xo(rr)[c];
+      if (r < N) {
+        UNR for (int a = 0; a < NU; ++a) ug(r)[a] = uo(r)[a];
+      } else if (r == N) {
+        UNR for (int a = 0; a < NU; ++a) ug(r)[a] = 0.0;
+      }
+    }
+    s->N = N + 1;
+    request(N + 1);
+    return 1;
+  }
+
+  __device__ __forceinline__ void finish(int job, int ok) {
+    __syncthreads();
+    if (t == 0) {
+      J.row_cnt[job] = ok ? 1 : -1;
+      double* st = J.stats + (long long)job * DG_NSTAT;
+      st[DG_SOLVES] = (double)s->solves;
+      st[DG_RK4] = 0.0;
+      st[DG_SQP] = s->sqp;
+      st[DG_NSQP] = s->nsqp;
+      st[DG_NQP] = s->nqp;
+      st[DG_T0] = s->t0;
+      st[DG_T1] = (double)__builtin_amdgcn_s_memrealtime();
+      st[DG_ST1] = s->st1;
+      st[DG_IT1] = s->it1;
+    }
+    if (ok && t < NXR) J.rows[(long long)job * NXR + t] = xo(0)[t];
+    __syncthreads();
+    if (t == 0) atomicAdd(J.done, 1u);
+  }
+};
+
+template <int NQ>
+__device__ __forceinline__ bool tt_start(const TtJobs* J, const Inputs* in, int wg, int t, int job) {
+  Tt<NQ> T(*J, *in, wg, t);
+  return T.start(job);
+}
+template <int NQ>
+__device__ __forceinline__ int tt_feed(const TtJobs* J, const Inputs* in, int wg, int t, int job, int& ok) {
+  Tt<NQ> T(*J, *in, wg, t);
+  return T.feed(job, ok);
+}
+template <int NQ>
+__device__ __forceinline__ void tt_finish(const TtJobs* J, const Inputs* in, int wg, int t, int job, int ok) {
+  Tt<NQ> T(*J, *in, wg, t);
+  T.finish(job, ok);
+}
+
+// one workgroup = one wave = one testing_test problem at a time; HC: the Cartesian keep-out circle (a problem whose
+// initial tip is inside it gets status 4 without iterating, as k_wave)
+template <int NQ, bool FM, bool HC>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WavesPerEu<NQ>::v, WavesPerEu<NQ>::v)))
+void k_tt(Work w, Opts o, Inputs in, const Inputs* inp, const TtJobs* J, WaveJobs jb) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int t = (int)threadIdx.x;
+  const int wg = (int)blockIdx.x;
+  Coop<NQ, FM, HC> C(smem, gptr(jb.regions) + (long long)wg * jb.region_doubles, w, o, t);
+  if constexpr (HC) C.gh = gptr(jb.hc) + (long long)wg * jb.hc_doubles;
+  const int count = J->count;
+  for (;;) {
+    int got = -1;
+    if (t == 0 && __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)count) {
+      const unsigned i = atomicAdd(jb.next, 1u);
+      if (i < (unsigned)count) got = (int)i;
+    }
+    got = dg_bcast(got);
+    if (got < 0) break;
+    int code = tt_start<NQ>(J, inp, wg, t, got) ? 1 : 0, ok = 0;
+    while (code) {
+      __syncthreads();
+      int it = 0, qit = 0;
+      Lane<NQ> chk(w, o, 0u);
+      bool run = chk.supported(in, wg);
+      if (!run) {
+        if (t == 0) { in.status[wg] = 5; in.sqp_iter[wg] = 0; in.qp_iter[wg] = 0; }
+      }
+      if constexpr (HC) {
+        if (run) {
+          double q0[NQ];
+          UNR for (int j = 0; j < NQ; ++j) q0[j] = in.lbx0[(long long)wg * (2 * NQ + 1) + j];
+          const double h0 = C.hc_eval(q0, nullptr);
+          if (!(h0 >= o.hlh && h0 <= o.huh)) {
+            run = false;
+            if (t == 0) { in.status[wg] = 4; in.sqp_iter[wg] = 0; in.qp_iter[wg] = 0; }
+          }
+        }
+      }
+      if (run) {
+        C.from_inputs(in, wg);
+        const int status = C.run(it, qit);
+        C.store(in, wg, status, it, qit);
+      }
+      __syncthreads();
+      code = tt_feed<NQ>(J, inp, wg, t, got, ok);
+    }
+    tt_finish<NQ>(J, inp, wg, t, got, ok);
+    __syncthreads();
+  }
+}
+
 }  // namespace vboc

@@ -1506,6 +1506,8 @@ struct vboc_solver {
   size_t dg_bytes = 0;
   DgJobs* dg_jobs = nullptr;        // device copies of the job descriptor and of the per-workgroup batch
   Inputs* dg_in = nullptr;
+  TtJobs* tt_jobs = nullptr;        // device copy of the testing_test job descriptor
+  bool tt_attr[2] = {false, false};
   bool dg_attr[4] = {false, false, false, false};
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
@@ -1684,6 +1686,26 @@ static hipError_t launch_dg(vboc_solver* h, const DgJobs& J, const Inputs& in, l
   return hipGetLastError();
 }
 
+template <int NQ, bool FM, bool HC>
+static hipError_t launch_tt(vboc_solver* h, const TtJobs& J, const Inputs& in, long long groups, hipStream_t st) {
+  const void* fn = (const void*)k_tt<NQ, FM, HC>;
+  bool& attr = h->tt_attr[NQ == 4 ? 1 : 0];
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->wave_lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  WaveJobs jb{nullptr, J.count, J.next, h->regions, h->region_doubles, HC ? h->wave_hc : nullptr,
+              HC ? h->wave_hc_doubles : 0};
+  hipError_t e = hipMemcpyAsync(h->tt_jobs, &J, sizeof(TtJobs), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(h->dg_in, &in, sizeof(Inputs), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_tt<NQ, FM, HC>), dim3((unsigned)groups), dim3(64), h->wave_lds, st, h->w, h->o, in,
+                     (const Inputs*)h->dg_in, (const TtJobs*)h->tt_jobs, jb);
+  return hipGetLastError();
+}
+
 extern "C" {
 
 const char* vboc_last_error(void) { return g_err.c_str(); }
@@ -1794,6 +1816,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->dg_scratch) (void)hipFree(h->dg_scratch);
   if (h->dg_jobs) (void)hipFree(h->dg_jobs);
   if (h->dg_in) (void)hipFree(h->dg_in);
+  if (h->tt_jobs) (void)hipFree(h->tt_jobs);
   if (h->dg_spec) (void)hipFree(h->dg_spec);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
@@ -2292,6 +2315,80 @@ int vboc_testing(vboc_handle h, vboc_dg_batch_t* b, int max_restarts, void* stre
   const int rc = dg_prepare(h, b, nullptr, nullptr, (hipStream_t)stream, true, max_restarts, "vboc_testing");
   if (rc != VBOC_OK || b->B == 0) return rc;
   return dg_wait(h, b, (hipStream_t)stream);
+}
+
+int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream) {
+  if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_testing_test: NULL argument");
+  const bool cart = h->nq == 2 && h->o.hc, arm = h->nq == 4;
+  if (!cart && !arm)
+    return fail(VBOC_ERR_UNSUPPORTED, "vboc_testing_test: defined for the UR5 arm (nq = 4) and the Cartesian double "
+                                      "pendulum (nq = 2 with the path constraint set)");
+  if (cart && !(h->hc_wave && h->wave_hc))
+    return fail(VBOC_ERR_UNSUPPORTED, "vboc_testing_test: the Cartesian constraint needs the wave solver (hc_wave)");
+  if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_testing_test: B < 0");
+  if (b->B == 0) return VBOC_OK;
+  if (b->N_start < 2 || b->N_start + 2 > h->nmax) return fail(VBOC_ERR_ARG, "vboc_testing_test: needs 2 <= N_start < nmax - 1");
+  if (!b->ids || !b->rows || !b->row_cnt || !b->stats) return fail(VBOC_ERR_ARG, "vboc_testing_test: NULL array");
+  if (!h->coop_ok) return fail(VBOC_ERR_HIP, "vboc_testing_test: wave solver unavailable on this device");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  long long groups = b->B < h->n_regions ? b->B : h->n_regions;
+  const long long cap = h->group_cap > 0 ? h->group_cap : (h->mall_mib > 0 ? wave_group_budget(h, b->N_start + 10) : 0);
+  if (cap > 0 && groups > cap) groups = cap;
+  const int nq = h->nq, NXR = 2 * nq + 1, NU = nq, NP = nq + 1, nm = h->nmax;
+  const int st_d = (int)((sizeof(TtState<4>) + 15) / 16 * 2);
+  const size_t G = (size_t)groups;
+  const size_t dbl = G * ((size_t)(nm + 1) * NXR * 2 + (size_t)nm * NU * 2 + NP + 6 * NXR + 2 * NU + 1 + st_d) + 64;
+  const size_t need = dbl * sizeof(double) + 4 * G * sizeof(int) + 256;
+  if (need > h->dg_bytes) {
+    if (h->dg_scratch) (void)hipFree(h->dg_scratch);
+    h->dg_scratch = nullptr;
+    h->dg_bytes = 0;
+    if (hipMalloc((void**)&h->dg_scratch, need) != hipSuccess)
+      return fail(VBOC_ERR_NOMEM, "vboc_testing_test: hipMalloc of the per-problem records");
+    h->dg_bytes = need;
+  }
+  if (!h->tt_jobs && hipMalloc((void**)&h->tt_jobs, sizeof(TtJobs)) != hipSuccess)
+    return fail(VBOC_ERR_NOMEM, "vboc_testing_test: hipMalloc of the job descriptor");
+  if (!h->dg_in && hipMalloc((void**)&h->dg_in, sizeof(Inputs)) != hipSuccess)
+    return fail(VBOC_ERR_NOMEM, "vboc_testing_test: hipMalloc of the batch descriptor");
+  double* d = h->dg_scratch;
+  auto take = [&](size_t n) { double* r = d; d += (n + 1) & ~(size_t)1; return r; };
+  Inputs in;
+  in.B = (int)groups; in.nmax = nm; in.head = nullptr;
+  in.xg = take(G * (nm + 1) * NXR); in.ug = take(G * nm * NU); in.p = take(G * NP);
+  in.lbx = take(G * NXR); in.ubx = take(G * NXR); in.lbu = take(G * NU); in.ubu = take(G * NU);
+  in.lbx0 = take(G * NXR); in.ubx0 = take(G * NXR); in.lbxe = take(G * NXR); in.ubxe = take(G * NXR);
+  in.xo = take(G * (nm + 1) * NXR); in.uo = take(G * nm * NU); in.cost = take(G);
+  TtJobs J;
+  J.st = take(G * st_d);
+  J.st_doubles = st_d;
+  int* ip = (int*)d;
+  in.N = ip; ip += G;
+  in.status = ip; ip += G;
+  in.sqp_iter = ip; ip += G;
+  in.qp_iter = ip; ip += G;
+  if ((size_t)((char*)ip - (char*)h->dg_scratch) > need) return fail(VBOC_ERR_ARG, "vboc_testing_test: internal size error");
+  J.ids = b->ids; J.count = b->B; J.N_start = b->N_start; J.nmax = nm; J.draw_stream = b->draw_stream;
+  J.fail_mod = h->dg_fail_mod;
+  J.seed = b->seed; J.tol = b->tol; J.dt = b->dt;
+  for (int c = 0; c < 8; ++c) { J.xlo[c] = b->xlo[c]; J.xhi[c] = b->xhi[c]; }
+  for (int c = 0; c < 4; ++c) J.ulim[c] = b->ulim[c];
+  J.rows = b->rows; J.row_cnt = b->row_cnt; J.stats = b->stats;
+  J.next = h->head; J.done = h->head + 1; J.err = h->head + 2;
+  HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
+  HIPCHK(hipEventRecord(h->ev0, st));
+  const hipError_t e = arm ? launch_tt<4, false, false>(h, J, in, groups, st) : launch_tt<2, false, true>(h, J, in, groups, st);
+  if (e != hipSuccess) return fail(VBOC_ERR_HIP, std::string("vboc_testing_test: ") + hipGetErrorString(e));
+  HIPCHK(hipEventRecord(h->ev1, st));
+  h->launches = 1;
+  h->coop_count = b->B;
+  HIPCHK(hipMemcpyAsync(h->host_done, h->head, 14 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const unsigned* c = h->host_done;
+  if (c[3]) return fail(VBOC_ERR_ARG, "vboc_testing_test: a horizon passed the handle's nmax");
+  if (c[1] != (unsigned)b->B) return fail(VBOC_ERR_HIP, "vboc_testing_test: not every problem finished");
+  return VBOC_OK;
 }
 
 // the end of a data-generation launch: its counters, the pool and horizon checks

@@ -657,6 +657,38 @@ def ur5_testing_batch(ids, backend, N_start=100, seed=SEED):
     return run_problems(4, gens, backend, nmax=getattr(backend, "nmax", 200))
 
 
+def _tt_results(out, ncols):
+    rows, cnt, st = out["rows"].cpu().numpy(), out["row_cnt"].cpu().numpy(), out["stats"].cpu().numpy()
+    results = [[rows[b, :ncols].copy()] if cnt[b] == 1 else None for b in range(len(cnt))]
+    return results, dict(solves=int(st[:, 0].sum()), sqp_iter=int(st[:, 2].sum()), rounds=1, per_problem=st)
+
+
+def ur5_testing_device(ids, solver, N_start=100, seed=SEED):
+    """`testing_test(v)` of the UR5 driver for every problem id with the whole state machine on the GPU
+    (vboc_testing_test: one wave per problem, dg.h k_tt).  Same return values as `ur5_testing_batch`.
+    `solver`: a lib.Solver(4, nmax)."""
+    import torch
+    from .ics import UR5_STREAM
+    from .ur5 import DT, NQ, U_LIMITS, XMAX, XMIN
+    ids_t = torch.as_tensor(np.asarray(ids, dtype=np.int64), device=f"cuda:{solver.device}")
+    out = solver.testing_test_device(ids_t, N_start, seed, UR5_STREAM, 1e-3, DT, XMIN, XMAX, U_LIMITS)
+    return _tt_results(out, 2 * NQ)
+
+
+def cartesian_testing_device(ids, solver, N_start=100, seed=SEED):
+    """`testing_test(v)` of the Cartesian driver for every problem id on the GPU (vboc_testing_test, k_tt with
+    the keep-out circle).  Same return values as `cartesian_testing_batch` ([x_0] with the dt column, or None).
+    `solver`: a lib.Solver(2, nmax) with set_path_constraint(systems.cartesian_constraint())."""
+    import torch
+    from .ics import CART_STREAM
+    sysd = system(2)
+    ids_t = torch.as_tensor(np.asarray(ids, dtype=np.int64), device=f"cuda:{solver.device}")
+    xlo = [sysd.q_min] * 2 + [-sysd.v_max] * 2
+    xhi = [sysd.q_max] * 2 + [sysd.v_max] * 2
+    out = solver.testing_test_device(ids_t, N_start, seed, CART_STREAM, sysd.tol, sysd.dt, xlo, xhi, [sysd.u_max] * 2)
+    return _tt_results(out, 5)
+
+
 def ur5_set(results):
     """X = np.array([i for f in X_temp for i in f]) over the non-None results (:493-495)."""
     rows = [row for t in results if t is not None for row in t]

@@ -21,7 +21,8 @@ EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", 
            "vboc_solve_batch_host", "vboc_solve_batch_ft", "vboc_solve_batch_ft_host", "vboc_rk4_batch", "vboc_rk4_batch_host",
            "vboc_rk4_sens_batch_host", "vboc_last_kernel_ms",
            "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_data_generation_async",
-           "vboc_data_generation_wait", "vboc_testing", "vboc_hjr_solve_batch", "vboc_set_path_constraint",
+           "vboc_data_generation_wait", "vboc_testing", "vboc_testing_test", "vboc_hjr_solve_batch",
+           "vboc_set_path_constraint",
            "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
@@ -59,6 +60,14 @@ class HjrBatch(ctypes.Structure):
                [(n, ctypes.c_void_p) for n in ("W0", "b0", "W1", "b1", "W2", "b2")] + \
                [(n, ctypes.c_double) for n in ("mean", "std", "u_max")] + \
                [(n, ctypes.c_void_p) for n in ("status", "cost", "u", "x1", "sqp_iter", "qp_iter")]
+
+
+class TtBatch(ctypes.Structure):
+    """vboc_tt_batch_t (include/vboc.h): the device testing_test call (UR5, Cartesian)."""
+    _fields_ = [("B", ctypes.c_int), ("ids", ctypes.c_void_p), ("seed", ctypes.c_ulonglong), ("N_start", ctypes.c_int),
+                ("draw_stream", ctypes.c_int), ("tol", ctypes.c_double), ("dt", ctypes.c_double),
+                ("xlo", ctypes.c_double * 8), ("xhi", ctypes.c_double * 8), ("ulim", ctypes.c_double * 4),
+                ("rows", ctypes.c_void_p), ("row_cnt", ctypes.c_void_p), ("stats", ctypes.c_void_p)]
 
 
 # per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
@@ -114,6 +123,7 @@ def load():
     lib.vboc_data_generation_wait.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_void_p]
     lib.vboc_hjr_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(HjrBatch), ctypes.c_void_p]
     lib.vboc_testing.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_int, ctypes.c_void_p]
+    lib.vboc_testing_test.argtypes = [ctypes.c_void_p, ctypes.POINTER(TtBatch), ctypes.c_void_p]
     lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
@@ -302,6 +312,25 @@ class Solver:
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         _check(self.lib.vboc_testing(self.h, ctypes.byref(b), int(max_restarts), ctypes.c_void_p(st.cuda_stream)))
         out["rows"] = rows[:B]
+        return out
+
+    def testing_test_device(self, ids, N_start, seed, draw_stream, tol, dt, xlo, xhi, ulim, stream=None):
+        """`testing_test(v)` for every problem id of the int64 cuda tensor `ids` (vboc_testing_test, dg.h k_tt): the
+        UR5 arm (nq 4) or the Cartesian double pendulum (nq 2, handle with the circle).  Returns a dict of device
+        tensors: rows [B, 2nq + 1] (x0 with the dt column), row_cnt (1, or -1 for None), stats [B, len(DG_STATS)]."""
+        import torch
+        assert ids.is_cuda and ids.dtype == torch.int64 and ids.is_contiguous()
+        B, dev, nx = ids.shape[0], ids.device, 2 * self.nq
+        out = dict(rows=torch.zeros((max(B, 1), nx + 1), dtype=torch.float64, device=dev),
+                   row_cnt=torch.empty(B, dtype=torch.int32, device=dev),
+                   stats=torch.empty((B, len(DG_STATS)), dtype=torch.float64, device=dev))
+        pad = lambda v, n: (ctypes.c_double * n)(*(list(map(float, v)) + [0.0] * (n - len(v))))
+        b = TtBatch(B=B, ids=ids.data_ptr(), seed=int(seed), N_start=int(N_start), draw_stream=int(draw_stream),
+                    tol=float(tol), dt=float(dt), xlo=pad(xlo, 8), xhi=pad(xhi, 8), ulim=pad(ulim, 4),
+                    rows=out["rows"].data_ptr(), row_cnt=out["row_cnt"].data_ptr(), stats=out["stats"].data_ptr())
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        _check(self.lib.vboc_testing_test(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        out["rows"] = out["rows"][:B]
         return out
 
     def hjr_solve_device(self, x0, weights, mean, std, u_max, stream=None):
