@@ -63,12 +63,12 @@ def main():
             line(case, "host-rounds", m, res, st, sec)
         elif case == "ur5":              # configs[4]'s per-GPU share: 12 500 testing_test problems
             ids = np.arange(10**6, 10**6 + 12500)
-            s = lib.Solver(4, 200)
+            s = lib.Solver(4, 400)            # a few arm problems keep extending past 100 stages
             D.ur5_testing_device(ids[:256], s, N_start=100)
             (res, st), sec = timed(lambda: D.ur5_testing_device(ids, s, N_start=100))
             line(case, "device", len(ids), res, st, sec)
             m = min(len(ids), a.host_max)
-            (res, st), sec = timed(lambda: D.ur5_testing_batch(ids[:m], D.GpuBackend(4, nmax=200), N_start=100))
+            (res, st), sec = timed(lambda: D.ur5_testing_batch(ids[:m], D.GpuBackend(4, nmax=400), N_start=100))
             line(case, "host-rounds", m, res, st, sec)
 
 
