@@ -66,9 +66,25 @@ def load_artifacts(out_dir, nq, device="cpu"):
                 rmse=np.load(os.path.join(out_dir, f"rmse_{tag}.npy")))
 
 
+def _device_solver(backend, nmin):
+    """The backend's lib.Solver when the state machines can run on the device (the product GPU backend with a
+    horizon capacity of at least nmin), else None (the oracle backends of the CPU tests)."""
+    solver = getattr(backend, "solver", None)
+    if solver is not None and hasattr(solver, "testing_device") and solver.nmax >= nmin:
+        return solver
+    return None
+
+
 def make_test_set(nq, backend, num_prob=1000, first_id=0, out_dir=None, seed=SEED):
-    """`testing` over num_prob problems -> X_test (data<n>_test.npy, triplependulum_testdata.py:137-145)."""
-    res, stats = testing_batch(nq, np.arange(first_id, first_id + num_prob), backend, seed=seed)
+    """`testing` over num_prob problems -> X_test (data<n>_test.npy, triplependulum_testdata.py:137-145).  On the
+    product GPU backend the whole state machine runs on the device (drivers.testing_device, one launch)."""
+    from .drivers import testing_device
+    ids = np.arange(first_id, first_id + num_prob)
+    solver = _device_solver(backend, system(nq).N + 12) if nq in (2, 3) else None
+    if solver is not None:
+        res, stats = testing_device(nq, ids, solver, seed=seed)
+    else:
+        res, stats = testing_batch(nq, ids, backend, seed=seed)
     X = heldout_set(nq, res)
     if out_dir is not None:
         os.makedirs(out_dir, exist_ok=True)
@@ -322,11 +338,13 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
     new initial states instead of repeating the Philox-keyed ones.  Returns dict(X_test, X_train, fit,
     rmse_train, rmse_test, stats)."""
     import torch
-    from .drivers import GpuBackend, ur5_set, ur5_testing_batch
+    from .drivers import GpuBackend, ur5_set, ur5_testing_batch, ur5_testing_device
     log = log or (lambda *a: None)
-    backend = backend or GpuBackend(4, nmax=200)
+    backend = backend or GpuBackend(4, nmax=400)   # some arm problems extend past 100 stages (tools/testing_probe.py)
     t0 = time.time()
-    res, st_test = ur5_testing_batch(np.arange(num_test), backend)
+    dev = _device_solver(backend, 112)
+    tt = (lambda ids: ur5_testing_device(ids, dev)) if dev is not None else (lambda ids: ur5_testing_batch(ids, backend))
+    res, st_test = tt(np.arange(num_test))
     X_test = ur5_set(res)
     log(f"test set: {X_test.shape[0]} rows of {num_test} in {time.time() - t0:.1f} s")
     t1 = time.time()
@@ -338,7 +356,7 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
         X_old = np.load(old_path)                      # allow_pickle=False: plain float64 rows
         with open(old_path[:-4] + ".next_id") as f:
             first = int(f.read())
-    res, st_train = ur5_testing_batch(np.arange(first, first + num_train), backend)
+    res, st_train = tt(np.arange(first, first + num_train))
     X_save = ur5_set(res)
     X_train = np.concatenate((X_old, X_save))
     log(f"training set: {X_save.shape[0]} new rows of {num_train} in {time.time() - t1:.1f} s, "
@@ -382,17 +400,20 @@ def cartesian_run(backend=None, num_test=1000, num_train=100000, out_dir=None, d
     backend: a drivers backend carrying the circle (default: GpuBackend(2, path_constraint=...)).  Returns
     dict(X_test, X_train, fit, rmse_train, rmse_test, stats)."""
     import torch
-    from .drivers import GpuBackend, cartesian_testing_batch
+    from .drivers import GpuBackend, cartesian_testing_batch, cartesian_testing_device
     from .systems import cartesian_constraint
     log = log or (lambda *a: None)
     backend = backend or GpuBackend(2, nmax=200, path_constraint=cartesian_constraint())
     rows = lambda res: np.array([r for t in res if t is not None for r in t], dtype=np.float64).reshape(-1, 5)
     t0 = time.time()
-    res, st_test = cartesian_testing_batch(np.arange(num_test), backend)
+    dev = _device_solver(backend, 112)
+    tt = (lambda ids: cartesian_testing_device(ids, dev)) if dev is not None else \
+        (lambda ids: cartesian_testing_batch(ids, backend))
+    res, st_test = tt(np.arange(num_test))
     X_test = rows(res)
     log(f"test set: {X_test.shape[0]} rows of {num_test} in {time.time() - t0:.1f} s")
     t1 = time.time()
-    res, st_train = cartesian_testing_batch(np.arange(num_test, num_test + num_train), backend)
+    res, st_train = tt(np.arange(num_test, num_test + num_train))
     X_train = rows(res)
     log(f"training set: {X_train.shape[0]} rows of {num_train} in {time.time() - t1:.1f} s")
     mean, std = position_stats(X_train, 2)
