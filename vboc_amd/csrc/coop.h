@@ -76,6 +76,15 @@ struct WaveLayout {
   static constexpr int RSF = NQ <= 3 ? 256 : 128 * P_FAC, NSF = VBOC_NSF, DF = VBOC_DF,
                        RSV = NQ <= 3 ? 128 : 128 * P_VMAX, NSV = VBOC_NSV, DV = VBOC_DV;
   static constexpr int RING_D = NSF * RSF > NSV * RSV ? NSF * RSF : NSV * RSV;
+  // Grouped recursions (pendulum chains): one LDS-DMA lands 64 chunks of 16 B, i.e. the windows of S
+  // consecutive stages (lane l: chunk l % (W/2) of stage l / (W/2)), so the vector / forward sweeps issue one
+  // DMA per S stages and walk a group's stages with compile-time slot offsets.  Groups may run past stage
+  // N - 1 (the partial top group): the region carries SLACK stage records behind stage nmax for those loads.
+  static constexpr int S_CAP = 4;
+  static constexpr int S_VEC = NQ <= 3 ? (64 / (W_VEC / 2) < S_CAP ? 64 / (W_VEC / 2) : S_CAP) : 1,
+                       S_FWD = NQ <= 3 ? (64 / (W_FWD / 2) < S_CAP ? 64 / (W_FWD / 2) : S_CAP) : 1, SLACK = S_CAP;
+  static_assert(NQ > 3 || (S_VEC * W_VEC <= RSV && S_FWD * W_FWD <= RSV && (NSV & (NSV - 1)) == 0),
+                "grouped windows fit one ring slot");
   static_assert(OB % 2 == 0 && OZ % 2 == 0 && OD % 2 == 0 && OK % 2 == 0 && OPE % 2 == 0 && OC % 2 == 0 &&
                     OACL % 2 == 0 && OX % 2 == 0,
                 "16-byte aligned field ranges");
@@ -91,7 +100,7 @@ struct WaveLayout {
   // costate) so that the recursions issue no global stores
   static_assert(M0 * NX <= NX * NX, "stage-0 B'P reuses the PA scratch");
   static constexpr size_t lds_bytes(int nmax) { return ((size_t)XS + (size_t)(nmax + 1) * NX) * sizeof(double); }
-  static constexpr size_t region_doubles(int nmax) { return (size_t)REC * (nmax + 1); }
+  static constexpr size_t region_doubles(int nmax) { return (size_t)REC * (nmax + 1 + SLACK); }
 };
 
 // one output of a recursion step:  out = s[ini] + sg * sum_q s[x1+q*sx1] s[y1+q*sy1]
@@ -321,6 +330,29 @@ struct Coop {
                  : "=&s"(keep)
                  : "v"(src), "s"(lds)
                  : "memory");
+  }
+  // the same with a wave-uniform base (SGPR pair) and a per-lane byte offset: no per-lane 64-bit address
+  // arithmetic in the recursions' loops (the lane offsets are computed once per pass)
+  __device__ __forceinline__ void dma_s(const gdouble* base, unsigned voff, int dst) const {
+    const unsigned lds = lds0 + 8u * (unsigned)dst;
+    // the base as an SGPR pair (readfirstlane folds away where the compiler already holds it in SGPRs)
+    const unsigned long long b = (unsigned long long)(size_t)base;
+    const unsigned long long bs = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32)) << 32) |
+                                  (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(bs), "s"(lds)
+                 : "memory");
+  }
+  // lane byte offset of a grouped window load: chunk l % (W/2) of stage l / (W/2) (lanes past S windows repeat
+  // the last chunk of stage S - 1; they land in the slot's junk tail)
+  template <int LO, int W, int S>
+  __device__ __forceinline__ unsigned grp_off() const {
+    constexpr int CH = W / 2;
+    const int u = t / CH < S ? t / CH : S - 1;
+    const int c = t - u * CH < CH ? t - u * CH : CH - 1;
+    return 8u * (unsigned)(u * REC + LO + 2 * c);
   }
   // wait until at most N VMEM ops of this wave are outstanding (LDS-DMA landings are ordered for this
   // wave's own ds_reads by this wait alone)
@@ -1247,6 +1279,49 @@ struct Coop {
     if (t < NX) s[L::PV + t] = pcur;
     const int cnt = N - 1;   // stages N-1 .. 1
     __syncthreads();
+    if constexpr (L::S_VEC > 1) {
+      // grouped sweep: group G = stages [1 + G S, 1 + G S + S), walked from the top group down (sweep index
+      // j = ng - 1 - G selects the ring slot); one DMA lands a group's windows [PE | C | ACL], DV groups ahead
+      constexpr int S = L::S_VEC, W = L::W_VEC;
+      const int ng = (cnt + S - 1) / S;
+      const unsigned voff = grp_off<L::LO_VEC, W, S>();
+      auto gdma = [&](int j) {
+        const int G = ng - 1 - j >= 0 ? ng - 1 - j : 0;
+        dma_s(g + (long long)(1 + G * S) * REC, voff, vslot(j & (L::NSV - 1)));
+      };
+      const int i = t < NX ? t : NX - 1;
+      // v rows land in XS (lanes past NX write their own TRASH word: no exec-masked store in the chain)
+      const int xm = t < NX ? NX : 0, xb = t < NX ? L::XS + t : L::TRASH + t;
+      double pv[NX];
+      UNR for (int q = 0; q < NX; ++q) pv[q] = rdlane(pcur, q);
+      settle();
+      if (ng >= 1) {
+        UNR for (int d = 0; d < L::DV; ++d) gdma(d);
+      }
+      for (int j = 0; j < ng; ++j) {
+        const int G = ng - 1 - j;
+        gdma(j + L::DV);
+        vmwait<L::DV>();   // group j has landed (the DV younger DMAs stay in flight)
+        const int kb = vslot(j & (L::NSV - 1));
+        double acl[S][NX], cc[S], pe[S];
+        UNR for (int u = 0; u < S; ++u) {
+          UNR for (int q = 0; q < NX; ++q) acl[u][q] = s[kb + u * W + (OACL - OPE) + q * NX + i];
+          cc[u] = s[kb + u * W + (OC - OPE) + i];
+          pe[u] = s[kb + u * W + i];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        UNR for (int u = S - 1; u >= 0; --u) {
+          const int k = 1 + G * S + u;
+          if (k > cnt) continue;   // stages past N - 1 in the top group (wave-uniform)
+          double p0 = cc[u], p1 = 0.0;
+          UNR for (int q = 0; q < NX; q += 2) p0 += acl[u][q] * pv[q];
+          UNR for (int q = 1; q < NX; q += 2) p1 += acl[u][q] * pv[q];
+          s[xb + k * xm] = pe[u] + pcur;
+          pcur = p0 + p1;
+          UNR for (int q = 0; q < NX; ++q) pv[q] = rdlane(pcur, q);
+        }
+      }
+    } else {
     // stage windows [PE | C | ACL] through the 8-slot LDS-DMA ring, DV stages ahead (sweep index j <->
     // stage N-1-j, clamped at 1): one DMA per stage, so DV - 1 are younger than the one waited for
     constexpr int PV = L::P_VEC;
@@ -1288,6 +1363,7 @@ struct Coop {
       UNR for (int q = 0; q < NX; ++q) acl[q] = an[q];
       cc = cn;
       pe = pn;
+    }
     }
     if (t < NX) s[L::PV + t] = pcur;
     __syncthreads();
@@ -1408,6 +1484,45 @@ struct Coop {
     SPROF(1)
     const int cnt = N - 1;   // stages 1 .. N-1
     __syncthreads();
+    if constexpr (L::S_FWD > 1) {
+      // grouped sweep (see vec): group j = stages [1 + j S, 1 + j S + S), windows [C | ACL]
+      constexpr int S = L::S_FWD, W = L::W_FWD;
+      const int ng = (cnt + S - 1) / S;
+      const unsigned voff = grp_off<L::LO_FWD, W, S>();
+      auto gdma = [&](int j) {
+        const int G = j < ng ? j : ng - 1;
+        dma_s(g + (long long)(1 + G * S) * REC, voff, vslot(j & (L::NSV - 1)));
+      };
+      const int i = t < NX ? t : NX - 1;
+      const int xm = t < NX ? NX : 0, xb = t < NX ? L::XS + NX + t : L::TRASH + t;
+      double dx[NX];
+      UNR for (int q = 0; q < NX; ++q) dx[q] = s[L::DXV + q];
+      settle();
+      if (ng >= 1) {
+        UNR for (int d = 0; d < L::DV; ++d) gdma(d);
+      }
+      for (int j = 0; j < ng; ++j) {
+        gdma(j + L::DV);
+        vmwait<L::DV>();   // group j has landed
+        const int kb = vslot(j & (L::NSV - 1));
+        double acl[S][NX], cc[S];
+        UNR for (int u = 0; u < S; ++u) {
+          UNR for (int q = 0; q < NX; ++q) acl[u][q] = s[kb + u * W + (OACL - OC) + i * NX + q];
+          cc[u] = s[kb + u * W + i];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        UNR for (int u = 0; u < S; ++u) {
+          const int k = 1 + j * S + u;
+          if (k > cnt) break;   // stages past N - 1 in the top group (wave-uniform)
+          double p0 = cc[u], p1 = 0.0;
+          UNR for (int q = 0; q < NX; q += 2) p0 += acl[u][q] * dx[q];
+          UNR for (int q = 1; q < NX; q += 2) p1 += acl[u][q] * dx[q];
+          const double dn = p0 + p1;
+          s[xb + k * xm] = dn;
+          UNR for (int q = 0; q < NX; ++q) dx[q] = rdlane(dn, q);
+        }
+      }
+    } else {
     // stage windows [C | ACL] through the 8-slot LDS-DMA ring, DV stages ahead (sweep index j <-> stage
     // 1 + j, clamped at N - 1)
     constexpr int PW = L::P_FWD;
@@ -1448,6 +1563,7 @@ struct Coop {
         UNR for (int q = 0; q < NX; ++q) acl[q] = an[q];
         cc = cn;
       }
+    }
     }
     __syncthreads();   // dx rows (global) visible to the stage-parallel pass
     SPROF(2)
