@@ -1044,6 +1044,15 @@ struct Coop {
   // H_u rows NX .. NX+NU-1 live in accumulator registers HR0, HR0 + 1; the LDS image keeps those two
   // registers of every lane group: image row (row & 3) + 4 * ((row >> 2) - HR0)
   static constexpr int HR0 = NX >> 2;
+  // -DVBOC_RINV (measurement builds): factor_mfma stores Ru^-1 in closed form instead of chol(Ru) for the
+  // triple, vec's k_f reads it as such.  Off in the product: 2 % less kernel time on 16k first solves, but a
+  // rounding-level change that flips one tolerance decision of the reference fixture's 12 data-generation
+  // problems (profiles/r03z_rinv_ab.json)
+#ifdef VBOC_RINV
+  static constexpr bool RINV = FM && NU == 3;
+#else
+  static constexpr bool RINV = false;
+#endif
   static_assert(((NX + NU - 1) >> 2) <= HR0 + 1, "H_u spans two accumulator registers");
   __device__ __forceinline__ static constexpr int hrow(int row) { return (row & 3) + 4 * ((row >> 2) - HR0); }
   // The loop body is written for a low VALU count (the wave solver is VALU-issue bound): loop-invariant
@@ -1120,8 +1129,9 @@ struct Coop {
       fdma(j + 2);
       vmwait<2 * P>();   // loads only, as in factor()
       dbg_check(kb, k, 0, L::W_FAC, 1);
-      double g0 = s[kb * gb[0] + goff[0]] * gm[0], g1 = s[kb * gb[1] + goff[1]] * gm[1];
-      const double hv = s[kb * hb + hoff];
+      // the three operand reads issue back to back (one LDS latency, not three)
+      const double r0 = s[kb * gb[0] + goff[0]], r1 = s[kb * gb[1] + goff[1]], hv = s[kb * hb + hoff];
+      double g0 = r0 * gm[0], g1 = r1 * gm[1];
       vreg(g0);
       vreg(g1);
       // P G (rows / columns of D beyond the stage blocks only meet zero rows of G)
@@ -1152,6 +1162,28 @@ struct Coop {
         }
         hu[a] = s[HS + ia * 16 + c];
       }
+      double w[NU];
+      if constexpr (RINV) {
+        // Ru^-1 in closed form (adjugate / determinant): a dependent chain of ~14 FP64 ops instead of the
+        // Cholesky's ~35; positive definiteness by Sylvester's criterion (the Cholesky's pivot test in exact
+        // arithmetic).  K = -Ru^-1 S and the Schur update S' Ru^-1 S = hu' w use the same w.
+        const double a = Lm[0], b = Lm[1], c = Lm[2], d = Lm[4], e = Lm[5], f = Lm[8];
+        const double c00 = d * f - e * e, c01 = c * e - b * f, c02 = b * e - c * d;
+        const double c11 = a * f - c * c, c12 = b * c - a * e, c22 = a * d - b * b;
+        const double det = a * c00 + b * c01 + c * c02;
+        ok = ok && (a > 0.0) && (c22 > 0.0) && (det > 0.0);
+        double r = __builtin_amdgcn_rcp(det);
+        UNR for (int it = 0; it < 2; ++it) r = fma(r, fma(-det, r, 1.0), r);
+        Lm[0] = c00 * r; Lm[1] = Lm[3] = c01 * r; Lm[2] = Lm[6] = c02 * r;
+        Lm[4] = c11 * r; Lm[5] = Lm[7] = c12 * r; Lm[8] = c22 * r;
+        UNR for (int i = 0; i < NU; ++i) w[i] = Lm[i * NU] * hu[0] + Lm[i * NU + 1] * hu[1] + Lm[i * NU + 2] * hu[2];
+        double zs = 0.0, ws = 0.0;
+        UNR for (int i = 0; i < NU; ++i) { zs = fma(hu[i], zm[i], zs); ws = fma(w[i], zm[i], ws); }
+        double nz = -zs;
+        vreg(ws);
+        vreg(nz);
+        Dm = __builtin_amdgcn_mfma_f64_16x16x4f64(nz, ws, h, 0, 0, 0);
+      } else {
       const bool okk = chol_inv<NU>(Lm, id);
       ok = ok && okk;
       double z[NU], zs = 0.0;
@@ -1165,13 +1197,18 @@ struct Coop {
       vreg(zs);
       vreg(nz);
       Dm = __builtin_amdgcn_mfma_f64_16x16x4f64(nz, zs, h, 0, 0, 0);
-      // outputs of stage k into its ring slot: K = -Ru^-1 S, M = Ru^-1 Y, chol(Ru), Y, P e
-      double w[NU];
       UNR for (int a = NU - 1; a >= 0; --a) {
         double tt = z[a];
         UNR for (int b = a + 1; b < NU; ++b) tt -= Lm[b * NU + a] * w[b];
         w[a] = tt * id[a];
       }
+      }
+#ifndef VBOC_FAC_NOSB
+      // the recursion's state update issues before the stage's outputs (they are off the critical path):
+      // the empty asm keeps the MFMA from being sunk to the loop latch
+      asm volatile("" : "+v"(Dm));
+#endif
+      // outputs of stage k into its ring slot: K = -Ru^-1 S, M = Ru^-1 Y, chol(Ru) (RINV: Ru^-1), Y, P e
       UNR for (int a = 0; a < NU; ++a) {
         s[kb + kofs + a * NX] = -w[a];
         s[kb + mofs + a * NQ] = w[a];
@@ -1387,7 +1424,16 @@ struct Coop {
         r[a] = x;
       }
       UNR for (int e = 0; e < NU * NU; ++e) Lm[e] = ly[LR_ + e];
-      chol_solve<NU>(Lm, r);
+      if constexpr (RINV) {
+        double q[NU];
+        UNR for (int a = 0; a < NU; ++a) {
+          q[a] = 0.0;
+          UNR for (int b = 0; b < NU; ++b) q[a] += Lm[a * NU + b] * r[b];
+        }
+        UNR for (int a = 0; a < NU; ++a) r[a] = q[a];
+      } else {
+        chol_solve<NU>(Lm, r);
+      }
       UNR for (int a = 0; a < NU; ++a) {
         r[a] = -r[a];
         st(k, OKF + a) = r[a];
@@ -1789,7 +1835,11 @@ struct Coop {
     // VGPR lanes, VGPRs to AGPRs) under a partial exec mask, and that build returned wrong merit values on a
     // few problems per batch: longer line searches than the oracle's, 3 % SQP-iteration agreement
     // (profiles/r02p_ur5_merit_bisect.log).
+#ifdef VBOC_MERIT_PARTIAL_EXEC
+    constexpr bool UNI = false;   // reproducer build of the round-2 defect (tools/ur5_merit_repro.sh)
+#else
     constexpr bool UNI = NQ == 4;
+#endif
     for (int k0 = UNI ? 0 : t; k0 <= N; k0 += 64) {
       const bool live = !UNI || k0 + t <= N;
       const int k = UNI ? (live ? k0 + t : N) : k0;
