@@ -128,17 +128,65 @@ __device__ __forceinline__ double rdlane(double v, int lane) {
   const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), lane);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
-__device__ __forceinline__ double wsum(double v) {
-  UNR for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+// Wave reductions: the butterfly `for (off = 32; off >= 1; off >>= 1) v = op(v, shfl_xor(v, off))` with the same
+// association, but without the LDS crossbar (ds_bpermute: two per double per step, each a ~60-cycle round trip):
+// off 32 / 16 by v_permlane32_swap / v_permlane16_swap (gfx950; each lane ends up with its own and its partner's
+// value in the two outputs), off 8 by DPP row_ror:8 (= xor 8 inside a 16-lane row), off 4 by row_ror:4 (= xor 4
+// once lanes i and i^8 hold equal values, which the off-8 step leaves), off 2 / 1 by quad_perm.  op is
+// commutative (IEEE add / max / min), so every lane computes the bits of the shuffle butterfly.
+__device__ __forceinline__ double dbl_of(unsigned hi, unsigned lo) {
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <bool P32>
+__device__ __forceinline__ void wswap(double v, double& a, double& b) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned l = (unsigned)u, h = (unsigned)(u >> 32);
+  if constexpr (P32) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(l, l, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(h, h, false, false);
+    a = dbl_of(hi[0], lo[0]); b = dbl_of(hi[1], lo[1]);
+  } else {
+    const auto lo = __builtin_amdgcn_permlane16_swap(l, l, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+    a = dbl_of(hi[0], lo[0]); b = dbl_of(hi[1], lo[1]);
+  }
+}
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const int l = __builtin_amdgcn_update_dpp(0, (int)(unsigned)u, CTRL, 0xF, 0xF, false);
+  const int h = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(u >> 32), CTRL, 0xF, 0xF, false);
+  return dbl_of((unsigned)h, (unsigned)l);
+}
+template <class OP>
+__device__ __forceinline__ double wred(double v, OP op) {
+  double a, b;
+  wswap<true>(v, a, b);
+  v = op(a, b);
+  wswap<false>(v, a, b);
+  v = op(a, b);
+  v = op(v, dppd<0x128>(v));   // row_ror:8
+  v = op(v, dppd<0x124>(v));   // row_ror:4
+  v = op(v, dppd<0x4E>(v));    // quad_perm [2,3,0,1]
+  v = op(v, dppd<0xB1>(v));    // quad_perm [1,0,3,2]
   return uni(v);
+}
+#ifdef VBOC_SHFL_RED   // measurement builds: the ds_bpermute butterfly
+template <class OP>
+__device__ __forceinline__ double wred_shfl(double v, OP op) {
+  UNR for (int off = 32; off >= 1; off >>= 1) v = op(v, __shfl_xor(v, off));
+  return uni(v);
+}
+#define wred wred_shfl
+#endif
+__device__ __forceinline__ double wsum(double v) {
+  return wred(v, [](double x, double y) { return x + y; });
 }
 __device__ __forceinline__ double wmaxd(double v) {
-  UNR for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-  return uni(v);
+  return wred(v, [](double x, double y) { return fmax(x, y); });
 }
 __device__ __forceinline__ double wmind(double v) {
-  UNR for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off));
-  return uni(v);
+  return wred(v, [](double x, double y) { return fmin(x, y); });
 }
 
 // Ordering point inside a recursion.  A k_wave workgroup is ONE wave and the LDS executes a wave's DS
@@ -240,6 +288,7 @@ __device__ unsigned g_dbg_cnt;
 #ifndef VBOC_REPEAT
 #define VBOC_REPEAT 0
 #endif
+
 #define VREP(id, stmt) do { stmt; if constexpr (VBOC_REPEAT == (id)) { stmt; } } while (0)
 
 // HC: the Cartesian path-constraint rows (vboc_set_path_constraint; oracle/vboc_oracle.c hc_*, Lane::hc_*) on
@@ -323,6 +372,11 @@ struct Coop {
   __device__ __forceinline__ void dma(int k, int lo, int W, int dst, int part) const {
     const int nc = W / 2;
     const int c = part * 64 + t < nc ? part * 64 + t : nc - 1;
+#ifndef VBOC_SBASE_DMA
+    // per-lane 64-bit addresses.  The SGPR-base form (dma_s, -DVBOC_SBASE_DMA) gives the pendulum chains the same
+    // bits, but deterministically broke the UR5 instantiation (k_wave<4>: 24 % status agreement with the oracle,
+    // tools/ur5_bisect.sh, profiles/r03z_ur5_sgpr_base_dma_bisect.log) for a reason not found; the grouped
+    // recursions (nq <= 3) keep dma_s
     const gdouble* src = g + (long long)k * REC + lo + 2 * c;
     const unsigned lds = lds0 + 8u * (unsigned)(dst + part * 128);
     unsigned keep;
@@ -330,6 +384,9 @@ struct Coop {
                  : "=&s"(keep)
                  : "v"(src), "s"(lds)
                  : "memory");
+#else
+    dma_s(g + (long long)k * REC, 8u * (unsigned)(lo + 2 * c), dst + part * 128);
+#endif
   }
   // the same with a wave-uniform base (SGPR pair) and a per-lane byte offset: no per-lane 64-bit address
   // arithmetic in the recursions' loops (the lane offsets are computed once per pass)
@@ -339,8 +396,10 @@ struct Coop {
     const unsigned long long b = (unsigned long long)(size_t)base;
     const unsigned long long bs = ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32)) << 32) |
                                   (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
+    // s_nop 4: an "s" operand fresh from readfirstlane / v_readlane, read by a VMEM instruction as its base, needs
+    // 5 wait states that hipcc does not insert in front of inline asm (cdna_hip_programming.md, inline asm rules)
     unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(voff), "s"(bs), "s"(lds)
                  : "memory");
