@@ -63,6 +63,7 @@ struct DgJobs {
   const int* cancel;
   // speculative restarts (see "Speculative restarts" below); spec_events == 0 switches them off
   int spec_events, spec_stride;   // events in the pool, doubles per event
+  int spec_early;                 // once at most this many problems are left unclaimed, queued restart jobs go first
   double* spec;                   // [spec_events][spec_stride]: snapshot header, then DG_SPEC_JOBS results
   int* spec_claim;                // [spec_events][DG_SPEC_JOBS + 1]: 0 free, 1 claimed
   int* spec_done;                 // [spec_events][DG_SPEC_JOBS + 1]: 1 = result written
@@ -876,8 +877,20 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
   const bool spec = J->spec_events > 0;
   for (;;) {
     int mode = 0, idx = 0, ev = 0, jj = 0, code = 0;
+    // 0. near the end of the problem queue (spec_early), a queued restart job of a running chain goes before a new
+    //    problem: the chains that make the launch tail start getting help before the last problems are handed out
+    int pre = 0;
+    if (spec && J->spec_early > 0) {
+      if (t == 0) {
+        const unsigned nx = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (nx < (unsigned)count && nx + (unsigned)J->spec_early >= (unsigned)count)
+          pre = __hip_atomic_load(J->spec_q_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                __hip_atomic_load(J->spec_q_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      pre = dg_bcast(pre);
+    }
     // 1. the next problem
-    {
+    if (!pre) {
       int got = -1;
       if (t == 0 && __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)count) {
         const unsigned i = atomicAdd(jb.next, 1u);
@@ -928,6 +941,7 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
       }
     }
     // 3. nothing to do: leave once every problem is finished, else wait for restart jobs
+    if (mode == 0 && pre) continue;   // the restart job went to another wave: back to the problem queue
     if (mode == 0) {
       int fin = 0;
       if (t == 0) fin = __hip_atomic_load(J->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)count;

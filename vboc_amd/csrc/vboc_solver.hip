@@ -1511,6 +1511,7 @@ struct vboc_solver {
   bool dg_attr[4] = {false, false, false, false};
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
+  int dg_spec_early = 0;            // restart jobs before new problems once this few problems are left (0: only after)
   double* wave_hc = nullptr;        // path-constraint rows of the wave solver, one region per workgroup
   long long wave_hc_doubles = 0;
   bool hc_wave = true;              // constrained problems on the wave solver (k_wave<NQ, false, true>)
@@ -1853,6 +1854,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "mall_mib") h->mall_mib = v;
   else if (s == "dg_fail_mod") h->dg_fail_mod = (int)v;
   else if (s == "dg_speculate") h->dg_speculate = v != 0.0;
+  else if (s == "dg_spec_early") h->dg_spec_early = v > 0.0 ? (int)v : 0;
   else if (s == "hc_wave") h->hc_wave = v != 0.0;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
@@ -1888,6 +1890,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "coop_available") *v = h->coop_ok ? 1.0 : 0.0;
   else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
   else if (s == "dg_speculate") *v = h->dg_speculate ? 1.0 : 0.0;
+  else if (s == "dg_spec_early") *v = (double)h->dg_spec_early;
   else if (s == "hc_wave") *v = h->hc_wave ? 1.0 : 0.0;
   else if (s == "factor_mfma") *v = h->factor_mfma ? 1.0 : 0.0;
   else if (s == "wave_groups") *v = (double)h->n_regions;
@@ -2265,7 +2268,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   J.spec_ev_next = h->head + 6; J.spec_q_tail = h->head + 7; J.spec_q_head = h->head + 8;
   J.spec_count = (unsigned long long*)(h->head + 10);
   // speculative restarts: one event per failed horizon-extension chain, at most min(B, 8192) per launch
-  J.spec_events = 0; J.spec_stride = 0; J.spec = nullptr;
+  J.spec_events = 0; J.spec_stride = 0; J.spec = nullptr; J.spec_early = h->dg_spec_early;
   J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = nullptr;
   size_t spec_ctl = 0;
   if (h->dg_speculate && !testing) {
