@@ -430,14 +430,17 @@ struct Coop {
     const dbl2* src = (const dbl2*)(s + fslot(slot));
     gdbl2* dst = (gdbl2*)(g + (long long)k * REC);
 #ifndef VBOC_WB_MASKED
-    // every lane stores (lanes past the field range repeat the last chunk: same bytes, same address), no exec mask:
-    // 16k first solves 4 082 -> 3 949 ms on one box, same results (profiles/r03z_wb_ab.json)
-    constexpr int NCH = (HI - LO) / 2;
-    const int c = t < NCH ? t : NCH - 1;
-    dst[LO / 2 + c] = src[LO / 2 + c];
-#else
-    if (t < (HI - LO) / 2) dst[LO / 2 + t] = src[LO / 2 + t];
+    if constexpr (NQ <= 3) {
+      // every lane stores (lanes past the field range repeat the last chunk: same bytes, same address), no exec
+      // mask: 16k first solves 4 082 -> 3 949 ms on one box, same results (profiles/r03z_wb_ab.json).  The arm
+      // keeps the masked store: its k_wave<4> lost parity with the unmasked one
+      constexpr int NCH = (HI - LO) / 2;
+      const int c = t < NCH ? t : NCH - 1;
+      dst[LO / 2 + c] = src[LO / 2 + c];
+      return;
+    }
 #endif
+    if (t < (HI - LO) / 2) dst[LO / 2 + t] = src[LO / 2 + t];
   }
 
   // debug (-DVBOC_DBG_CHECK): compare a landed ring window with a direct global read of the same fields
