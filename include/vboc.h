@@ -180,7 +180,9 @@ int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const dou
  * Speculative restarts (solver option "dg_speculate", default 1): when a horizon-extension solve fails, the
  * inputs of the problem's later attempts (perturbed restarts, up to 10 attempts) are known in advance, so
  * other waves solve them in parallel and the problem takes the results in order; results are identical to
- * the sequential chain.  Only solves the problem consumes count in stats. */
+ * the sequential chain.  Only solves the problem consumes count in stats.  They run on waves the problem queue
+ * no longer feeds; solver option "dg_spec_early" = n (default 0) lets queued restart jobs go before new problems
+ * once at most n problems are left (measured: no gain at n = 5 % of the queue, -10 % when always on). */
 typedef struct {
   int B;
   const long long* ids;
