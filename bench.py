@@ -145,6 +145,8 @@ class GpuEngine:
         self.solver.set_option("factor_mfma", 1 if args.factor == "mfma" else 0)
         self.solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
         self.solver.set_option("dg_spec_early", getattr(args, "spec_early", 0))
+        if getattr(args, "spec_min_ext", 0):   # measurement builds only (tools/spec_early_ab.sh, VBOC_LIB variant)
+            self.solver.set_option("dg_spec_min_ext", args.spec_min_ext)
         self.stream = torch.cuda.current_stream(self.device)
         self.kernel = {("dg-loop", "wave"): f"k_dg<{nq}>", ("first-solve", "wave"): f"k_wave<{nq}>",
                        ("first-solve", "lane"): f"k_qp_factor<{nq}>"}[(args.workload, args.mode)]
@@ -229,6 +231,8 @@ def parse(argv=None):
     ap.add_argument("--spec-early", type=int, default=0,
                     help="dg-loop: queued speculative restarts go before new problems once this few problems are left "
                          "(0: only once the problem queue is drained)")
+    ap.add_argument("--spec-min-ext", type=int, default=0,
+                    help="dg-loop: a failed horizon-extension chain publishes speculative restarts only from this solve on")
     ap.add_argument("--mode", choices=("wave", "lane"), default="wave",
                     help="first-solve: wave (one problem per wave, default) or lane (lane-per-problem kernels)")
     args = ap.parse_args(argv)

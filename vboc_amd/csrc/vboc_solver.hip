@@ -1512,6 +1512,7 @@ struct vboc_solver {
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
   int dg_spec_early = 0;            // restart jobs before new problems once this few problems are left (0: only after)
+  int dg_spec_min_ext = 0;          // (-DVBOC_SPEC_MIN_EXT builds) restart jobs only from this extension solve on
   double* wave_hc = nullptr;        // path-constraint rows of the wave solver, one region per workgroup
   long long wave_hc_doubles = 0;
   bool hc_wave = true;              // constrained problems on the wave solver (k_wave<NQ, false, true>)
@@ -1855,6 +1856,9 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "dg_fail_mod") h->dg_fail_mod = (int)v;
   else if (s == "dg_speculate") h->dg_speculate = v != 0.0;
   else if (s == "dg_spec_early") h->dg_spec_early = v > 0.0 ? (int)v : 0;
+#ifdef VBOC_SPEC_MIN_EXT
+  else if (s == "dg_spec_min_ext") h->dg_spec_min_ext = v > 0.0 ? (int)v : 0;
+#endif
   else if (s == "hc_wave") h->hc_wave = v != 0.0;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
@@ -2269,6 +2273,9 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   J.spec_count = (unsigned long long*)(h->head + 10);
   // speculative restarts: one event per failed horizon-extension chain, at most min(B, 8192) per launch
   J.spec_events = 0; J.spec_stride = 0; J.spec = nullptr; J.spec_early = h->dg_spec_early;
+#ifdef VBOC_SPEC_MIN_EXT
+  J.spec_min_ext = h->dg_spec_min_ext;
+#endif
   J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = nullptr;
   size_t spec_ctl = 0;
   if (h->dg_speculate && !testing) {
