@@ -38,11 +38,20 @@ Output: ONE JSON line on rank 0 (contract in the task statement), with
                workload on the host's cores, rank 0, N = 1 only.
 `run(args, engine_factory)` takes another engine (tests/test_distributed.py runs the N = 2 path on gloo with
 the oracle as the engine).
+
+Ranks: launched by torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK in the environment) every process is one
+rank.  `python bench.py --gpus N` with no launcher environment starts the N rank processes itself (children of this
+process, started before anything here touches the GPU; rank r on GPU r, rendezvous on 127.0.0.1) and exits with
+their status - the reference's own fan-out is one command too (`Pool(30).map`, VBOC/triplependulum_vboc.py:399-405).
+Every rank checks that the process group's size equals --gpus, and `n_gpus` is the process group's size.
 """
 import argparse
+import hashlib
 import json
 import os
+import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -145,6 +154,8 @@ class GpuEngine:
         self.solver.set_option("factor_mfma", 1 if args.factor == "mfma" else 0)
         self.solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
         self.solver.set_option("dg_spec_early", getattr(args, "spec_early", 0))
+        if getattr(args, "wave_groups", 0):   # resident problems (default: sized to the 256 MiB MALL)
+            self.solver.set_option("wave_groups", args.wave_groups)
         if getattr(args, "spec_min_ext", 0):   # measurement builds only (tools/spec_early_ab.sh, VBOC_LIB variant)
             self.solver.set_option("dg_spec_min_ext", args.spec_min_ext)
         self.stream = torch.cuda.current_stream(self.device)
@@ -170,6 +181,14 @@ class GpuEngine:
 
     def lane_stats(self):
         return self.solver.kernel_stats()
+
+    def library(self):
+        """Which solver build was timed: its path (VBOC_LIB may select a measurement variant) and sha1."""
+        path = self.lib.LIB_PATH
+        with open(path, "rb") as f:
+            digest = hashlib.sha1(f.read()).hexdigest()
+        return {"path": os.path.relpath(path, ROOT), "sha1": digest,
+                "variant": bool(os.environ.get("VBOC_LIB")), "resident_problems": int(self.solver.get_option("wave_groups"))}
 
 
 def cpu_baseline(nq, workload, B, seconds, threads):
@@ -235,6 +254,14 @@ def parse(argv=None):
                     help="dg-loop: a failed horizon-extension chain publishes speculative restarts only from this solve on")
     ap.add_argument("--mode", choices=("wave", "lane"), default="wave",
                     help="first-solve: wave (one problem per wave, default) or lane (lane-per-problem kernels)")
+    ap.add_argument("--wave-groups", type=int, default=0,
+                    help="resident problems (persistent workgroups) of the wave solver / data-generation launch "
+                         "(0: sized so their hot stage records fit the 256 MiB MALL)")
+    ap.add_argument("--progress", type=float, default=0.0,
+                    help="print an elapsed-time line to stderr every this many seconds (long runs under a watchdog)")
+    ap.add_argument("--engine", default="gpu",
+                    help="'gpu' (the product: libvboc_amd) or module:Class of a test engine with GpuEngine's interface "
+                         "(CPU tests of the rank launcher only; such a line carries engine = that name)")
     args = ap.parse_args(argv)
     if args.batch is None:
         args.batch = 20_000 if args.workload == "dg-loop" else 100_000
@@ -253,11 +280,20 @@ def run(args, engine_factory=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     nq, B = args.nq, args.batch
+    if engine_factory is None and args.engine != "gpu":
+        import importlib
+        mod, cls = args.engine.split(":")
+        engine_factory = getattr(importlib.import_module(mod), cls)
     engine = (engine_factory or GpuEngine)(nq, args, local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl" if engine.device.type == "cuda" else "gloo", rank=rank, world_size=world)
+        world = dist.get_world_size()
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {world} rank(s) "
+                         f"(launch with torch.distributed.run --nproc-per-node {args.gpus}, or without a launcher)")
     dev = engine.device
+    beat = _progress(args.progress, rank)
     dgl = args.workload == "dg-loop"
 
     # first-solve inputs: `max_batches` distinct batches generated and copied to HBM before any timing
@@ -405,6 +441,8 @@ def run(args, engine_factory=None):
                 "note": "last timed launch, device real-time clock from the first problem's start"}
     sqp = np.concatenate(rec["sqp"]) if rec["sqp"] else np.zeros(1)
     ok = np.concatenate(rec["status"]) if rec["status"] else np.zeros(1)
+    if beat is not None:
+        beat.set()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -431,6 +469,7 @@ def run(args, engine_factory=None):
         "path_fp64": {"achieved": round(flops / elapsed / 1e12, 4), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                       "frac": round(flops / elapsed / 1e12 / FP64_PEAK_TFLOPS, 5)},
         "cpu_baseline": cpu,
+        "library": engine.library() if hasattr(engine, "library") else {"engine": args.engine},
         "solver": {"ok_frac": round(float(np.mean(ok)), 4), "sqp_iter_mean": round(float(sqp.mean()), 1),
                    "sqp_iter_max": round(float(sqp.max()), 1)},
     }
@@ -465,8 +504,55 @@ def run(args, engine_factory=None):
     return line
 
 
+def _progress(period, rank):
+    """A daemon thread printing the elapsed time to stderr every `period` s (0: none); set() the returned event
+    to stop it."""
+    if not period or period <= 0:
+        return None
+    stop, t0 = threading.Event(), time.time()
+
+    def beat():
+        while not stop.wait(period):
+            print(f"bench rank {rank}: {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+    return stop
+
+
+def spawn_ranks(argv, n):
+    """`bench.py --gpus n` without a launcher: n child processes of this one, rank r on GPU r (LOCAL_RANK), one
+    rendezvous on 127.0.0.1 (a free port).  Nothing in this process touches the GPU.  Rank 0 prints the line; a
+    failing rank ends the others.  Returns the exit status (the first non-zero one)."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code   # killed by a signal: the shell's convention
+                for q in live:        # our own children, by PID
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main(argv=None):
-    line = run(parse(argv))
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(argv, args.gpus))
+    line = run(args)
     if line is not None:
         print(json.dumps(line), flush=True)
 

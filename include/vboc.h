@@ -207,7 +207,9 @@ int vboc_data_generation(vboc_handle h, vboc_dg_batch_t* batch, void* stream);
  * another stream may read that problem's results while the launch runs; cancel (a device int, may be NULL),
  * set by the caller while the launch runs, makes the problems not yet started return at once with
  * row_cnt -3.  vboc_data_generation_wait ends the launch (synchronises `stream`, fills rows_used and the
- * speculation counts, reports pool overflow).  No other call may use the handle in between.
+ * speculation counts, reports pool overflow).  No other call may use the handle in between: the solve, testing,
+ * data-generation, HJR and option entry points return VBOC_ERR_ARG on a handle with an un-waited launch, and
+ * vboc_destroy synchronises the device before it frees the launch's buffers.
  * Replaces the reference's synchronous Pool(30).map per VBOC iteration (VBOC/triplependulum_vboc.py:493-506)
  * by one producer over every iteration's problems. */
 int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* batch, int* done_flag, const int* cancel,

@@ -161,3 +161,35 @@ def test_bench_runs_at_world_two_on_gloo(tmp_path, workload):
         assert abs(line["value"] - solves / (line["ms_per_step"] * steps / 1e3)) < 0.01 * line["value"] + 0.01
     else:
         assert abs(line["value"] - 2 * steps * B / (line["ms_per_step"] * steps / 1e3)) < 0.01 * line["value"] + 0.01
+
+
+def test_bench_gpus_two_starts_two_ranks_without_a_launcher(tmp_path):
+    """`python bench.py --gpus 2` with no torch.distributed.run environment starts the two rank processes itself
+    (the driver's N-GPU command), and the line's n_gpus is the process group's size.  The oracle engine stands
+    in for the GPU (--engine, a test hook); everything else is the product's launcher and step loop."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["PYTHONPATH"] = os.pathsep.join([os.path.dirname(os.path.abspath(__file__)), ROOT])
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "dg-loop", "--nq", "2",
+           "--batch", "2", "--steps", "1", "--warmup", "1", "--no-cpu", "--engine", "test_distributed:OracleEngine"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 prints the only line
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "dp2"
+    assert line["library"] == {"engine": "test_distributed:OracleEngine"}
+    assert line["value"] > 0 and line["loop"]["samples"] >= 0
+
+
+def test_bench_refuses_a_world_that_differs_from_gpus():
+    """A single process asked for --gpus 2 under a launcher environment of world size 1 exits non-zero instead
+    of printing a one-rank line labelled as two."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0",
+               PYTHONPATH=os.pathsep.join([os.path.dirname(os.path.abspath(__file__)), ROOT]))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "first-solve", "--nq", "2",
+           "--batch", "2", "--steps", "1", "--warmup", "0", "--no-cpu", "--engine", "test_distributed:OracleEngine"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "process group has 1 rank" in r.stderr

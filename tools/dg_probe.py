@@ -1,0 +1,71 @@
+"""One data-generation launch (k_dg, the bench's dominant kernel) on a fixed id range, for driver-shape A/Bs.
+
+The bench's timed launch is 400k problems; its rate is the bulk rate (every resident wave busy) plus one tail
+(the slowest problem after the queue drains).  This probe reports both for a launch of B problems:
+  kernel_ms     the whole launch (HIP events)
+  bulk          solves per second while the queue still feeds every wave: solves of the problems that ended
+                inside [t_first + 5 % of the drain time, queue drained] / that window (device real-time clock)
+  drained_ms    when the last problem started; last_ms when the last one finished
+  digest        sha1 of the per-problem rows / counts / solve statistics (variants that claim the same results
+                must reproduce the product's digest)
+Run once per library (VBOC_LIB=<variant .so>) and resident-problem count (--groups).
+usage: python tools/dg_probe.py [--nq 3] [--B 100000] [--groups 0 ...] [--first 0]
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from bench import dg_flops, order_rows
+    from vboc_amd import lib
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nq", type=int, default=3)
+    ap.add_argument("--B", type=int, default=100_000)
+    ap.add_argument("--first", type=int, default=0)
+    ap.add_argument("--groups", type=int, nargs="*", default=[0])
+    a = ap.parse_args()
+    s = lib.Solver(a.nq, 120, device=0)
+    ids = torch.arange(a.first, a.first + a.B, dtype=torch.int64, device="cuda:0")
+    for g in a.groups:
+        s.set_option("wave_groups", g)
+        t = time.time()
+        out = s.data_generation_device(ids)
+        torch.cuda.synchronize()
+        wall = time.time() - t
+        ms, _ = s.last_kernel_ms()
+        st = out["stats"].cpu().numpy()
+        t0, t1 = st[:, 5], st[:, 6]
+        base = t0.min()
+        drained = t0.max() - base
+        lo = base + 0.05 * drained
+        hi = base + drained
+        inwin = (t1 >= lo) & (t1 <= hi)
+        bulk = float(st[inwin, 0].sum()) / ((hi - lo) / lib.DG_CLOCK_HZ) if hi > lo else None
+        h = hashlib.sha1()
+        h.update(order_rows(out).cpu().numpy().tobytes())
+        h.update(out["row_cnt"].cpu().numpy().tobytes())
+        h.update(st[:, [0, 1, 2, 3, 4, 7, 8]].tobytes())
+        rec = {"lib": os.path.basename(os.environ.get("VBOC_LIB") or "libvboc_amd.so"), "nq": a.nq, "B": a.B,
+               "groups": int(s.get_option("last_groups")), "kernel_ms": round(ms, 1), "wall_s": round(wall, 2),
+               "solves": int(st[:, 0].sum()), "solves_per_s": round(float(st[:, 0].sum()) / (ms / 1e3), 1),
+               "bulk_solves_per_s": round(bulk, 1) if bulk else None,
+               "drained_ms": round(drained / lib.DG_CLOCK_HZ * 1e3, 1),
+               "last_ms": round((t1.max() - base) / lib.DG_CLOCK_HZ * 1e3, 1),
+               "stage_ipm_iters_per_s": round(float(st[:, 4].sum()) / (ms / 1e3), 1),
+               "tflops": round(dg_flops(a.nq, st) / (ms / 1e3) / 1e12, 4),
+               "digest": h.hexdigest()}
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -49,6 +49,12 @@ typedef __attribute__((address_space(1))) void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
 
 __host__ __device__ constexpr int even_up(int v) { return (v + 1) & ~1; }
+// stage-record stride: VBOC_REC_ALIGN doubles (2 = 16 B, the product; 16 = 128-B L2 lines: every stage record then
+// starts on a line, measurement builds)
+#ifndef VBOC_REC_ALIGN
+#define VBOC_REC_ALIGN 2
+#endif
+__host__ __device__ constexpr int rec_up(int v) { return (v + VBOC_REC_ALIGN - 1) / VBOC_REC_ALIGN * VBOC_REC_ALIGN; }
 
 template <int NQ>
 struct WaveLayout {
@@ -60,7 +66,7 @@ struct WaveLayout {
                        OE = OQU + NZ, OD = OE + NX, ODA = OD + NZ, OK = ODA + NZ, OKF = OK + NU * NX,
                        OLR = OKF + NU, OM = OLR + NU * NU, OY = OM + NU * NQ, OPE = OY + NU * NQ, OC = OPE + NX,
                        OACL = OC + NX, OX = OACL + NX * NX, OU = OX + NX, OPI = OU + NU, OLL = OPI + NX,
-                       OLU = OLL + NZ, OWPI = OLU + NZ, REC = even_up(OWPI + NX);
+                       OLU = OLL + NZ, OWPI = OLU + NZ, REC = rec_up(OWPI + NX);
   // OC: per-pass constant of the vector / forward recursion; OACL: closed-loop A + B K (row-major)
   // ring windows [lo, lo + W): factor [0, OC) (writes back [OK, OC)); vector pass [OPE, OX);
   // forward sweep [OC, OX); costate [0, OE)

@@ -1518,6 +1518,10 @@ struct vboc_solver {
   bool hc_wave = true;              // constrained problems on the wave solver (k_wave<NQ, false, true>)
   void* dg_spec = nullptr;          // their pool (events, results, control words, queue)
   size_t dg_spec_bytes = 0;
+  // a vboc_data_generation_async launch is running on this handle's buffers (dg_scratch, regions, head counters)
+  // until vboc_data_generation_wait: every other entry point that would reuse them refuses (VBOC_ERR_ARG)
+  bool dg_busy = false;
+  long long last_groups = 0;        // resident problems (workgroups) of the last wave-solver / data-generation launch
 };
 
 static void default_opts(Opts& o) {
@@ -1643,6 +1647,7 @@ static hipError_t launch_wave(vboc_solver* h, const WaveJobs& jb, long long jobs
   const long long cap = h->group_cap > 0 ? h->group_cap : (h->mall_mib > 0 ? wave_group_budget(h, in.nmax) : 0);
   if (cap > 0 && groups > cap) groups = cap;
   if (groups < 1) return hipSuccess;
+  h->last_groups = groups;
   const dim3 grid((unsigned)groups), block(64);
   switch (h->nq) {
     case 1:
@@ -1706,6 +1711,14 @@ static hipError_t launch_tt(vboc_solver* h, const TtJobs& J, const Inputs& in, l
   hipLaunchKernelGGL((k_tt<NQ, FM, HC>), dim3((unsigned)groups), dim3(64), h->wave_lds, st, h->w, h->o, in,
                      (const Inputs*)h->dg_in, (const TtJobs*)h->tt_jobs, jb);
   return hipGetLastError();
+}
+
+// an entry point that would reuse the handle's buffers while an async data-generation launch runs on them
+static bool busy(const vboc_solver* h, const char* who) {
+  if (!h || !h->dg_busy) return false;
+  fail(VBOC_ERR_ARG, std::string(who) + ": a vboc_data_generation_async launch is still running on this handle "
+                                        "(call vboc_data_generation_wait first)");
+  return true;
 }
 
 extern "C" {
@@ -1805,6 +1818,7 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
 int vboc_destroy(vboc_handle h) {
   if (!h) return VBOC_OK;
   (void)hipSetDevice(h->device);
+  if (h->dg_busy) (void)hipDeviceSynchronize();   // an un-waited async launch still uses the buffers freed below
   if (h->pool) (void)hipFree(h->pool);
   if (h->head) (void)hipFree(h->head);
   if (h->ist) (void)hipFree(h->ist);
@@ -1828,6 +1842,7 @@ int vboc_destroy(vboc_handle h) {
 }
 
 int vboc_set_option(vboc_handle h, const char* f, double v) {
+  if (busy(h, "vboc_set_option")) return VBOC_ERR_ARG;
   if (!h || !f) return fail(VBOC_ERR_ARG, "vboc_set_option: NULL argument");
   Opts& o = h->o;
   const std::string s(f);
@@ -1898,6 +1913,8 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "hc_wave") *v = h->hc_wave ? 1.0 : 0.0;
   else if (s == "factor_mfma") *v = h->factor_mfma ? 1.0 : 0.0;
   else if (s == "wave_groups") *v = (double)h->n_regions;
+  else if (s == "last_groups") *v = (double)h->last_groups;
+  else if (s == "dg_busy") *v = h->dg_busy ? 1.0 : 0.0;
   else if (s == "mall_mib") *v = h->mall_mib;
   else if (s == "coop_problems") *v = (double)h->coop_count;
   else if (s == "slots") *v = (double)h->slots;
@@ -1907,6 +1924,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
 }
 
 int vboc_set_path_constraint(vboc_handle h, int kind, double x_c, double y_c, double lh, double uh) {
+  if (busy(h, "vboc_set_path_constraint")) return VBOC_ERR_ARG;
   if (!h) return fail(VBOC_ERR_ARG, "vboc_set_path_constraint: NULL handle");
   if (kind == 0) { h->o.hc = 0; return VBOC_OK; }
   if (kind != 1) return fail(VBOC_ERR_ARG, "vboc_set_path_constraint: unknown kind");
@@ -1938,6 +1956,7 @@ int vboc_set_path_constraint(vboc_handle h, int kind, double x_c, double y_c, do
 }
 
 int vboc_solve_batch(vboc_handle h, const vboc_batch_t* b, void* stream) {
+  if (busy(h, "vboc_solve_batch")) return VBOC_ERR_ARG;
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_solve_batch: NULL argument");
   if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_solve_batch: B < 0");
   if (b->nmax > h->nmax || b->nmax < 1)
@@ -2080,6 +2099,7 @@ int vboc_kernel_stats(vboc_handle h, double* factor_ms, long long* factor_launch
 }
 
 int vboc_solve_batch_ft(vboc_handle h, const vboc_batch_t* b, void* stream) {
+  if (busy(h, "vboc_solve_batch_ft")) return VBOC_ERR_ARG;
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: NULL argument");
   if (h->o.hc) return fail(VBOC_ERR_UNSUPPORTED, "vboc_solve_batch_ft: no path constraint in the free-time OCP");
   if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_solve_batch_ft: B < 0");
@@ -2192,6 +2212,7 @@ int vboc_data_generation_wait(vboc_handle h, vboc_dg_batch_t* b, void* stream) {
 static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const int* cancel, hipStream_t st,
                       bool testing, int max_restarts, const char* who) {
   const std::string W(who);
+  if (busy(h, who)) return VBOC_ERR_ARG;
   if (h->nq != 2 && h->nq != 3)
     return fail(VBOC_ERR_UNSUPPORTED, W + ": defined for the double (nq = 2) and triple (nq = 3) pendulum");
   if (h->o.hc)
@@ -2214,6 +2235,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   const long long cap = h->group_cap > 0 ? h->group_cap
                                          : (h->mall_mib > 0 ? wave_group_budget(h, b->N_start + 10) : 0);
   if (cap > 0 && groups > cap) groups = cap;
+  h->last_groups = groups;
   // per-workgroup arrays: the solver's one-problem batch (Inputs layout) + x_sol, u_sol, saved rows, state
   const int nq = h->nq, NXR = 2 * nq + 1, NU = nq, NP = nq + 1, NX = 2 * nq, nm = h->nmax;
   const int vr_cap = 2 * nm + 2;
@@ -2317,7 +2339,9 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
 
 int vboc_data_generation_async(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const int* cancel, void* stream) {
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_data_generation: NULL argument");
-  return dg_prepare(h, b, done_flag, cancel, (hipStream_t)stream, false, 0, "vboc_data_generation");
+  const int rc = dg_prepare(h, b, done_flag, cancel, (hipStream_t)stream, false, 0, "vboc_data_generation");
+  if (rc == VBOC_OK && b->B > 0) h->dg_busy = true;
+  return rc;
 }
 
 int vboc_testing(vboc_handle h, vboc_dg_batch_t* b, int max_restarts, void* stream) {
@@ -2328,6 +2352,7 @@ int vboc_testing(vboc_handle h, vboc_dg_batch_t* b, int max_restarts, void* stre
 }
 
 int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream) {
+  if (busy(h, "vboc_testing_test")) return VBOC_ERR_ARG;
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_testing_test: NULL argument");
   const bool cart = h->nq == 2 && h->o.hc, arm = h->nq == 4;
   if (!cart && !arm)
@@ -2345,6 +2370,7 @@ int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream) {
   long long groups = b->B < h->n_regions ? b->B : h->n_regions;
   const long long cap = h->group_cap > 0 ? h->group_cap : (h->mall_mib > 0 ? wave_group_budget(h, b->N_start + 10) : 0);
   if (cap > 0 && groups > cap) groups = cap;
+  h->last_groups = groups;
   const int nq = h->nq, NXR = 2 * nq + 1, NU = nq, NP = nq + 1, nm = h->nmax;
   const int st_d = (int)((sizeof(TtState<4>) + 15) / 16 * 2);
   const size_t G = (size_t)groups;
@@ -2395,6 +2421,7 @@ int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream) {
   h->coop_count = b->B;
   HIPCHK(hipMemcpyAsync(h->host_done, h->head, 14 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  h->dg_busy = false;
   const unsigned* c = h->host_done;
   if (c[3]) return fail(VBOC_ERR_ARG, "vboc_testing_test: a horizon passed the handle's nmax");
   if (c[1] != (unsigned)b->B) return fail(VBOC_ERR_HIP, "vboc_testing_test: not every problem finished");
@@ -2417,6 +2444,7 @@ static int dg_wait(vboc_handle h, vboc_dg_batch_t* b, hipStream_t st) {
 }
 
 int vboc_hjr_solve_batch(vboc_handle h, const vboc_hjr_batch_t* b, void* stream) {
+  if (busy(h, "vboc_hjr_solve_batch")) return VBOC_ERR_ARG;
   if (!h || !b) return fail(VBOC_ERR_ARG, "vboc_hjr_solve_batch: NULL argument");
   if (h->nq > 3) return fail(VBOC_ERR_UNSUPPORTED, "vboc_hjr_solve_batch: defined for the pendulum chains (nq 1-3)");
   if (b->B < 0) return fail(VBOC_ERR_ARG, "vboc_hjr_solve_batch: B < 0");
