@@ -193,3 +193,77 @@ def test_bench_refuses_a_world_that_differs_from_gpus():
            "--batch", "2", "--steps", "1", "--warmup", "0", "--no-cpu", "--engine", "test_distributed:OracleEngine"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode != 0 and "process group has 1 rank" in r.stderr
+
+
+# ------------------------------------------------------------------------------------------------
+# the VBOC loop (streamed segments) and the UR5 / Cartesian main blocks at world size 2 on gloo
+# ------------------------------------------------------------------------------------------------
+class _RankSegment:
+    """A streamed segment whose round r is this rank's shard of iteration first + r (pipeline._rank_ids, what the
+    product's StreamedRounds launches), solved by the host driver on the oracle."""
+
+    def __init__(self, first, n, nq, num_prob):
+        self.first, self.n, self.nq, self.num_prob = first, n, nq, num_prob
+
+    def round(self, r):
+        from oracle_backend import OracleBackend
+        from vboc_amd.pipeline import _generate, _rank_ids
+        return _generate(self.nq, OracleBackend(self.nq), _rank_ids(self.first + r, self.num_prob), None, 20250124)
+
+    def cancel(self):
+        pass
+
+    def close(self):
+        return dict(seconds=0.0, spec_solves=0, spec_used=0, waited_s=0.0)
+
+
+def _main_blocks_worker(rank, world, port, out_dir):
+    import pickle
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle_backend import OracleBackend
+    from vboc_amd.pipeline import cartesian_run, ur5_run, vboc_run
+    from vboc_amd.systems import cartesian_constraint
+    X_test = np.tile([np.pi, np.pi, 1.0, 1.0], (4, 1))
+    loop = vboc_run(2, OracleBackend(2), X_test, stop_time=1e9, num_prob=5, max_iterations=2, stream_rounds=2,
+                    segment_factory=lambda f, k: _RankSegment(f, k, 2, 5),
+                    trainer_kw=dict(hidden=8, minibatch=16, stop_val=1e9))
+    u = ur5_run(OracleBackend(4), num_test=5, num_train=7, device="cpu", minibatch=8, hidden=16)
+    c = cartesian_run(OracleBackend(2, path_constraint=cartesian_constraint()), num_test=3, num_train=5,
+                      device="cpu", minibatch=8, hidden=16)
+    res = dict(loop=loop["X_save"], loop_rmse=loop["rmse"], ur5_test=u["X_test"], ur5_train=u["X_train"],
+               ur5_fit=u["fit"], cart_test=c["X_test"], cart_train=c["X_train"], cart_fit=c["fit"])
+    with open(os.path.join(out_dir, f"rank{rank}.pkl"), "wb") as f:
+        pickle.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_main_blocks_at_world_two_equal_one_process(tmp_path):
+    """configs[3] / config 4's sharding on gloo: the streamed VBOC loop (each rank streams its shard of every
+    iteration, the samples all-gathered per iteration), ur5_run and cartesian_run (each rank one contiguous share
+    of the test and training ids, rows all-gathered) give every rank the single-process rows in problem order;
+    only rank 0 fits."""
+    import pickle
+    import torch.multiprocessing as mp
+    from oracle_backend import OracleBackend
+    from vboc_amd.pipeline import _generate, cartesian_run, samples_array, ur5_run
+    from vboc_amd.systems import cartesian_constraint
+    mp.spawn(_main_blocks_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = [pickle.load(open(tmp_path / f"rank{r}.pkl", "rb")) for r in range(2)]
+    loop_ref = np.concatenate([samples_array(2, _generate(2, OracleBackend(2), np.arange(i * 5, (i + 1) * 5), None,
+                                                           20250124)[0]) for i in range(3)])
+    u = ur5_run(OracleBackend(4), num_test=5, num_train=7, device="cpu", minibatch=8, hidden=16)
+    c = cartesian_run(OracleBackend(2, path_constraint=cartesian_constraint()), num_test=3, num_train=5,
+                      device="cpu", minibatch=8, hidden=16)
+    for r in (r0, r1):
+        np.testing.assert_array_equal(r["loop"], loop_ref)
+        np.testing.assert_array_equal(r["ur5_test"], u["X_test"])
+        np.testing.assert_array_equal(r["ur5_train"], u["X_train"])
+        np.testing.assert_array_equal(r["cart_test"], c["X_test"])
+        np.testing.assert_array_equal(r["cart_train"], c["X_train"])
+    assert len(r0["loop_rmse"]) == 3 and r1["loop_rmse"] == []
+    assert r0["ur5_fit"] is not None and r1["ur5_fit"] is None and r1["cart_fit"] is None

@@ -250,3 +250,62 @@ def test_large_refit_with_graphs_on_gpu():
     assert r["iterations"] == 255 and np.isfinite(r["val"])
     idx = tr._sample(n // 2, n, 2048)
     assert idx.min().item() >= n // 2 and idx.max().item() < n and torch.unique(idx).numel() == 2048
+
+
+class _FakeSegment:
+    """A streamed segment (StreamedRounds' interface) over precomputed rounds: round r of the segment starting at
+    `first` returns the host driver's results for iteration first + r (oracle backend), or synthetic rows."""
+    made = []
+
+    def __init__(self, first, n, rounds_fn):
+        self.first, self.n, self.fn, self.cancelled = first, n, rounds_fn, False
+        _FakeSegment.made.append((first, n))
+
+    def round(self, r):
+        assert 0 <= r < self.n
+        return self.fn(self.first + r)
+
+    def cancel(self):
+        self.cancelled = True
+
+    def close(self):
+        return dict(seconds=0.0, spec_solves=0, spec_used=0, waited_s=0.0)
+
+
+def test_streamed_segments_equal_synchronous_rounds_on_oracle():
+    """vboc_run's segmented producer (stream_rounds = 2 rounds per launch, 5 iterations -> segments [0, 1], [2, 3],
+    [4]) trains on exactly the rows of the synchronous round-by-round loop."""
+    from oracle_backend import OracleBackend
+    from vboc_amd.pipeline import _generate, vboc_run
+    nq, n = 2, 4
+    be = OracleBackend(nq)
+    X_test = np.tile([np.pi, np.pi, 1.0, 1.0], (4, 1))
+    kw = dict(stop_time=1e9, num_prob=n, max_iterations=4, trainer_kw=dict(hidden=8, minibatch=16, stop_val=1e9))
+    sync = vboc_run(nq, be, X_test, stream=False, **kw)
+    _FakeSegment.made = []
+    fn = lambda it: _generate(nq, be, np.arange(it * n, (it + 1) * n), None, 20250124)
+    seg = vboc_run(nq, be, X_test, stream_rounds=2, segment_factory=lambda f, k: _FakeSegment(f, k, fn), **kw)
+    assert _FakeSegment.made == [(0, 2), (2, 2), (4, 1)]
+    assert seg["producer"]["segments"] == 3
+    np.testing.assert_array_equal(seg["X_save"], sync["X_save"])
+
+
+def test_time_budget_is_the_only_stop_rule_of_a_streamed_run():
+    """without an iteration limit a streamed run must not stop when its first launch's rounds run out
+    (stream_rounds = 2): the next segment starts and the loop runs until the time budget is spent."""
+    import time as _t
+    from vboc_amd.pipeline import vboc_run
+    nq = 3
+
+    def fn(it):
+        _t.sleep(0.15)
+        rows = [[[3.0 + 0.01 * (it % 7), 3.1, 3.2, 1.0 + 0.1 * b, -1.0, 0.5]] for b in range(8)]
+        return rows, dict(solves=8, rk4=0, sqp_iter=8, rounds=1)
+    _FakeSegment.made = []
+    X_test = np.tile([3.0, 3.1, 3.2, 1.0, -1.0, 0.5], (4, 1))
+    out = vboc_run(nq, None, X_test, stop_time=2.0, num_prob=8, stream_rounds=2,
+                   segment_factory=lambda f, k: _FakeSegment(f, k, fn),
+                   trainer_kw=dict(hidden=8, minibatch=8, stop_val=1e9))
+    assert len(out["stats"]) > 4                       # past the first segment's 2 rounds
+    assert len(_FakeSegment.made) >= 3 and all(k == 2 for _, k in _FakeSegment.made)
+    assert out["producer"]["segments"] == len(_FakeSegment.made)

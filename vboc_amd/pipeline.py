@@ -105,22 +105,49 @@ def _generate(nq, backend, ids, N_start, seed):
 
 
 def _round(nq, backend, iteration, num_prob, N_start, seed):
-    """One data-generation round over the problem ids [iteration * num_prob, (iteration + 1) * num_prob),
-    split into contiguous per-rank shards (np.array_split) when torch.distributed is initialised, so any
-    world size solves the same id set; the samples are all-gathered in rank (= problem) order."""
+    """One synchronous data-generation round over the problem ids [iteration * num_prob, (iteration + 1) * num_prob),
+    this rank's contiguous shard of them under torch.distributed; the samples are all-gathered in rank (= problem)
+    order."""
+    res, stats = _generate(nq, backend, _rank_ids(iteration, num_prob), N_start, seed)
+    return _gather_rows(samples_array(nq, res)), stats
+
+
+def _rank_ids(iteration, num_prob):
+    """This rank's ids of VBOC iteration `iteration`: [iteration * num_prob, (iteration + 1) * num_prob) split into
+    contiguous per-rank shards (np.array_split) under torch.distributed, so every world size solves the same ids and
+    the rank-ordered gather is the problem order."""
+    return _shard(np.arange(iteration * num_prob, (iteration + 1) * num_prob))
+
+
+def _shard(ids):
+    """This rank's contiguous share of `ids` under torch.distributed (np.array_split), else all of them."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return np.array_split(np.asarray(ids), dist.get_world_size())[dist.get_rank()]
+    return np.asarray(ids)
+
+
+def _is_rank0():
+    import torch.distributed as dist
+    return not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+
+
+def _gather_rows(X):
+    """All ranks' rows in rank (= problem) order (dist.gather_samples: RCCL under nccl, gloo on the CPU); the local
+    rows when torch.distributed is not initialised."""
+    import torch
     import torch.distributed as dist
     from .dist import gather_samples
-    ids = np.arange(iteration * num_prob, (iteration + 1) * num_prob)
-    if dist.is_available() and dist.is_initialized():
-        import torch
-        world, rank = dist.get_world_size(), dist.get_rank()
-        res, stats = _generate(nq, backend, np.array_split(ids, world)[rank], N_start, seed)
-        local = torch.from_numpy(samples_array(nq, res))
-        if dist.get_backend() == "nccl":
-            local = local.cuda()
-        return gather_samples(local).cpu().numpy(), stats
-    res, stats = _generate(nq, backend, ids, N_start, seed)
-    return samples_array(nq, res), stats
+    if not (dist.is_available() and dist.is_initialized()):
+        return X
+    local = torch.from_numpy(np.ascontiguousarray(X))
+    if dist.get_backend() == "nccl":
+        local = local.cuda()
+    return gather_samples(local).cpu().numpy()
+
+
+# row pool of one streamed segment: at most this many bytes (the segment then covers fewer rounds)
+STREAM_POOL_BYTES = 16 << 30
 
 
 class StreamedRounds:
@@ -128,46 +155,61 @@ class StreamedRounds:
 
     The reference regenerates num_prob problems per iteration with a synchronous Pool.map and refits in
     between (VBOC/triplependulum_vboc.py:493-568); `data_generation` never reads the model, so the ids of every
-    iteration are known up front.  One producer launch on its own stream works through the ids of `rounds`
-    iterations in order, and the host takes iteration r once all of its problems are finished (per-problem done
-    flags, released to memory by the kernel, polled on a side stream) - while iteration r is being fitted on
-    the default stream, the GPU keeps generating r + 1, r + 2, ...; no round pays its own tail.  `cancel()` skips
-    the problems not yet started (the time budget is spent); `close()` ends the launch."""
+    iteration are known up front.  One producer launch on its own stream works through the ids of its rounds
+    in order, and the host takes round r once all of its problems are finished (per-problem done flags, released
+    to memory by the kernel, polled on a side stream) - while round r is being fitted on the default stream, the
+    GPU keeps generating r + 1, r + 2, ...; no round pays its own tail.  `cancel()` skips the problems not yet
+    started (the time budget is spent); `close()` ends the launch.
 
-    def __init__(self, nq, solver, rounds, num_prob, first_id=0, N_start=None, seed=SEED, rows_per_problem=None,
-                 poll_s=0.005):
+    round_ids: one id array per round (this rank's shard under torch.distributed; default: `rounds` rounds of
+    num_prob consecutive ids from first_id).  The row pool holds the most a problem can save (2 (N_start + 12) + 2
+    rows, quirk A.3 included), so it cannot overflow; a segment whose pool would pass STREAM_POOL_BYTES is the
+    caller's to split (vboc_run's segments)."""
+
+    def __init__(self, nq, solver, rounds=None, num_prob=None, first_id=0, N_start=None, seed=SEED, poll_s=0.005,
+                 round_ids=None):
         import torch
-        self.torch, self.nq, self.num_prob, self.poll_s = torch, nq, num_prob, poll_s
+        self.torch, self.nq, self.poll_s = torch, nq, poll_s
         self.solver = solver
         dev = torch.device("cuda", solver.device)
-        B = rounds * num_prob
+        if round_ids is None:
+            round_ids = [np.arange(first_id + r * num_prob, first_id + (r + 1) * num_prob) for r in range(rounds)]
+        self.sizes = [len(r) for r in round_ids]
+        self.offs = np.concatenate([[0], np.cumsum(self.sizes)]).astype(np.int64)
+        B = int(self.offs[-1])
         N_start = int(N_start or system(nq).N)
-        # row pool: at most 2 N + 2 rows per problem (quirk A.3 included); typical is ~25, so a long producer is
-        # sized by rows_per_problem (an overflow is reported by close(), never written out of bounds)
-        rpp = rows_per_problem or (2 * (N_start + 12) + 2 if B <= 50_000 else 100)
-        self.ids = torch.arange(first_id, first_id + B, dtype=torch.int64, device=dev)
+        rpp = 2 * (N_start + 12) + 2
+        self.ids = torch.as_tensor(np.concatenate(round_ids).astype(np.int64), device=dev)
         self.flags = torch.zeros(B, dtype=torch.int32, device=dev)
         self.cancel_word = torch.zeros(1, dtype=torch.int32, device=dev)
         self.producer = torch.cuda.Stream(dev)
         self.side = torch.cuda.Stream(dev)
-        self.host_flags = torch.zeros(num_prob, dtype=torch.int32).pin_memory()
+        self.host_flags = torch.zeros(max(self.sizes + [1]), dtype=torch.int32).pin_memory()
         torch.cuda.synchronize(dev)
         self.t_start = time.time()
         self.out = solver.data_generation_device(self.ids, N_start=N_start, seed=seed, rows_cap=B * rpp,
                                                  stream=self.producer, done_flag=self.flags, cancel=self.cancel_word,
                                                  wait=False)
         self.waited = 0.0
+        self.closed = False
+
+    @staticmethod
+    def rounds_within(num_prob, nq, N_start=None, budget=STREAM_POOL_BYTES):
+        """How many rounds of num_prob problems one segment's row pool holds within `budget` bytes (>= 1)."""
+        rpp = 2 * (int(N_start or system(nq).N) + 12) + 2
+        return max(1, int(budget // max(1, num_prob * rpp * 2 * nq * 8)))
 
     def round(self, r):
-        """Results of iteration r in problem order (drivers.data_generation_batch's format) and its stats."""
-        torch, n = self.torch, self.num_prob
-        sl = slice(r * n, (r + 1) * n)
+        """Results of round r in problem order (drivers.data_generation_batch's format) and its stats."""
+        torch = self.torch
+        sl = slice(int(self.offs[r]), int(self.offs[r + 1]))
+        n = self.sizes[r]
         t = time.time()
-        while True:
+        while n:
             with torch.cuda.stream(self.side):
-                self.host_flags.copy_(self.flags[sl], non_blocking=True)
+                self.host_flags[:n].copy_(self.flags[sl], non_blocking=True)
             self.side.synchronize()
-            if bool(self.host_flags.all()):
+            if bool(self.host_flags[:n].all()):
                 break
             time.sleep(self.poll_s)
         self.waited += time.time() - t
@@ -180,7 +222,7 @@ class StreamedRounds:
         self.side.synchronize()
         cnt, off, st, ic, slot = cnt.numpy(), off.numpy(), st.numpy(), ic.numpy(), slot.numpy()
         if (cnt < -1).any():
-            raise RuntimeError(f"iteration {r}: row pool overflow or cancelled problems")
+            raise RuntimeError(f"round {r}: row pool overflow (-2) or cancelled problems (-3): {np.unique(cnt[cnt < -1])}")
         used = cnt > 0
         lo = int(off[used].min()) if used.any() else 0
         hi = int((off + np.maximum(cnt, 0))[used].max()) if used.any() else 0
@@ -205,9 +247,45 @@ class StreamedRounds:
         self.side.synchronize()
 
     def close(self):
+        if self.closed:
+            return None
+        self.closed = True
         out = self.solver.data_generation_wait(self.out)
         return dict(seconds=time.time() - self.t_start, spec_solves=out["spec_solves"], spec_used=out["spec_used"],
                     waited_s=self.waited)
+
+
+class SegmentedProducer:
+    """The VBOC loop's data generation as consecutive streamed segments of `R` rounds each: round `it` comes from
+    the segment that covers it; once the loop passes a segment's last round (all of its problems consumed) the
+    next segment starts at `it`.  So the time budget stays the only stop rule of a run without an iteration limit
+    (the reference's `while time.time() - start_time < stop_time`, VBOC/triplependulum_vboc.py:493).
+    make_segment(first_round, rounds) -> an object with round(r), cancel(), close() (StreamedRounds)."""
+
+    def __init__(self, make_segment, R, last_round=None):
+        self.make, self.R, self.last = make_segment, int(R), last_round
+        self.seg, self.first, self.infos = None, 0, []
+
+    def round(self, it):
+        if self.seg is None or it >= self.first + self.R:
+            if self.seg is not None:
+                self.infos.append(self.seg.close())
+            n = self.R if self.last is None else max(1, min(self.R, self.last + 1 - it))
+            self.seg, self.first = self.make(it, n), it
+        return self.seg.round(it - self.first)
+
+    def close(self, cancel=True):
+        if self.seg is not None:
+            if cancel:
+                self.seg.cancel()
+            self.infos.append(self.seg.close())
+            self.seg = None
+        infos = [i for i in self.infos if i]
+        if not infos:
+            return None
+        return dict(segments=len(infos), seconds=sum(i["seconds"] for i in infos),
+                    spec_solves=sum(i["spec_solves"] for i in infos), spec_used=sum(i["spec_used"] for i in infos),
+                    waited_s=sum(i["waited_s"] for i in infos))
 
 
 def _agree(flag):
@@ -225,11 +303,16 @@ def _agree(flag):
 
 def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None, N_start=None, seed=SEED,
              out_dir=None, device=None, trainer_kw=None, triple_refit_quirk=True, log=None, stream=None,
-             stream_rounds=None):
+             stream_rounds=None, segment_factory=None):
     """Run the VBOC loop; returns dict(X_save, mean, std, trainer, times, rmse, stats).
-    stream (default: on the GPU backend in a single process): the iterations' data generation runs as one
-    producer launch ahead of the fits (StreamedRounds) over max_iterations + 1 iterations (or stream_rounds;
-    problems not reached when the time budget is spent are cancelled)."""
+    stream (default: on the GPU backend): the iterations' data generation runs as producer launches ahead of the
+    fits (StreamedRounds), each over stream_rounds iterations (default: max_iterations + 1, else 64, capped by the
+    row-pool budget STREAM_POOL_BYTES); when the loop passes a launch's last iteration the next launch starts
+    (SegmentedProducer), so without an iteration limit the time budget is the only stop rule, as in the reference.
+    Under torch.distributed every rank streams its own shard of each iteration's ids (np.array_split, the same
+    shards as the synchronous rounds) and each iteration's samples are all-gathered (RCCL) in problem order; rank 0
+    fits, and rank 0's stop decision is broadcast.  Problems not reached when the loop stops are cancelled.
+    segment_factory(first_round, rounds) replaces StreamedRounds (tests)."""
     import torch
     import torch.distributed as dist
     if nq not in (2, 3):
@@ -241,51 +324,54 @@ def vboc_run(nq, backend, X_test, stop_time, num_prob=1000, max_iterations=None,
     t0 = time.time()
     iteration = 0
     solver = getattr(backend, "solver", None)
-    distributed = dist.is_available() and dist.is_initialized()
     if stream is None:
-        stream = (solver is not None and hasattr(solver, "data_generation_device") and not distributed and
-                  solver.nmax >= (N_start or system(nq).N) + 12)
+        stream = segment_factory is not None or (
+            solver is not None and hasattr(solver, "data_generation_device") and
+            solver.nmax >= (N_start or system(nq).N) + 12)
     producer = None
     if stream:
         R = stream_rounds or ((max_iterations + 1) if max_iterations is not None else 64)
-        producer = StreamedRounds(nq, solver, R, num_prob, N_start=N_start, seed=seed)
-        get_round = lambda it: (lambda r: (samples_array(nq, r[0]), r[1]))(producer.round(it))
-        if max_iterations is None:
-            max_iterations = R - 1
-        else:
-            max_iterations = min(max_iterations, R - 1)
+        R = min(R, StreamedRounds.rounds_within(num_prob, nq, N_start))
+        make = segment_factory or (lambda first, n: StreamedRounds(
+            nq, solver, N_start=N_start, seed=seed, round_ids=[_rank_ids(first + r, num_prob) for r in range(n)]))
+        producer = SegmentedProducer(make, R, last_round=max_iterations)
+
+        def get_round(it):
+            res, st = producer.round(it)
+            return _gather_rows(samples_array(nq, res)), st
     else:
         get_round = lambda it: _round(nq, backend, it, num_prob, N_start, seed)
-    X_save, st = get_round(iteration)
-    stats = [st]
-    log(f"iteration 0: {X_save.shape[0]} rows")
-    mean, std = position_stats(X_save, nq)
-    F = dir_features(X_save, mean, std, nq)
-    F_test = dir_features(X_test, mean, std, nq)
-    trainer = make_trainer(nq, device, **(trainer_kw or {})) if rank0 else None
-    times, rmse, fits = [], [], []
-    if rank0:
-        fits.append(trainer.fit(F))
-        times.append(time.time() - t0)
-        rmse.append(trainer.rmse(F_test))
-        log(f"fit: {fits[-1]}  rmse {rmse[-1]:.4g}")
-    while _agree(time.time() - t0 < stop_time and (max_iterations is None or iteration < max_iterations)):
-        iteration += 1
-        X_new, st = get_round(iteration)
+    times, rmse, fits, stats = [], [], [], []
+    trainer = None
+    try:
+        X_save, st = get_round(iteration)
         stats.append(st)
-        X_save = np.concatenate((X_save, X_new))
+        log(f"iteration 0: {X_save.shape[0]} rows")
+        mean, std = position_stats(X_save, nq)
+        F = dir_features(X_save, mean, std, nq)
+        F_test = dir_features(X_test, mean, std, nq)
+        trainer = make_trainer(nq, device, **(trainer_kw or {})) if rank0 else None
         if rank0:
-            src = X_save if (nq == 3 and triple_refit_quirk) else X_new
-            F_new = dir_features(src, mean, std, nq)
-            F = np.concatenate((F, F_new))
-            fits.append(trainer.fit(F, n_new=F_new.shape[0]))
+            fits.append(trainer.fit(F))
             times.append(time.time() - t0)
             rmse.append(trainer.rmse(F_test))
-            log(f"iteration {iteration}: {X_save.shape[0]} rows, fit {fits[-1]}, rmse {rmse[-1]:.4g}")
-    producer_info = None
-    if producer is not None:
-        producer.cancel()
-        producer_info = producer.close()
+            log(f"fit: {fits[-1]}  rmse {rmse[-1]:.4g}")
+        while _agree(time.time() - t0 < stop_time and (max_iterations is None or iteration < max_iterations)):
+            iteration += 1
+            X_new, st = get_round(iteration)
+            stats.append(st)
+            X_save = np.concatenate((X_save, X_new))
+            if rank0:
+                src = X_save if (nq == 3 and triple_refit_quirk) else X_new
+                F_new = dir_features(src, mean, std, nq)
+                F = np.concatenate((F, F_new))
+                fits.append(trainer.fit(F, n_new=F_new.shape[0]))
+                times.append(time.time() - t0)
+                rmse.append(trainer.rmse(F_test))
+                log(f"iteration {iteration}: {X_save.shape[0]} rows, fit {fits[-1]}, rmse {rmse[-1]:.4g}")
+    finally:
+        # an exception anywhere above must not leave a producer launch running on the handle
+        producer_info = producer.close(cancel=True) if producer is not None else None
     if rank0 and out_dir is not None:
         save_artifacts(out_dir, nq, X_save, mean, std, trainer.model, times, rmse)
     return dict(X_save=X_save, mean=mean, std=std, trainer=trainer, times=times, rmse=rmse, stats=stats, fits=fits,
@@ -323,7 +409,8 @@ def pendulum_vboc_run(out_dir=None, device="cuda", seed=0, backend=None, it_max=
 
 def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device="cuda", seed=0,
             minibatch=1 << 15, hidden=1000, log=None, resume=False):
-    """VBOC/UR5/vboc_multiprocessing_ur5.py's main block (config 5) on one GPU:
+    """VBOC/UR5/vboc_multiprocessing_ur5.py's main block (config 5), on one GPU or sharded over the ranks of
+    torch.distributed (config 5's 8 MI355X: each rank one contiguous share of every id range, rows all-gathered):
       test set      `testing_test` over ids [0, num_test) (:487-498)      -> data_4dof_vboc_test.npy
       training set  `testing_test` over ids [num_test, + num_train) (:506-528) -> data_4dof_vboc_train.npy
       features      [(q - mean) / std, qdot / |qdot|, |qdot|] with the position mean / std of the training set
@@ -344,8 +431,10 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
     t0 = time.time()
     dev = _device_solver(backend, 112)
     tt = (lambda ids: ur5_testing_device(ids, dev)) if dev is not None else (lambda ids: ur5_testing_batch(ids, backend))
-    res, st_test = tt(np.arange(num_test))
-    X_test = ur5_set(res)
+    # under torch.distributed every rank runs a contiguous shard of each id range and the rows are all-gathered in
+    # rank (= problem) order (the reference's Pool.map over range(num_prob), :487-528); rank 0 fits and writes
+    res, st_test = tt(_shard(np.arange(num_test)))
+    X_test = _gather_rows(ur5_set(res).reshape(-1, 8))
     log(f"test set: {X_test.shape[0]} rows of {num_test} in {time.time() - t0:.1f} s")
     t1 = time.time()
     first, X_old = num_test, np.zeros((0, 8))
@@ -356,12 +445,15 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
         X_old = np.load(old_path)                      # allow_pickle=False: plain float64 rows
         with open(old_path[:-4] + ".next_id") as f:
             first = int(f.read())
-    res, st_train = tt(np.arange(first, first + num_train))
-    X_save = ur5_set(res)
+    res, st_train = tt(_shard(np.arange(first, first + num_train)))
+    X_save = _gather_rows(ur5_set(res).reshape(-1, 8))
     X_train = np.concatenate((X_old, X_save))
     log(f"training set: {X_save.shape[0]} new rows of {num_train} in {time.time() - t1:.1f} s, "
         f"{X_train.shape[0]} with the previous run's")
     mean, std = position_stats(X_train, 4)
+    if not _is_rank0():
+        return dict(X_test=X_test, X_train=X_train, fit=None, rmse_train=None, rmse_test=None,
+                    stats=(st_test, st_train), mean=mean, std=std)
     F = dir_features(X_train, mean, std, 4)
     F_test = dir_features(X_test, mean, std, 4)
     k = min(minibatch, F.shape[0])
@@ -387,7 +479,7 @@ def ur5_run(backend=None, num_test=10000, num_train=100000, out_dir=None, device
 def cartesian_run(backend=None, num_test=1000, num_train=100000, out_dir=None, device="cuda", seed=0,
                   minibatch=4096, hidden=300, log=None):
     """The main block of VBOC/Cartesian constraints/vboc_multiprocessing.py (double pendulum with the end-effector
-    keep-out circle) on one GPU:
+    keep-out circle), on one GPU or sharded over the ranks of torch.distributed like ur5_run:
       test set      `testing_test` over ids [0, num_test) (:557-562)
       training set  `testing_test` over ids [num_test, + num_train) (:567-585)  -> data_2dof_vboc_10.npy (5 columns,
                     dt included, as the reference saves X_save)
@@ -409,14 +501,18 @@ def cartesian_run(backend=None, num_test=1000, num_train=100000, out_dir=None, d
     dev = _device_solver(backend, 112)
     tt = (lambda ids: cartesian_testing_device(ids, dev)) if dev is not None else \
         (lambda ids: cartesian_testing_batch(ids, backend))
-    res, st_test = tt(np.arange(num_test))
-    X_test = rows(res)
+    # under torch.distributed: per-rank contiguous shards, rows all-gathered in problem order, rank 0 fits and writes
+    res, st_test = tt(_shard(np.arange(num_test)))
+    X_test = _gather_rows(rows(res))
     log(f"test set: {X_test.shape[0]} rows of {num_test} in {time.time() - t0:.1f} s")
     t1 = time.time()
-    res, st_train = tt(np.arange(num_test, num_test + num_train))
-    X_train = rows(res)
+    res, st_train = tt(_shard(np.arange(num_test, num_test + num_train)))
+    X_train = _gather_rows(rows(res))
     log(f"training set: {X_train.shape[0]} rows of {num_train} in {time.time() - t1:.1f} s")
     mean, std = position_stats(X_train, 2)
+    if not _is_rank0():
+        return dict(X_test=X_test, X_train=X_train, fit=None, rmse_train=None, rmse_test=None,
+                    stats=(st_test, st_train), mean=mean, std=std)
     F = dir_features(X_train, mean, std, 2)
     F_test = dir_features(X_test, mean, std, 2)
     k = min(minibatch, F.shape[0])
