@@ -252,6 +252,33 @@ def test_large_refit_with_graphs_on_gpu():
     assert idx.min().item() >= n // 2 and idx.max().item() < n and torch.unique(idx).numel() == 2048
 
 
+@pytest.mark.gpu
+def test_consecutive_captured_fits_on_gpu():
+    """Verdict r03 item 2: consecutive HIP-graph-captured fits in ONE process, at the shapes of the configs[2] loop
+    whose third fit faulted in round 3 (profiles/r03f_vboc_loop_fault.log: a first fit, then refits whose halves
+    grow past 2^20 rows; the triple's refit quirk makes the new half all of X_save), each a new capture over new
+    feature tensors, then the UR5's 8-1000-1 fit (minibatch 2^15) twice on the same trainer class.  Every fit
+    runs its steps and keeps the parameters finite."""
+    from vboc_amd.learn import DirTrainer
+    nq = 3
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    tr = DirTrainer(nq, "cuda", seed=4, graphs=True, poll=64)
+    tr.it_max = 10**9
+    for n, n_new in ((500_000, 0), (1_010_000, 505_000), (2_520_000, 1_510_000), (4_030_000, 2_520_000)):
+        F = torch.rand((n, 2 * nq + 1), device="cuda", generator=g)
+        r = tr.fit(F, n_new=n_new, it_max=192)
+        assert r["iterations"] == 191 and np.isfinite(r["val"]), (n, r)
+        del F
+    assert all(torch.isfinite(p).all() for p in tr.model.parameters())
+    arm = DirTrainer(4, "cuda", hidden=1000, minibatch=1 << 15, seed=1, graphs=True, poll=64)
+    for n, n_new in ((200_000, 0), (400_000, 200_000)):
+        F = torch.rand((n, 9), device="cuda", generator=g)
+        r = arm.fit(F, n_new=n_new, it_max=128)
+        assert r["iterations"] == 127 and np.isfinite(r["val"])
+    assert all(torch.isfinite(p).all() for p in arm.model.parameters())
+
+
 class _FakeSegment:
     """A streamed segment (StreamedRounds' interface) over precomputed rounds: round r of the segment starting at
     `first` returns the host driver's results for iteration first + r (oracle backend), or synthetic rows."""

@@ -125,6 +125,17 @@ class DirTrainer:
         self.poll = poll
         self.it_max = None
         self.total_steps = 0
+        self.seed, self.fits = seed, 0
+        # Every buffer a captured step writes or reads across fits is allocated ONCE, here, outside any capture:
+        # the gradients (backward accumulates into them after an in-graph zero_(), instead of allocating them in
+        # the graph's private pool, where a new capture would find the previous graph's blocks), and the stop
+        # rule's state (val, it, it_lim, active: refilled per fit, never re-allocated).  See fit() for the sampler.
+        for p in self.params:
+            p.grad = torch.zeros_like(p)
+        self.val = torch.zeros((), device=self.device)
+        self.it = torch.ones((), dtype=torch.int64, device=self.device)
+        self.it_lim = torch.zeros((), dtype=torch.int64, device=self.device)
+        self.active = torch.ones((), dtype=torch.bool, device=self.device)
 
     # -- one gated step, written with device tensors only (capturable) ---------------------------------
     # top-k slices are kept at most this long: a uniform k-subset of a long range is the top-k of the per-chunk
@@ -133,9 +144,9 @@ class DirTrainer:
     # whose halves exceeded 2^20 rows; the fits before it (halves of 0.5M rows) had run in the same process.
     TOPK_CHUNK = 1 << 18
 
-    def _sample(self, lo, hi, k):
+    def _sample(self, lo, hi, k, gen=None):
         n = hi - lo
-        keys = torch.rand(n, device=self.device, generator=self.gen)
+        keys = torch.rand(n, device=self.device, generator=gen or self.gen)
         if n <= self.TOPK_CHUNK:
             return torch.topk(keys, k, sorted=False).indices + lo
         c = self.TOPK_CHUNK
@@ -146,17 +157,17 @@ class DirTrainer:
         best = torch.topk(part.values.reshape(-1), k, sorted=False).indices
         return cand.reshape(-1).index_select(0, best) + lo
 
-    def _step(self, F, X, y, n, n_new):
+    def _step(self, F, X, y, n, n_new, gen=None):
         if n_new:
-            idx = torch.cat([self._sample(0, n - n_new, self.k // 2), self._sample(n - n_new, n, self.k // 2)])
+            idx = torch.cat([self._sample(0, n - n_new, self.k // 2, gen), self._sample(n - n_new, n, self.k // 2, gen)])
         else:
-            idx = self._sample(0, n, self.k)
+            idx = self._sample(0, n, self.k, gen)
         xb = X.index_select(0, idx)
         yb = y.index_select(0, idx)
         active = (self.val > self.stop_val) & (self.it < self.it_lim)
         a = active.to(torch.float32)
         for p in self.params:
-            p.grad = None
+            p.grad.zero_()
         loss = torch.mean((self.model(xb) - yb) ** 2)
         loss.backward()
         grads = [p.grad for p in self.params]
@@ -194,28 +205,34 @@ class DirTrainer:
             raise ValueError(f"need at least {self.k} rows (random.sample of a minibatch)")
         X = F[:, :self.nin].contiguous()
         y = F[:, self.nin:self.nin + 1].contiguous()
-        self.val = torch.max(F[:, self.nin]).reshape(())     # :73 val = max |qdot|
-        self.it = torch.ones((), dtype=torch.int64, device=self.device)
-        self.it_lim = torch.tensor(it_max, dtype=torch.int64, device=self.device)
-        self.active = torch.ones((), dtype=torch.bool, device=self.device)
+        self.val.copy_(torch.max(F[:, self.nin]))          # :73 val = max |qdot|
+        self.it.fill_(1)
+        self.it_lim.fill_(it_max)
+        self.active.fill_(True)
+        self.fits += 1
         steps = 0
         if self.graphs:
+            # Each captured fit draws from a generator of its own (seeded from the trainer's seed and the fit's
+            # index) that only that graph registers: re-registering one generator with a second graph after the
+            # first was destroyed is the pattern that ran in the round-3 fault (profiles/r03f_vboc_loop_fault.log,
+            # DESIGN.md section 11), and nothing of a destroyed graph is referenced by the next one.
+            gen = torch.Generator(device=self.device)
+            gen.manual_seed(self.seed * 1_000_003 + self.fits)
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):                      # warm-up outside capture (allocations)
-                self._step(F, X, y, n, n_new)
+                self._step(F, X, y, n, n_new, gen)
             torch.cuda.current_stream(self.device).wait_stream(s)
             steps += 1
             g = torch.cuda.CUDAGraph()
-            g.register_generator_state(self.gen)             # replays advance the sampler's Philox offset
-            for p in self.params:
-                p.grad = None
+            g.register_generator_state(gen)                  # replays advance this fit's Philox offset
             with torch.cuda.graph(g):
-                self._step(F, X, y, n, n_new)
+                self._step(F, X, y, n, n_new, gen)
             while bool(self.active.item()):
                 for _ in range(self.poll):
                     g.replay()
                 steps += self.poll
+            torch.cuda.synchronize(self.device)
             del g
         else:
             while bool(self.active.item()):
