@@ -58,7 +58,11 @@ from vboc_amd.drivers import IC_DRAWS, TEST_DRAWS, TEST_STREAM, ProblemRNG  # no
 from vboc_amd.ics import SEED, uniforms  # noqa: E402
 from vboc_amd.systems import system  # noqa: E402
 
-IDS = {3: list(range(0, 12)), 2: list(range(100, 124))}
+# data_generation fixtures: 256 problems each, the triple's long-tail ids (first solves that run hundreds of SQP
+# iterations, tests/test_gpu.py LONG_TAIL), and a failure-injected set (FAIL_MOD: restart branches, None returns)
+LONG_TAIL = (988, 358, 832, 1464, 703, 125, 73)
+IDS = {3: sorted(set(range(0, 256)) | set(LONG_TAIL)), 2: list(range(100, 356))}
+FAIL_IDS = {3: list(range(2000, 2064)), 2: list(range(3000, 3064))}
 TEST_IDS = {3: list(range(0, 64)), 2: list(range(0, 64)), 1: list(range(0, 128))}
 FAIL_MOD = 3   # oracle_backend.forced_failure: about a third of the solves fail -> restarts exercised
 N_START = 100
@@ -117,16 +121,19 @@ class FakeSolver:
 
 
 class FakeOCP:
-    def __init__(self, nq):
+    def __init__(self, nq, fail_mod=0):
         s = system(nq)
-        self.nq, self.N = nq, N_START
+        self.nq, self.N, self.fail_mod = nq, N_START, fail_mod
         self.ocp_solver = FakeSolver()
         self.g, self.l1, self.m1 = s.g, s.l[0], s.m[0]
         if nq == 2:
             self.l2, self.m2 = s.l[1], s.m[1]
 
     def OCP_solve(self, *args):
+        from oracle_backend import forced_failure
         st, x, u, c = oracle_solve(self.nq, self.N, *args)
+        if forced_failure(args[7][0], self.fail_mod):   # q_init_lb[0]: tests/oracle_backend.py's injection rule
+            st = 4
         self.ocp_solver.x, self.ocp_solver.u, self.ocp_solver.cost = x, u, c
         return st
 
@@ -164,25 +171,43 @@ def tolist(v):
     return float(v) if isinstance(v, (float, np.floating)) else v
 
 
+def _dg_chunk(args):
+    """The reference's data_generation for a chunk of problem ids (one worker process)."""
+    nq, fname, ids, fail_mod = args
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    code = extract(os.path.join(REF, fname))
+    s = system(nq)
+    ocp = FakeOCP(nq, fail_mod)
+    g = dict(np=np, norm=norm, math=math, ocp=ocp, sim=FakeSim(nq), q_min=s.q_min, q_max=s.q_max,
+             v_min=-s.v_max, v_max=s.v_max, tau_max=s.u_max, dt_sym=s.dt, tol=s.tol, eps=s.eps)
+    exec(code, g)
+    U = uniforms(np.array(ids), 3 * nq + 1, SEED)
+    out = []
+    for b, pid in enumerate(ids):
+        g["random"] = FakeRandom(U[b, :IC_DRAWS[nq]], ProblemRNG(pid, SEED))
+        ocp.N = N_START                       # N_start per problem (SURVEY App. A.1)
+        out.append(tolist(g["data_generation"](pid)))
+        print(nq, fail_mod, pid, "None" if out[-1] is None or out[-1][0] is None else
+              len(out[-1] if nq == 3 else out[-1][0]), flush=True)
+    return out
+
+
+def _dg_run(nq, fname, ids, fail_mod, workers=8):
+    from multiprocessing import Pool
+    chunks = [list(c) for c in np.array_split(np.array(ids), workers) if len(c)]
+    with Pool(len(chunks)) as pool:
+        parts = pool.map(_dg_chunk, [(nq, fname, [int(i) for i in c], fail_mod) for c in chunks])
+    return [r for part in parts for r in part]
+
+
 def main():
     for nq, fname in ((3, "triplependulum_vboc.py"), (2, "doublependulum_vboc.py")):
-        code = extract(os.path.join(REF, fname))
-        s = system(nq)
-        ocp = FakeOCP(nq)
-        g = dict(np=np, norm=norm, math=math, ocp=ocp, sim=FakeSim(nq), q_min=s.q_min, q_max=s.q_max,
-                 v_min=-s.v_max, v_max=s.v_max, tau_max=s.u_max, dt_sym=s.dt, tol=s.tol, eps=s.eps)
-        exec(code, g)
-        ids = IDS[nq]
-        U = uniforms(np.array(ids), 3 * nq + 1, SEED)
-        out = []
-        for b, pid in enumerate(ids):
-            g["random"] = FakeRandom(U[b, :IC_DRAWS[nq]], ProblemRNG(pid, SEED))
-            ocp.N = N_START                       # N_start per problem
-            out.append(tolist(g["data_generation"](pid)))
-            print(nq, pid, "None" if out[-1] is None or out[-1][0] is None else len(out[-1] if nq == 3 else out[-1][0]),
-                  flush=True)
+        out = _dg_run(nq, fname, IDS[nq], 0)
+        fout = _dg_run(nq, fname, FAIL_IDS[nq], FAIL_MOD)
         with open(os.path.join(HERE, f"driver_{nq}.json"), "w") as f:
-            json.dump({"nq": nq, "ids": ids, "N_start": N_START, "seed": SEED, "results": out}, f)
+            json.dump({"nq": nq, "ids": IDS[nq], "N_start": N_START, "seed": SEED, "results": out,
+                       "fail_mod": FAIL_MOD, "fail_ids": FAIL_IDS[nq], "fail_results": fout,
+                       "long_tail": [i for i in LONG_TAIL if nq == 3]}, f)
 
 
 def main_testing():

@@ -68,11 +68,14 @@ def test_device_loop_matches_reference_fixture(nq):
     from vboc_amd import lib
     from vboc_amd.drivers import data_generation_device
     g = json.load(open(os.path.join(HERE, "golden", f"driver_{nq}.json")))
-    res, _ = data_generation_device(nq, np.array(g["ids"]), lib.Solver(nq, g["N_start"] + 20),
-                                    N_start=g["N_start"], seed=g["seed"])
-    same, _ = _compare(nq, res, g["results"], 1e-5)
-    # measured on MI355X: 12 / 12 (triple), 24 / 24 (double), profiles/r02y_gpu_driver_agreement.log
-    assert same >= 0.95 * len(g["ids"]), (same, len(g["ids"]))
+    assert len(g["ids"]) >= 256
+    for ids, results, fail_mod in ((g["ids"], g["results"], 0), (g["fail_ids"], g["fail_results"], g["fail_mod"])):
+        s = lib.Solver(nq, g["N_start"] + 20)
+        s.set_option("dg_fail_mod", fail_mod)
+        res, _ = data_generation_device(nq, np.array(ids), s, N_start=g["N_start"], seed=g["seed"])
+        same, _ = _compare(nq, res, results, 1e-5)
+        print(f"nq {nq} fail_mod {fail_mod}: {same} / {len(ids)} problems as the reference's function")
+        assert same >= 0.95 * len(ids), (fail_mod, same, len(ids))
 
 
 @pytest.mark.gpu

@@ -29,23 +29,33 @@ def _samples(nq, r):
     return None if s is None else np.asarray(s, dtype=float)
 
 
+def _sets(g):
+    """(ids, results, fail_mod) of the fixture's sets: the plain one and the failure-injected one."""
+    yield g["ids"], g["results"], 0
+    if "fail_ids" in g:
+        yield g["fail_ids"], g["fail_results"], g["fail_mod"]
+
+
 @pytest.mark.parametrize("nq", [3, 2])
 def test_driver_matches_reference_state_machine(nq):
     from vboc_amd.drivers import data_generation_batch
     g = _golden(nq)
-    res, stats = data_generation_batch(nq, np.array(g["ids"]), OracleBackend(nq), N_start=g["N_start"])
-    assert stats["solves"] > len(g["ids"]) and stats["rk4"] > 0
-    for pid, got, ref in zip(g["ids"], res, g["results"]):
-        a, b = _samples(nq, got), _samples(nq, ref)
-        assert (a is None) == (b is None), pid
-        if a is not None:
-            np.testing.assert_array_equal(a, b, err_msg=f"problem {pid}")
-        if nq == 2:
-            for k in (1, 2):
-                if ref[k] is None:
-                    assert got[k] is None
-                else:
-                    np.testing.assert_array_equal(np.asarray(got[k], float), np.asarray(ref[k], float))
+    assert len(g["ids"]) >= 256
+    for ids, results, fail_mod in _sets(g):
+        res, stats = data_generation_batch(nq, np.array(ids), OracleBackend(nq, fail_mod=fail_mod),
+                                           N_start=g["N_start"])
+        assert stats["solves"] > len(ids) and stats["rk4"] > 0
+        for pid, got, ref in zip(ids, res, results):
+            a, b = _samples(nq, got), _samples(nq, ref)
+            assert (a is None) == (b is None), pid
+            if a is not None:
+                np.testing.assert_array_equal(a, b, err_msg=f"problem {pid} (fail_mod {fail_mod})")
+            if nq == 2:
+                for k in (1, 2):
+                    if ref[k] is None:
+                        assert got[k] is None
+                    else:
+                        np.testing.assert_array_equal(np.asarray(got[k], float), np.asarray(ref[k], float))
 
 
 @pytest.mark.gpu

@@ -2,8 +2,8 @@
 CPU baseline of bench.py's dg-loop leg) against the reference's own function.
 
 tests/golden/driver_{2,3}.json are the return values of `data_generation` AST-extracted from
-VBOC/{triple,double}pendulum_vboc.py and run on the CPU oracle with the fixtures' failure injection
-(tests/golden/make_driver_golden.py; no failure injection).  The C state machine, one problem per OpenMP thread on the same oracle,
+VBOC/{triple,double}pendulum_vboc.py and run on the CPU oracle (tests/golden/make_driver_golden.py): 256+ problems without failure injection (the triple's
+long-tail ids included) and 64 with it (fail_mod 3: restart branches).  The C state machine, one problem per OpenMP thread on the same oracle,
 must return the same samples bit for bit (and for the double the same 3-tuples).  A second check runs more
 problems, with and without the fixtures' failure injection (restart branches), against the batched Python
 driver (vboc_amd.drivers, itself pinned to the same fixtures) on the oracle."""
@@ -29,11 +29,13 @@ def _same(nq, got, ref):
 @pytest.mark.parametrize("nq", [3, 2])
 def test_c_data_generation_matches_reference_fixture(nq):
     g = json.load(open(os.path.join(HERE, "golden", f"driver_{nq}.json")))
-    res, st = oracle.data_generation(nq, np.array(g["ids"]), N_start=g["N_start"], seed=g["seed"],
-                                     nthreads=4)
-    assert st["solves"] > len(g["ids"]) and st["rk4"] > 0
-    bad = [pid for pid, a, b in zip(g["ids"], res, g["results"]) if not _same(nq, a, b)]
-    assert not bad, bad
+    assert len(g["ids"]) >= 256
+    for ids, results, fail_mod in ((g["ids"], g["results"], 0), (g["fail_ids"], g["fail_results"], g["fail_mod"])):
+        res, st = oracle.data_generation(nq, np.array(ids), N_start=g["N_start"], seed=g["seed"], fail_mod=fail_mod,
+                                         nthreads=8)
+        assert st["solves"] > len(ids) and st["rk4"] > 0
+        bad = [pid for pid, a, b in zip(ids, res, results) if not _same(nq, a, b)]
+        assert not bad, (fail_mod, bad)
 
 
 @pytest.mark.parametrize("nq,fail_mod", [(3, 0), (2, 0), (3, 3), (2, 3)])
