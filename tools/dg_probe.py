@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--B", type=int, default=100_000)
     ap.add_argument("--first", type=int, default=0)
     ap.add_argument("--groups", type=int, nargs="*", default=[0])
+    ap.add_argument("--save", default=None, help="write the per-problem stats (lib.DG_STATS) of each launch to "
+                                                 "<save>_g<groups>.npy (scheduling studies)")
     a = ap.parse_args()
     s = lib.Solver(a.nq, 120, device=0)
     ids = torch.arange(a.first, a.first + a.B, dtype=torch.int64, device="cuda:0")
@@ -65,6 +67,8 @@ def main():
                "tflops": round(dg_flops(a.nq, st) / (ms / 1e3) / 1e12, 4),
                "digest": h.hexdigest()}
         print(json.dumps(rec), flush=True)
+        if a.save:
+            np.save(f"{a.save}_g{rec['groups']}.npy", st)
 
 
 if __name__ == "__main__":

@@ -423,7 +423,12 @@ struct Coop {
   // wave's own ds_reads by this wait alone)
   template <int N>
   __device__ __forceinline__ static void vmwait() {
+#ifdef VBOC_VMWAIT_DRAIN
+    // measurement builds: every counted ring wait drains (an under-counted wait can then not read a stale slot)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+#endif
   }
   // retire every ordinary VMEM op in a way the compiler's waitcnt pass sees (the builtin, vmcnt(0)):
   // called before a ring's first DMA, so no loop-carried register is still "pending" in the pass's
@@ -436,7 +441,12 @@ struct Coop {
     const dbl2* src = (const dbl2*)(s + fslot(slot));
     gdbl2* dst = (gdbl2*)(g + (long long)k * REC);
 #ifndef VBOC_WB_MASKED
-    if constexpr (NQ <= 3) {
+#ifdef VBOC_WB_UNMASKED_ALL
+    constexpr bool UNMASKED = true;    // measurement builds: the arm with the chains' unmasked store
+#else
+    constexpr bool UNMASKED = NQ <= 3;
+#endif
+    if constexpr (UNMASKED) {
       // every lane stores (lanes past the field range repeat the last chunk: same bytes, same address), no exec
       // mask: 16k first solves 4 082 -> 3 949 ms on one box, same results (profiles/r03z_wb_ab.json).  The arm
       // keeps the masked store: its k_wave<4> lost parity with the unmasked one
@@ -1116,7 +1126,17 @@ struct Coop {
   // dot-product steps on P, Pi, Sc, LINE flushed to LDS.  Same algebra as factor(); the summation order
   // inside an MFMA differs (rounding-level).
   static constexpr int CE = NX + NU, CP = CE + 1;   // H row / G column of rs e; first Pi column
-  static constexpr bool MFMA_OK = (NX <= 8) && (CP + NQ <= 16) && (L::W_FAC + 2 * NX + 2 <= L::RSF);
+  // A_cl = A + B K of stages N-1..1 is formed inside factor_mfma (acl_slot) and written back with the
+  // stage's outputs (ring_wb<OK, OX>: K .. Pe, C (dead until vec rebuilds it), A_cl): no acl_pass re-reading A, B
+  // and K from the stage records.  -DVBOC_ACL_PASS keeps the separate pass (measurement builds).
+#ifdef VBOC_ACL_PASS
+  static constexpr bool ACL_FUSED = false;
+#else
+  static constexpr bool ACL_FUSED = FM;
+#endif
+  // factor_mfma's junk target: lanes without an output write the slot's tail past the written-back fields
+  static constexpr int FJUNK = L::OX;
+  static constexpr bool MFMA_OK = (NX <= 8) && (CP + NQ <= 16) && (FJUNK + 2 * NX + 2 <= L::RSF);
   // H_u rows NX .. NX+NU-1 live in accumulator registers HR0, HR0 + 1; the LDS image keeps those two
   // registers of every lane group: image row (row & 3) + 4 * ((row >> 2) - HR0)
   static constexpr int HR0 = NX >> 2;
@@ -1135,6 +1155,18 @@ struct Coop {
   // per-lane masks are FP64 0/1 multipliers (no lane-mask SGPRs to spill), H_u goes through an LDS image
   // (no readlane / bpermute), and outputs a lane does not own land in the slot's junk tail [W_FAC, RSF)
   // (never written back) instead of behind an exec mask.
+  // A_cl = A + B K of the stage held in factor slot `sl` (its window and the K just computed), into the slot's
+  // A_cl field: one entry per lane, acl_pass's arithmetic and order (same bits)
+  __device__ __forceinline__ void acl_slot(int sl) {
+    const int kb = fslot(sl);
+    if (t < NX * NX) {
+      const int q = t / NX, i = t - q * NX;
+      double a = s[kb + OA + q * NX + i];
+      UNR for (int c = 0; c < NU; ++c) a += s[kb + OB + q * NU + c] * s[kb + OK + c * NX + i];
+      s[kb + OACL + t] = a;
+    }
+  }
+
   __device__ __forceinline__ bool factor_mfma() {
     static_assert(MFMA_OK, "stage blocks fit one 16x16 FP64 MFMA tile");
     fresh();
@@ -1185,10 +1217,10 @@ struct Coop {
     double zm[NU];
     UNR for (int a = 0; a < NU; ++a) zm[a] = (zc && g == a) ? 1.0 : 0.0;
     // output addresses (slot-relative; lanes without that output write the junk tail)
-    const int kofs = (g == 0 && c < NX) ? OK + c : L::W_FAC;
-    const int mofs = (g == 0 && c >= CP && c < CP + NQ) ? OM + (c - CP) : L::W_FAC;
-    const int pofs = (c == CE) ? OPE + g : L::W_FAC;
-    int yofs = L::W_FAC, ysrc = HS;
+    const int kofs = (g == 0 && c < NX) ? OK + c : FJUNK;
+    const int mofs = (g == 0 && c >= CP && c < CP + NQ) ? OM + (c - CP) : FJUNK;
+    const int pofs = (c == CE) ? OPE + g : FJUNK;
+    int yofs = FJUNK, ysrc = HS;
     if (t < NU * NQ) {
       const int a = t / NQ, jj = t % NQ, row = NX + a;
       yofs = OY + t;
@@ -1201,7 +1233,14 @@ struct Coop {
     bool ok = true;
     for (int j = 0; j < N - 1; ++j) {
       const int k = N - 1 - j, kb = fslot(j % L::NSF);
-      if (j >= 1) ring_wb<OK, OC>((j - 1) % L::NSF, k + 1);
+      if (j >= 1) {
+        if constexpr (ACL_FUSED) {
+          acl_slot((j - 1) % L::NSF);                   // LDS ops of this wave run in order: the write-back's
+          ring_wb<OK, L::OX>((j - 1) % L::NSF, k + 1);  // reads of the slot see them
+        } else {
+          ring_wb<OK, OC>((j - 1) % L::NSF, k + 1);
+        }
+      }
       fdma(j + 2);
       vmwait<2 * P>();   // loads only, as in factor()
       dbg_check(kb, k, 0, L::W_FAC, 1);
@@ -1306,7 +1345,14 @@ struct Coop {
     lsync();
     {
       const int j = N - 1, kb = fslot(j % L::NSF);
-      if (j >= 1) ring_wb<OK, OC>((j - 1) % L::NSF, 1);
+      if (j >= 1) {
+        if constexpr (ACL_FUSED) {
+          acl_slot((j - 1) % L::NSF);
+          ring_wb<OK, L::OX>((j - 1) % L::NSF, 1);
+        } else {
+          ring_wb<OK, OC>((j - 1) % L::NSF, 1);
+        }
+      }
       // stage 0's window was issued two sweeps ago (and the clamped repeats after it): retire all
       vmwait<0>();
       Dsc z1[RD], z2[RD], z4[RD];
@@ -2047,7 +2093,7 @@ struct Coop {
         bool okf;
         if constexpr (FM) VREP(2, okf = factor_mfma());
         else VREP(2, okf = factor());
-        VREP(3, acl_pass());
+        if constexpr (!ACL_FUSED) VREP(3, acl_pass());
         CPROF(3)
         bool okv;
         VREP(4, okv = vec(ODA, w0, nun));
