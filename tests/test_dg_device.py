@@ -79,6 +79,41 @@ def test_device_loop_matches_reference_fixture(nq):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nq", [3, 2])
+def test_parked_first_solves_change_nothing(nq):
+    """dg.h "Parked first solves": a problem whose first solve succeeded is parked and resumed later on any wave
+    (IC sampling re-run, the parked result taken as its first solve).  Every problem's rows, counts and solve
+    statistics equal those of the same launch without parking (dg_park 0), with and without the fixtures'
+    failure injection (restart chains), with a small park window and the high queue in use."""
+    import torch
+    from vboc_amd import lib
+    ids = torch.arange(7_000, 7_000 + 3_000, dtype=torch.int64, device="cuda:0")
+    keep = [0, 1, 2, 3, 4, 7, 8]
+    for fail_mod in (0, 3):
+        outs = []
+        for park, window in ((0, 0), (1, 0), (1, 64)):
+            s = lib.Solver(nq, 120)
+            s.set_option("dg_fail_mod", fail_mod)
+            s.set_option("dg_park", park)
+            s.set_option("dg_park_window", window)
+            s.set_option("dg_park_hi", 20)
+            o = s.data_generation_device(ids)
+            torch.cuda.synchronize()
+            outs.append(o)
+        ref = outs[0]
+        cnt = ref["row_cnt"].cpu().numpy()
+        for o in outs[1:]:
+            assert torch.equal(o["row_cnt"], ref["row_cnt"])
+            assert torch.equal(o["stats"][:, keep], ref["stats"][:, keep])
+            if nq == 2:
+                assert torch.equal(o["ic"], ref["ic"]) and torch.equal(o["ic_slot"], ref["ic_slot"])
+            ra, rb = ref["rows"].cpu().numpy(), o["rows"].cpu().numpy()
+            oa, ob = ref["row_off"].cpu().numpy(), o["row_off"].cpu().numpy()
+            for i in np.flatnonzero(cnt > 0):
+                np.testing.assert_array_equal(ra[oa[i]:oa[i] + cnt[i]], rb[ob[i]:ob[i] + cnt[i]])
+
+
+@pytest.mark.gpu
 def test_device_loop_properties_at_scale():
     """4096 triple problems: every saved row satisfies the save filter (:362-365) or is a quirk-A.3
     duplicate of a state at the velocity box; statistics are consistent; a second run is identical."""

@@ -76,6 +76,14 @@ struct DgJobs {
   unsigned* spec_q_tail;          // queue: entries pushed / popped
   unsigned* spec_q_head;
   unsigned long long* spec_count; // [0] speculative solves run by other waves, [1] of them used
+  // parked first solves (see "Parked first solves" below); park_res == nullptr switches parking off
+  double* park_res;               // [count][park_stride]: status, cost, sqp, qp, t0, then x [N + 1][nx + 1], u [N][nu]
+  int park_stride;
+  int park_window;                // new problems go first while fewer than this many parked problems wait
+  int park_hi_it;                 // first solves with >= this many SQP iterations resume first (queue 0)
+  int* park_q;                    // [2][count]: queues 0 (high) and 1 of job + 1, 0 = not yet written
+  unsigned* park_tail;            // [2] entries pushed
+  unsigned* park_head;            // [2] entries taken
 };
 
 // a horizon extension gives up after 10 solves (VBOC/triplependulum_vboc.py:107): a failure at attempt a
@@ -91,7 +99,7 @@ enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST
 template <int NQ>
 struct DgState {
   int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, spec_ev,
-      spec_base;
+      spec_base, resumed;
   double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
   double sqp, nsqp, nqp, t0, st1, it1;
   double ran[2], store_ic[4], xsym[2 * NQ];
@@ -298,6 +306,7 @@ struct Dg {
     const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max, eps = J.eps;
     s->phase = HEXT; s->N = J.N_start; s->ext = 0; s->f = 0; s->at_limit = 0; s->N_test = 0; s->ver = 0;
     s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0;
+    s->resumed = 0;
     s->sqp = 0.0; s->nsqp = 0.0; s->nqp = 0.0; s->cost = 1e6;
     int di = 0;
     auto draw = [&]() { return philox_uniform(pid, di++, J.seed, 0u); };
@@ -373,6 +382,10 @@ struct Dg {
       const long long q = (long long)(fabs(qlb0()[0]) * 1e6);
       if (q % J.fail_mod == 0) ((int*)in.status)[wg] = 4;
     }
+    if (s->solves == 1 && !s->resumed && J.park_res && this->status() == 0 && park_open()) {
+      park(it);
+      return 3;
+    }
     const int more = s->phase == HEXT ? on_hext() : (on_verif() ? 1 : 0);
     if (more) return more;
     return s->phase == SWEEP && sweep() ? 1 : 0;   // one inlined copy of the sweep (with its RK4)
@@ -426,6 +439,55 @@ struct Dg {
         }
       }
     }
+  }
+
+  // ---- Parked first solves ----
+  // A launch ends with its slowest problems, and the slow ones are known after their first solve: in the measured
+  // launches every problem longer than 5 s started with a first solve of >= 100 SQP iterations, and 97 % of the
+  // 100 slowest with a FAILED first solve (max_iter, the chains of restarts).  So a problem whose first solve
+  // succeeded is parked - its first-solve result goes to park_res[job] and the job to a queue - and the wave takes
+  // the next new problem, while a failed first solve continues at once.  Once the new problems run out (or
+  // park_window problems wait) waves resume parked problems, those with a first solve of >= park_hi_it SQP
+  // iterations first: the long problems start early and the last ones to start are short.  Resuming re-runs the
+  // deterministic IC sampling of start() and takes the parked result as the first solve, so every problem's
+  // results are those of an unparked run (same inputs, same solver; tests/test_dg_device.py).
+  __device__ __forceinline__ bool park_open() const {
+    // parking only pays while new problems remain (else the wave would resume its own problem at once)
+    return __hip_atomic_load(J.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)J.count;
+  }
+  __device__ __forceinline__ void park(int it) {
+    const int N = nreq();
+    double* r = J.park_res + (long long)job * J.park_stride;
+    for (int e = t; e < (N + 1) * NXR; e += 64) st_coh(r + 8 + e, xo(0)[e]);
+    for (int e = t; e < N * NU; e += 64) st_coh(r + 8 + (N + 1) * NXR + e, uo(0)[e]);
+    if (t == 0) {
+      st_coh(r, (double)status()); st_coh(r + 1, in.cost[wg]);
+      st_coh(r + 2, (double)in.sqp_iter[wg]); st_coh(r + 3, (double)in.qp_iter[wg]);
+      st_coh(r + 4, s->t0);
+      const int q = it >= J.park_hi_it ? 0 : 1;
+      const unsigned pos = atomicAdd(&J.park_tail[q], 1u);
+      st_flag(&J.park_q[(long long)q * J.count + pos], job + 1);   // waits for every lane's stores first
+    }
+    __syncthreads();
+  }
+  // a parked job: start()'s IC sampling and first request again, then the parked result as its solve
+  __device__ __forceinline__ void resume(int job_) {
+    start(job_);
+    __syncthreads();
+    const int N = nreq();
+    const double* r = J.park_res + (long long)job * J.park_stride;
+    for (int e = t; e < (N + 1) * NXR; e += 64) ((double*)in.xo)[row(0) * NXR + e] = ld_coh(r + 8 + e);
+    for (int e = t; e < N * NU; e += 64)
+      ((double*)in.uo)[((long long)wg * J.nmax) * NU + e] = ld_coh(r + 8 + (N + 1) * NXR + e);
+    if (t == 0) {
+      ((int*)in.status)[wg] = (int)ld_coh(r);
+      ((double*)in.cost)[wg] = ld_coh(r + 1);
+      ((int*)in.sqp_iter)[wg] = (int)ld_coh(r + 2);
+      ((int*)in.qp_iter)[wg] = (int)ld_coh(r + 3);
+    }
+    s->t0 = ld_coh(r + 4);   // the problem's start: its first solve
+    s->resumed = 1;
+    __syncthreads();
   }
 
   // ---- Speculative restarts ----
@@ -844,6 +906,11 @@ __device__ __forceinline__ int dg_feed(const DgJobs* J, const Inputs* in, int wg
   return D.feed(job);
 }
 template <int NQ>
+__device__ __forceinline__ void dg_resume(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Dg<NQ> D(*J, *in, wg, t);
+  D.resume(job);
+}
+template <int NQ>
 __device__ __forceinline__ void dg_finish(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
   Dg<NQ> D(*J, *in, wg, t);
   D.finish(job);
@@ -867,6 +934,32 @@ __device__ __forceinline__ void dg_spec_store(const DgJobs* J, const Inputs* in,
 // wave-uniform value of lane 0
 __device__ __forceinline__ int dg_bcast(int v) { return __builtin_amdgcn_readfirstlane(__shfl(v, 0)); }
 
+// lane 0: take a parked job (queue 0 first), -1 if none is waiting
+__device__ __forceinline__ int dg_take_parked(const DgJobs* J) {
+  for (int q = 0; q < 2; ++q) {
+    unsigned h = __hip_atomic_load(&J->park_head[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (h < __hip_atomic_load(&J->park_tail[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      if (__hip_atomic_compare_exchange_strong(&J->park_head[q], &h, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) {
+        int e;
+        while ((e = ld_flag(&J->park_q[(long long)q * J->count + h])) == 0) __builtin_amdgcn_s_sleep(2);
+        after_flag();
+        return e - 1;
+      }
+      // h now holds the current head: retry against it
+    }
+  }
+  return -1;
+}
+// lane 0: parked jobs waiting (both queues)
+__device__ __forceinline__ unsigned dg_parked_waiting(const DgJobs* J) {
+  unsigned w = 0;
+  for (int q = 0; q < 2; ++q)
+    w += __hip_atomic_load(&J->park_tail[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+         __hip_atomic_load(&J->park_head[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return w;
+}
+
 // one workgroup = one wave: it owns one problem's whole data_generation at a time, or - once the problem
 // queue is drained - runs one speculative restart solve for another problem's owner (they shorten the
 // chains of failing solves that make the launch tail).  `in` is the Inputs batch of one problem per workgroup (the wave solver works on problem index wg
@@ -882,6 +975,7 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
   Coop<NQ, FM> C(smem, gptr(jb.regions) + (long long)wg * jb.region_doubles, w, o, t);
   const int count = J->count;
   const bool spec = J->spec_events > 0;
+  const bool park = J->park_res != nullptr;
   for (;;) {
     int mode = 0, idx = 0, ev = 0, jj = 0, code = 0;
     // 0. near the end of the problem queue (spec_early), a queued restart job of a running chain goes before a new
@@ -896,14 +990,26 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
       }
       pre = dg_bcast(pre);
     }
-    // 1. the next problem
+    // 1. the next problem: a new one, or a parked one once the new ones run out or park_window parked ones wait
     if (!pre) {
-      int got = -1;
-      if (t == 0 && __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)count) {
-        const unsigned i = atomicAdd(jb.next, 1u);
-        if (i < (unsigned)count) got = (int)i;
+      int got = -1, res = 0;
+      if (t == 0) {
+        const bool more = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)count;
+        if (park && (!more || dg_parked_waiting(J) >= (unsigned)J->park_window)) {
+          got = dg_take_parked(J);
+          res = got >= 0;
+        }
+        if (got < 0 && more) {
+          const unsigned i = atomicAdd(jb.next, 1u);
+          if (i < (unsigned)count) got = (int)i;
+        }
+        if (got < 0 && park) {
+          got = dg_take_parked(J);
+          res = got >= 0;
+        }
       }
       got = dg_bcast(got);
+      res = dg_bcast(res);
       int cancelled = 0;
       if (got >= 0 && J->cancel && t == 0)
         cancelled = __hip_atomic_load(J->cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -914,7 +1020,12 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
       if (got >= 0) {
         idx = got;
         mode = 1;
-        code = dg_start<NQ>(J, inp, wg, t, idx) ? 1 : 0;
+        if (res) {
+          dg_resume<NQ>(J, inp, wg, t, idx);
+          code = 2;   // the first solve's result is in place
+        } else {
+          code = dg_start<NQ>(J, inp, wg, t, idx) ? 1 : 0;
+        }
       }
     }
     // 2. no problem left: a queued speculative restart of a chain that is still running (they only run
@@ -952,10 +1063,13 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
     if (mode == 0) {
       int fin = 0;
       if (t == 0) fin = __hip_atomic_load(J->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)count;
+      // without speculation a wave leaves when it finds no work: every parked job was pushed by a wave that then
+      // comes back here and takes it (or another one), so no parked job is left without a taker
       if (dg_bcast(fin) || !spec) break;
       __builtin_amdgcn_s_sleep(64);
       continue;
     }
+    bool parked = false;
     while (code) {
       if (code == 1) {
         __syncthreads();
@@ -976,12 +1090,16 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
       }
       if (mode == 1) {
         code = dg_feed<NQ>(J, inp, wg, t, idx);
+        if (code == 3) {   // the first solve succeeded and the problem was parked
+          parked = true;
+          code = 0;
+        }
       } else {
         dg_spec_store<NQ>(J, inp, wg, t, ev, jj);
         code = 0;
       }
     }
-    if (mode == 1) dg_finish<NQ>(J, inp, wg, t, idx);
+    if (mode == 1 && !parked) dg_finish<NQ>(J, inp, wg, t, idx);
     __syncthreads();
   }
 }

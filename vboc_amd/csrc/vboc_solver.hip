@@ -1518,6 +1518,12 @@ struct vboc_solver {
   bool hc_wave = true;              // constrained problems on the wave solver (k_wave<NQ, false, true>)
   void* dg_spec = nullptr;          // their pool (events, results, control words, queue)
   size_t dg_spec_bytes = 0;
+  // parked first solves of the data-generation loop (dg.h): their results and the two resume queues
+  bool dg_park = true;
+  int dg_park_window = 0;           // 0: parked problems wait until the new ones run out
+  int dg_park_hi = 100;             // first solves with >= this many SQP iterations resume first
+  void* dg_park_buf = nullptr;
+  size_t dg_park_bytes = 0;
   // a vboc_data_generation_async launch is running on this handle's buffers (dg_scratch, regions, head counters)
   // until vboc_data_generation_wait: every other entry point that would reuse them refuses (VBOC_ERR_ARG)
   bool dg_busy = false;
@@ -1834,6 +1840,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->dg_in) (void)hipFree(h->dg_in);
   if (h->tt_jobs) (void)hipFree(h->tt_jobs);
   if (h->dg_spec) (void)hipFree(h->dg_spec);
+  if (h->dg_park_buf) (void)hipFree(h->dg_park_buf);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   for (auto ev : h->pev) (void)hipEventDestroy(ev);
@@ -1871,6 +1878,9 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "dg_fail_mod") h->dg_fail_mod = (int)v;
   else if (s == "dg_speculate") h->dg_speculate = v != 0.0;
   else if (s == "dg_spec_early") h->dg_spec_early = v > 0.0 ? (int)v : 0;
+  else if (s == "dg_park") h->dg_park = v != 0.0;
+  else if (s == "dg_park_window") h->dg_park_window = v > 0.0 ? (int)v : 0;
+  else if (s == "dg_park_hi") h->dg_park_hi = v > 0.0 ? (int)v : 0;
 #ifdef VBOC_SPEC_MIN_EXT
   else if (s == "dg_spec_min_ext") h->dg_spec_min_ext = v > 0.0 ? (int)v : 0;
 #endif
@@ -1910,6 +1920,9 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
   else if (s == "dg_speculate") *v = h->dg_speculate ? 1.0 : 0.0;
   else if (s == "dg_spec_early") *v = (double)h->dg_spec_early;
+  else if (s == "dg_park") *v = h->dg_park ? 1.0 : 0.0;
+  else if (s == "dg_park_window") *v = (double)h->dg_park_window;
+  else if (s == "dg_park_hi") *v = (double)h->dg_park_hi;
   else if (s == "hc_wave") *v = h->hc_wave ? 1.0 : 0.0;
   else if (s == "factor_mfma") *v = h->factor_mfma ? 1.0 : 0.0;
   else if (s == "wave_groups") *v = (double)h->n_regions;
@@ -2289,7 +2302,8 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   J.stats = b->stats;
   J.done_flag = done_flag; J.cancel = cancel;
   // counters: [0] job queue, [1] finished problems, [2..3] error flags, [4..5] rows used (u64),
-  // [6] speculation events, [7] / [8] restart-job queue tail / head, [10..13] speculative solves run / used (u64)
+  // [6] speculation events, [7] / [8] restart-job queue tail / head, [10..13] speculative solves run / used (u64),
+  // [16..17] / [18..19] parked-job queue tails / heads
   J.next = h->head; J.done = h->head + 1; J.err = h->head + 2; J.rows_next = (unsigned long long*)(h->head + 4);
   J.spec_ev_next = h->head + 6; J.spec_q_tail = h->head + 7; J.spec_q_head = h->head + 8;
   J.spec_count = (unsigned long long*)(h->head + 10);
@@ -2322,6 +2336,28 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
     J.spec = (double*)((char*)h->dg_spec + ((spec_ctl + 255) & ~(size_t)255));
     J.spec_events = E; J.spec_stride = (int)stride;
     HIPCHK(hipMemsetAsync(h->dg_spec, 0, spec_ctl, st));
+  }
+  // parked first solves (data generation only): one result record per job, two queues, counters head[16..19]
+  J.park_res = nullptr; J.park_q = nullptr; J.park_stride = 0;
+  J.park_window = 0; J.park_hi_it = h->dg_park_hi;
+  J.park_tail = h->head + 16; J.park_head = h->head + 18;
+  if (h->dg_park && !testing) {
+    const int stride = (8 + (b->N_start + 1) * NXR + b->N_start * NU + 1) & ~1;
+    const size_t qbytes = ((sizeof(int) * 2 * (size_t)b->B) + 255) & ~(size_t)255;
+    const size_t pneed = qbytes + sizeof(double) * (size_t)stride * (size_t)b->B;
+    if (pneed > h->dg_park_bytes) {
+      if (h->dg_park_buf) (void)hipFree(h->dg_park_buf);
+      h->dg_park_buf = nullptr;
+      h->dg_park_bytes = 0;
+      if (hipMalloc(&h->dg_park_buf, pneed) != hipSuccess)
+        return fail(VBOC_ERR_NOMEM, W + ": hipMalloc of the parked first solves");
+      h->dg_park_bytes = pneed;
+    }
+    J.park_q = (int*)h->dg_park_buf;
+    J.park_res = (double*)((char*)h->dg_park_buf + qbytes);
+    J.park_stride = stride;
+    J.park_window = h->dg_park_window > 0 ? h->dg_park_window : b->B;
+    HIPCHK(hipMemsetAsync(h->dg_park_buf, 0, sizeof(int) * 2 * (size_t)b->B, st));
   }
   HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
   HIPCHK(hipEventRecord(h->ev0, st));
