@@ -240,3 +240,41 @@ class DriverBackend:
 
     def rk4(self, x, u, T):
         return np.stack([rk4(self.nq, T, x[i], u[i]) for i in range(x.shape[0])])
+
+
+class MpcNN(ctypes.Structure):
+    """vboc_mpc_nn_t (vboc_oracle.h): the terminal row's network."""
+    _fields_ = [("hid", ctypes.c_int)] + [(n, ctypes.c_void_p) for n in ("W0", "b0", "W1", "b1", "W2", "b2")] + \
+               [(n, ctypes.c_double) for n in ("mean", "std", "lh", "uh")]
+
+
+def mpc_solve_batch(spec, x0, x_guess, u_guess, params=None, mean=0.0, std=1.0, rti=False, opts=None,
+                    nthreads=None, lh=0.0, uh=1e6):
+    """The Safe-MPC OCP_solve (vboc_oracle_ft.c vboc_oracle_mpc_solve) for every row of x0 [B, 6]: spec a
+    vboc_amd.safempc.MpcSpec, guesses [B, N+1, 6] / [B, N, 3], params the NeuralNetDIR weights (float64, None = no
+    terminal row).  Returns (x, u, results, h(x_N))."""
+    x0, xg, ug = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, x_guess, u_guess))
+    B, N = x0.shape[0], spec.N
+    assert xg.shape == (B, N + 1, 6) and ug.shape == (B, N, 3)
+    x_out, u_out = np.zeros_like(xg), np.zeros_like(ug)
+    res = np.zeros(B, dtype=RESULT_DTYPE)
+    hrow = np.zeros(B)
+    if opts is None:
+        opts = default_opts(lm=spec.lm, tol_stat=1e-6, qp_tol_stat=1e-8)
+    vec = [np.ascontiguousarray(a, dtype=np.float64) for a in
+           (spec.xmin, spec.xmax, spec.umin, spec.umax, spec.xmin, spec.xmax, spec.W, spec.W_e, spec.yref, spec.yref_e)]
+    nnp = None
+    keep = None
+    if params is not None:
+        keep = [np.ascontiguousarray(p, dtype=np.float64) for p in params]
+        nnp = MpcNN(hid=keep[0].shape[0], mean=float(mean), std=float(std), lh=float(lh), uh=float(uh),
+                    **{n: p.ctypes.data for n, p in zip(("W0", "b0", "W1", "b1", "W2", "b2"), keep)})
+    rc = lib().vboc_oracle_mpc_solve_batch(3, B, N, ctypes.c_double(spec.time_step), _p(x0), _p(xg), _p(ug),
+                                           *[_p(a) for a in vec], ctypes.c_double(spec.cost_scale),
+                                           ctypes.byref(nnp) if nnp is not None else None, int(bool(rti)),
+                                           ctypes.byref(opts), int(nthreads or os.cpu_count()), _p(x_out), _p(u_out),
+                                           _p(res), _p(hrow))
+    if rc != 0:
+        raise RuntimeError(f"oracle mpc_solve_batch failed rc={rc}")
+    del keep
+    return x_out, u_out, res, hrow

@@ -53,6 +53,26 @@ int vboc_oracle_ft_solve_batch(int nq, int B, int Nmax, const int* N, const doub
                                const double* lbu, const double* ubu, const double* lbx0, const double* ubx0,
                                const double* lbxe, const double* ubxe, const vboc_opts_t* opts, int nthreads,
                                double* x_out, double* u_out, vboc_result_t* res);
+/* Safe-MPC tracking OCP with the terminal NN row (vboc_oracle_ft.c): NeuralNetDIR(2 nq, hid, 1) weights in
+   float64 (row-major, torch's nn.Linear layout), the scalar position mean / std, the row's bounds */
+typedef struct {
+  int hid;
+  const double *W0, *b0, *W1, *b1, *W2, *b2;
+  double mean, std, lh, uh;
+} vboc_mpc_nn_t;
+/* x [N + 1][2 nq], u [N][nq]; W [3 nq] stage weights on [x; u], We [2 nq], yref [3 nq], yref_e [2 nq]; cs the
+   stage-cost scale; nn NULL = no terminal row; rti 1 = SQP_RTI (one QP, full step) */
+int vboc_oracle_mpc_solve(int nq, int N, double h, const double* x0, const double* x_guess, const double* u_guess,
+                          const double* xlb, const double* xub, const double* ulb, const double* uub,
+                          const double* xNlb, const double* xNub, const double* W, const double* We,
+                          const double* yref, const double* yref_e, double cs, const vboc_mpc_nn_t* nn, int rti,
+                          const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* hrow);
+int vboc_oracle_mpc_solve_batch(int nq, int B, int N, double h, const double* x0, const double* x_guess,
+                                const double* u_guess, const double* xlb, const double* xub, const double* ulb,
+                                const double* uub, const double* xNlb, const double* xNub, const double* W,
+                                const double* We, const double* yref, const double* yref_e, double cs,
+                                const vboc_mpc_nn_t* nn, int rti, const vboc_opts_t* opts, int nthreads,
+                                double* x_out, double* u_out, vboc_result_t* res, double* hrow);
 /* HJR one-step OCP (vboc_oracle_hjr.c): x0 fixed, N = 1, terminal cost = logit 0 of NeuralNetCLS */
 void vboc_oracle_hjr_default_opts(int nq, vboc_opts_t* o);
 int vboc_oracle_hjr_solve_batch(int nq, int B, const double* x0, int h, const double* W0, const double* b0,

@@ -21,6 +21,21 @@
  *    backward sweep through Pi = E', exactly as the terminal-velocity equality of vboc_oracle.c);
  *  - per-stage linear cost gradients.
  * Path bounds must be proper boxes (lb < ub on every component); otherwise -2 (unsupported).
+ *
+ * The same solver also restates the Safe-MPC OCP of the reference (`OCPtriplependulumHardTerm`,
+ * VBOC/Safe MPC/triplependulum_class_vboc.py:91-240; vboc_oracle_mpc_solve below):
+ *  - model MODELtriplependulum (nx 6, nu 3, :8-78) on intervals of time_step: here the dt column of the
+ *    free-time model pinned by the fixed x_0 (dt_{k+1} = dt_k, unbounded on the path), an exact reformulation;
+ *  - LINEAR_LS cost 1/2 |[x; u] - yref|^2_W at stages 0..N-1 and 1/2 |x_N - yref_e|^2_{W_e} at N (:108-134) with the
+ *    Gauss-Newton Hessian W (+ levenberg_marquardt), stage costs scaled by `cs` (ACADOS' cost_scaling: the time
+ *    step in current releases, 1 in older ones - the version is unpinned);
+ *  - x_0 fixed (OCP_solve's constraints_set(0, lbx / ubx, x0), :163-181), path and terminal boxes (:136-151);
+ *  - the terminal nonlinear row 0 <= h(x_N) = NN(x_N) - max(|x_N[2:]|, 1e-3) <= 1e6 (HardTerm :197-240,
+ *    nn_decisionfunction: NeuralNetDIR(6, hid, 1), positions (x - mean) / std, velocities / that norm - the
+ *    reference's x[2:] includes theta_3, kept), handled like the Cartesian rows of vboc_oracle.c (two slacks,
+ *    infeasible start, sigma c c' in the terminal Riccati block); no constraint Hessian (Gauss-Newton);
+ *  - SQP_RTI (the Safe-MPC driver's option, hard_terminal_constraints/3dof_sym.py:96): one linearisation, one QP,
+ *    the full step; status 0, or 4 if the QP fails.
  */
 #include <math.h>
 #include <stdlib.h>
@@ -54,7 +69,67 @@ typedef struct {
   double S[FX * FX], lin_e[FX], rs;
   fstage_t* st;
   vboc_opts_t o;
+  /* Safe-MPC tracking cost and terminal row (vboc_oracle_mpc_solve; all zero / NULL for the free-time OCP) */
+  int track, rti;
+  double wq[FZ], yr[FZ], we[FX], yre[FX], cs;
+  const vboc_mpc_nn_t* nn;
+  double hv, hg[FX], hL, hU, htl, htu, hql, hqu, hr0l, hr0u, hatl, hatu, haql, haqu, hll, hlu;
 } fprob_t;
+
+/* ------------------------------------------------------------------------------------------ */
+/* the Safe-MPC terminal row h(x) = NN(z(x)) - vn(x) (nn_decisionfunction, :208-230) and grad    */
+/* ------------------------------------------------------------------------------------------ */
+static double nn_row(const vboc_mpc_nn_t* n, int nq, const double* x, double* grad) {
+  const int nx = 2 * nq, H = n->hid;
+  double ss = 0.0;
+  for (int j = 2; j < nx; ++j) ss += x[j] * x[j];   /* norm_2(x[2:]) - theta_3 included, as the reference */
+  const double nrm = sqrt(ss), vn = nrm > 1e-3 ? nrm : 1e-3;
+  double z[2 * FQ];
+  for (int j = 0; j < nq; ++j) z[j] = (x[j] - n->mean) / n->std;
+  for (int j = nq; j < nx; ++j) z[j] = x[j] / vn;
+  double* a1 = (double*)malloc(sizeof(double) * 2 * H);
+  double* a2 = a1 + H;
+  for (int i = 0; i < H; ++i) {
+    double t = 0.0;
+    for (int j = 0; j < nx; ++j) t += n->W0[i * nx + j] * z[j];
+    t += n->b0[i];
+    a1[i] = t > 0.0 ? t : 0.0;   /* fmax(0., out) */
+  }
+  double out = 0.0;
+  for (int i = 0; i < H; ++i) {
+    double t = 0.0;
+    for (int j = 0; j < H; ++j) t += n->W1[i * H + j] * a1[j];
+    t += n->b1[i];
+    a2[i] = t;
+    if (t > 0.0) out += n->W2[i] * t;
+  }
+  out += n->b2[0];
+  if (grad) {
+    /* d out / d z by reverse mode through the two ReLUs (derivative 0 at a kink) */
+    double* g1 = (double*)calloc((size_t)H, sizeof(double));
+    for (int i = 0; i < H; ++i) {
+      if (!(a2[i] > 0.0)) continue;
+      const double w = n->W2[i];
+      for (int j = 0; j < H; ++j) g1[j] += w * n->W1[i * H + j];
+    }
+    double gz[2 * FQ] = {0};
+    for (int i = 0; i < H; ++i) {
+      if (!(a1[i] > 0.0)) continue;
+      for (int j = 0; j < nx; ++j) gz[j] += g1[i] * n->W0[i * nx + j];
+    }
+    free(g1);
+    /* chain rule through z(x) and vn(x) = max(|x[2:]|, 1e-3) */
+    double dvn[2 * FQ] = {0};
+    if (nrm > 1e-3) for (int j = 2; j < nx; ++j) dvn[j] = x[j] / nrm;
+    for (int j = 0; j < nx; ++j) {
+      double t = j < nq ? gz[j] / n->std : gz[j] / vn;
+      for (int q = nq; q < nx; ++q) t -= gz[q] * x[q] / (vn * vn) * dvn[j];
+      grad[j] = t - dvn[j];
+    }
+  }
+  free(a1);
+  return out - vn;
+}
 
 /* ------------------------------------------------------------------------------------------ */
 /* dynamics: physics rhs with analytic Jacobians (vboc_oracle_model), ERK4 with h = dt and the   */
@@ -141,26 +216,58 @@ static void fcomp(const fprob_t* P, int k, int i, double* val, double* lb, doubl
   if (k == 0) {
     if (i < P->nf0) { const int c = P->f0[i]; *val = s->x[c]; *lb = P->x0lb[c]; *ub = P->x0ub[c]; }
     else { *val = s->u[i - P->nf0]; *lb = P->ulb[i - P->nf0]; *ub = P->uub[i - P->nf0]; }
-    return;
-  }
-  if (k == P->N) {
+  } else if (k == P->N) {
     *val = s->x[i];
     if (P->xNfix[i]) { *lb = -INFINITY; *ub = INFINITY; *boxed = 0; }
     else { *lb = P->xNlb[i]; *ub = P->xNub[i]; }
-    return;
-  }
-  if (i < nx) { *val = s->x[i]; *lb = P->xlb[i]; *ub = P->xub[i]; }
+  } else if (i < nx) { *val = s->x[i]; *lb = P->xlb[i]; *ub = P->xub[i]; }
   else { *val = s->u[i - nx]; *lb = P->ulb[i - nx]; *ub = P->uub[i - nx]; }
+  if (isinf(*lb) && isinf(*ub)) *boxed = 0;   /* a free component (the Safe-MPC model's pinned dt) */
+}
+
+/* stage-variable index i of stage k -> index into the tracking weights [x (nx); u (nu)] (-1: none) */
+static int fwidx(const fprob_t* P, int k, int i) {
+  if (k == 0) return i < P->nf0 ? P->f0[i] : P->nx + (i - P->nf0);
+  return i;
+}
+/* Gauss-Newton Hessian diagonal of the tracking cost (0 for the free-time OCP) */
+static double fhq(const fprob_t* P, int k, int i) {
+  if (!P->track) return 0.0;
+  if (k == P->N) return P->we[i];
+  return P->cs * P->wq[fwidx(P, k, i)];
 }
 
 static double fgrad(const fprob_t* P, int k, int i) {
+  if (P->track) {   /* W ([x; u] - yref) at the current iterate */
+    double v, lb, ub; int boxed;
+    fcomp(P, k, i, &v, &lb, &ub, &boxed);
+    if (k == P->N) return P->we[i] * (v - P->yre[i]);
+    const int w = fwidx(P, k, i);
+    return P->cs * P->wq[w] * (v - P->yr[w]);
+  }
   if (k == 0) return i < P->nf0 ? P->c0[P->f0[i]] : 0.0;
   if (k == P->N) return 0.0;
   return i < P->nx ? P->cp[i] : 0.0;
 }
 
+/* the tracking cost of stage states (x, u) (u NULL at the terminal stage) */
+static double ftrack(const fprob_t* P, int k, const double* x, const double* u) {
+  double c = 0.0;
+  if (k == P->N) {
+    for (int i = 0; i < P->nx; ++i) { const double d = x[i] - P->yre[i]; c += P->we[i] * d * d; }
+    return 0.5 * c;
+  }
+  for (int i = 0; i < P->nx; ++i) { const double d = x[i] - P->yr[i]; c += P->wq[i] * d * d; }
+  for (int a = 0; a < P->nu; ++a) { const double d = u[a] - P->yr[P->nx + a]; c += P->wq[P->nx + a] * d * d; }
+  return 0.5 * P->cs * c;
+}
+
 static double fcost(const fprob_t* P) {
   double c = 0.0;
+  if (P->track) {
+    for (int k = 0; k <= P->N; ++k) c += ftrack(P, k, P->st[k].x, k < P->N ? P->st[k].u : NULL);
+    return c;
+  }
   for (int i = 0; i < P->nx; ++i) c += P->c0[i] * P->st[0].x[i];
   for (int k = 1; k < P->N; ++k)
     for (int i = 0; i < P->nx; ++i) c += P->cp[i] * P->st[k].x[i];
@@ -183,6 +290,10 @@ static void flinearize(fprob_t* P) {
   for (int i = 0; i < nx; ++i) {
     for (int j = 0; j < P->nf0; ++j) s0->F0[i * m0 + j] = s0->A[i * nx + P->f0[j]];
     for (int a = 0; a < nu; ++a) s0->F0[i * m0 + P->nf0 + a] = s0->B[i * nu + a];
+  }
+  if (P->nn) {   /* terminal row: value and gradient (the pinned dt column has none) */
+    memset(P->hg, 0, sizeof(P->hg));
+    P->hv = nn_row(P->nn, P->nq, P->st[P->N].x, P->hg);
   }
 }
 
@@ -210,6 +321,7 @@ static void fresiduals(const fprob_t* P, double* rstat, double* req, double* rin
       } else {
         gr -= P->st[N - 1].pi[i];
         for (int j = 0; j < P->ne; ++j) if (P->ei[j] == i) gr += P->tnu[j];
+        if (P->nn) gr += P->hg[i] * (P->hlu - P->hll);
       }
       st = fmax(st, fabs(gr));
       if (boxed) {
@@ -217,6 +329,10 @@ static void fresiduals(const fprob_t* P, double* rstat, double* req, double* rin
         cp = fmax(cp, fmax(fabs(s->ll[i] * (v - lb)), fabs(s->lu[i] * (ub - v))));
       }
     }
+  }
+  if (P->nn) {
+    in = fmax(in, fmax(P->nn->lh - P->hv, P->hv - P->nn->uh));
+    cp = fmax(cp, fmax(fabs(P->hll * (P->hv - P->nn->lh)), fabs(P->hlu * (P->nn->uh - P->hv))));
   }
   *rstat = st; *req = eq; *rineq = in; *rcomp = cp;
 }
@@ -262,6 +378,11 @@ static int fnewton(fprob_t* P, int factor, double* nu_new) {
   fstage_t* sN = &P->st[N];
   memset(Pm, 0, sizeof(Pm));
   for (int i = 0; i < nx; ++i) { Pm[i * nx + i] = sN->H[i]; p[i] = sN->g[i]; }
+  if (P->nn) {   /* the terminal row's barrier: sigma c c' */
+    const double sig = P->hql / P->htl + P->hqu / P->htu;
+    for (int i = 0; i < nx; ++i)
+      for (int j = 0; j < nx; ++j) Pm[i * nx + j] += sig * P->hg[i] * P->hg[j];
+  }
   memset(Pi, 0, sizeof(Pi));
   for (int j = 0; j < ne; ++j) Pi[P->ei[j] * ne + j] = 1.0;
   memset(lin, 0, sizeof(lin));
@@ -443,6 +564,23 @@ static void fr_add(fratio_t* m, double t, double dt) {
   if (dt < 0.0 && t * m->d < m->n * (-dt)) { m->n = t; m->d = -dt; }
 }
 
+/* the terminal row's c'd over the stage-N step d */
+static double frow_dot(const fprob_t* P, const double* d) {
+  double t = 0.0;
+  for (int i = 0; i < P->nx; ++i) t += P->hg[i] * d[i];
+  return t;
+}
+/* Newton directions of the terminal row's slacks / duals (vboc_oracle.c hc_dir; smu = 0 and zero affine
+   directions give the predictor's) */
+static void frow_dir(const fprob_t* P, double smu, double* dtl, double* dtu, double* dql, double* dqu) {
+  const double cd = frow_dot(P, P->st[P->N].d), rl = P->rs * P->hr0l, ru = P->rs * P->hr0u;
+  const double rcl = smu - P->htl * P->hql - P->hatl * P->haql, rcu = smu - P->htu * P->hqu - P->hatu * P->haqu;
+  *dtl = cd + rl;
+  *dtu = ru - cd;
+  *dql = (rcl - P->hql * *dtl) / P->htl;
+  *dqu = (rcu - P->hqu * *dtu) / P->htu;
+}
+
 static int fqp(fprob_t* P, int* iters) {
   const int nx = P->nx, nu = P->nu, ne = P->ne, N = P->N, m0 = P->nf0 + nu;
   const vboc_opts_t* o = &P->o;
@@ -465,6 +603,19 @@ static int fqp(fprob_t* P, int* iters) {
     }
   }
   for (int j = 0; j < ne; ++j) P->qnu[j] = 0.0;
+  if (P->nn) {   /* terminal row: slacks from the initial c'dz_N, clipped to ipm_push (infeasible start) */
+    const double gd = frow_dot(P, P->st[N].dz);
+    P->hL = P->nn->lh - P->hv;
+    P->hU = P->nn->uh - P->hv;
+    P->htl = fmax(gd - P->hL, o->ipm_push);
+    P->htu = fmax(P->hU - gd, o->ipm_push);
+    P->hql = o->mu0 / P->htl;
+    P->hqu = o->mu0 / P->htu;
+    P->hr0l = gd - P->hL - P->htl;
+    P->hr0u = P->hU - gd - P->htu;
+    P->hatl = P->hatu = P->haql = P->haqu = 0.0;
+    nbox += 2;
+  }
   double e00 = 0.0, rd0 = 0.0;
   for (int k = 0; k < N; ++k) {
     fstage_t* s = &P->st[k];
@@ -485,10 +636,12 @@ static int fqp(fprob_t* P, int* iters) {
     P->st[N].e0[j] = t;
     e00 = fmax(e00, fabs(t));
   }
+  if (P->nn) e00 = fmax(e00, fmax(fabs(P->hr0l), fabs(P->hr0u)));
   for (int k = 0; k <= N; ++k) {
     const fstage_t* s = &P->st[k];
     for (int i = 0; i < fnz(P, k); ++i)
-      rd0 = fmax(rd0, fabs(rho * s->dz[i] + fgrad(P, k, i) - s->ql[i] + s->qu[i]));
+      rd0 = fmax(rd0, fabs((rho + fhq(P, k, i)) * s->dz[i] + fgrad(P, k, i) - s->ql[i] + s->qu[i] +
+                           ((P->nn && k == N) ? P->hg[i] * (P->hqu - P->hql) : 0.0)));
   }
   P->rs = 1.0;
   int it, status = 1;
@@ -502,17 +655,24 @@ static int fqp(fprob_t* P, int* iters) {
         mu += (s->dz[i] - s->Lb[i]) * s->ql[i] + (s->Ub[i] - s->dz[i]) * s->qu[i];
       }
     }
+    if (P->nn) mu += P->htl * P->hql + P->htu * P->hqu;
     mu /= (double)nbox;
     if (!isfinite(mu)) { status = -1; break; }
     if (mu < o->qp_tol_comp && P->rs * rd0 < o->qp_tol_stat && P->rs * e00 < o->qp_tol_eq) { status = 0; break; }
     for (int k = 0; k <= N; ++k) {
       fstage_t* s = &P->st[k];
       for (int i = 0; i < fnz(P, k); ++i) {
-        double H = rho;
-        const double g = rho * s->dz[i] + fgrad(P, k, i);
+        const double hq = rho + fhq(P, k, i);
+        double H = hq;
+        const double g = hq * s->dz[i] + fgrad(P, k, i);
         if (isfinite(s->Lb[i])) H += s->ql[i] / (s->dz[i] - s->Lb[i]) + s->qu[i] / (s->Ub[i] - s->dz[i]);
         s->H[i] = H; s->g[i] = g;
       }
+    }
+    if (P->nn) {   /* the row's predictor term c gamma in the terminal gradient */
+      P->hatl = P->hatu = P->haql = P->haqu = 0.0;
+      const double gam = P->hql * (P->rs * P->hr0l) / P->htl - P->hqu * (P->rs * P->hr0u) / P->htu;
+      for (int i = 0; i < nx; ++i) P->st[N].g[i] += P->hg[i] * gam;
     }
     if (fnewton(P, 1, nu_new)) { status = -1; break; }
     fratio_t ma = {1.0, 1.0};
@@ -529,6 +689,15 @@ static int fqp(fprob_t* P, int* iters) {
         fr_add(&ma, s->qu[i], dlu);
       }
     }
+    if (P->nn) {
+      double dtl, dtu, dql, dqu;
+      frow_dir(P, 0.0, &dtl, &dtu, &dql, &dqu);
+      P->hatl = dtl; P->hatu = dtu; P->haql = dql; P->haqu = dqu;
+      fr_add(&ma, P->htl, dtl);
+      fr_add(&ma, P->htu, dtu);
+      fr_add(&ma, P->hql, dql);
+      fr_add(&ma, P->hqu, dqu);
+    }
     const double aa = ma.n / ma.d;
     double muaff = 0.0;
     for (int k = 0; k <= N; ++k) {
@@ -540,6 +709,8 @@ static int fqp(fprob_t* P, int* iters) {
         muaff += (tl + aa * d) * (s->ql[i] + aa * dll) + (tu - aa * d) * (s->qu[i] + aa * dlu);
       }
     }
+    if (P->nn)
+      muaff += (P->htl + aa * P->hatl) * (P->hql + aa * P->haql) + (P->htu + aa * P->hatu) * (P->hqu + aa * P->haqu);
     muaff /= (double)nbox;
     double sig = muaff / mu;
     sig = sig * sig * sig;
@@ -552,8 +723,14 @@ static int fqp(fprob_t* P, int* iters) {
         const double tl = s->dz[i] - s->Lb[i], tu = s->Ub[i] - s->dz[i], itl = 1.0 / tl, itu = 1.0 / tu, d = s->daff[i];
         const double dll = -s->ql[i] - s->ql[i] * d * itl, dlu = -s->qu[i] + s->qu[i] * d * itu;
         const double rl = smu - tl * s->ql[i] - d * dll, ru = smu - tu * s->qu[i] + d * dlu;
-        s->g[i] = rho * s->dz[i] + fgrad(P, k, i) - s->ql[i] - rl * itl + s->qu[i] + ru * itu;
+        s->g[i] = (rho + fhq(P, k, i)) * s->dz[i] + fgrad(P, k, i) - s->ql[i] - rl * itl + s->qu[i] + ru * itu;
       }
+    }
+    if (P->nn) {   /* the row's Mehrotra-corrected term */
+      const double rl = P->rs * P->hr0l, ru = P->rs * P->hr0u;
+      const double rcl = smu - P->htl * P->hql - P->hatl * P->haql, rcu = smu - P->htu * P->hqu - P->hatu * P->haqu;
+      const double gam = -P->hql + P->hqu - (rcl - P->hql * rl) / P->htl + (rcu - P->hqu * ru) / P->htu;
+      for (int i = 0; i < nx; ++i) P->st[N].g[i] += P->hg[i] * gam;
     }
     if (fnewton(P, 0, nu_new)) { status = -1; break; }
     fratio_t mx = {1.0, o->ipm_tau};
@@ -572,6 +749,14 @@ static int fqp(fprob_t* P, int* iters) {
         fr_add(&mx, s->qu[i], dlu);
       }
     }
+    double rdtl = 0, rdtu = 0, rdql = 0, rdqu = 0;
+    if (P->nn) {
+      frow_dir(P, smu, &rdtl, &rdtu, &rdql, &rdqu);
+      fr_add(&mx, P->htl, rdtl);
+      fr_add(&mx, P->htu, rdtu);
+      fr_add(&mx, P->hql, rdql);
+      fr_add(&mx, P->hqu, rdqu);
+    }
     const double alpha = fmin(1.0, o->ipm_tau * (mx.n / mx.d));
     for (int k = 0; k <= N; ++k) {
       fstage_t* s = &P->st[k];
@@ -587,6 +772,10 @@ static int fqp(fprob_t* P, int* iters) {
         s->dz[i] += alpha * d;
       }
     }
+    if (P->nn) {
+      P->htl += alpha * rdtl; P->htu += alpha * rdtu;
+      P->hql += alpha * rdql; P->hqu += alpha * rdqu;
+    }
     for (int j = 0; j < ne; ++j) P->qnu[j] += alpha * (nu_new[j] - P->qnu[j]);
     P->rs *= (1.0 - alpha);
   }
@@ -596,7 +785,10 @@ static int fqp(fprob_t* P, int* iters) {
   {
     double lam[FX];
     const fstage_t* sN = &P->st[N];
-    for (int i = 0; i < nx; ++i) lam[i] = rho * sN->dz[i] - sN->ql[i] + sN->qu[i];
+    for (int i = 0; i < nx; ++i) {
+      lam[i] = (rho + fhq(P, N, i)) * sN->dz[i] + fgrad(P, N, i) - sN->ql[i] + sN->qu[i];
+      if (P->nn) lam[i] += P->hg[i] * (P->hqu - P->hql);
+    }
     for (int j = 0; j < ne; ++j) lam[P->ei[j]] += P->qnu[j];
     for (int k = N - 1; k >= 0; --k) {
       fstage_t* s = &P->st[k];
@@ -604,7 +796,7 @@ static int fqp(fprob_t* P, int* iters) {
       if (k == 0) break;
       double ln[FX];
       for (int i = 0; i < nx; ++i) {
-        double t = rho * s->dz[i] + fgrad(P, k, i) - s->ql[i] + s->qu[i];
+        double t = (rho + fhq(P, k, i)) * s->dz[i] + fgrad(P, k, i) - s->ql[i] + s->qu[i];
         for (int q = 0; q < nx; ++q) t += s->A[q * nx + i] * lam[q];
         ln[i] = t;
       }
@@ -651,16 +843,22 @@ static double fmerit(const fprob_t* P, double alpha) {
   }
   val += P->wbnd * viol;
   fstate_at(P, 0, alpha, xk, uk);
-  for (int i = 0; i < nx; ++i) val += P->c0[i] * xk[i];
+  if (P->track) val += ftrack(P, 0, xk, uk);
+  else for (int i = 0; i < nx; ++i) val += P->c0[i] * xk[i];
   for (int k = 0; k < N; ++k) {
     ft_rk4(P->nq, xk, uk, phi);
     fstate_at(P, k + 1, alpha, xn, un);
     for (int i = 0; i < nx; ++i) val += P->st[k].wpi[i] * fabs(phi[i] - xn[i]);
-    if (k + 1 < N) for (int i = 0; i < nx; ++i) val += P->cp[i] * xn[i];
+    if (P->track) val += ftrack(P, k + 1, xn, un);
+    else if (k + 1 < N) for (int i = 0; i < nx; ++i) val += P->cp[i] * xn[i];
     memcpy(xk, xn, sizeof(xk));
     memcpy(uk, un, sizeof(uk));
   }
   for (int j = 0; j < P->ne; ++j) val += P->wnu[j] * fabs(xk[P->ei[j]] - P->ev[j]);
+  if (P->nn) {   /* the terminal row's violation at the trial state, weighted like the boxes */
+    const double hv = nn_row(P->nn, P->nq, xk, NULL);
+    val += P->wbnd * (fmax(0.0, P->nn->lh - hv) + fmax(0.0, hv - P->nn->uh));
+  }
   return val;
 }
 
@@ -678,7 +876,11 @@ static void fsqp(fprob_t* P, vboc_result_t* res) {
     flinearize(P);
     fresiduals(P, &rstat, &req, &rineq, &rcomp);
     if (!isfinite(rstat) || !isfinite(req)) { status = 1; break; }
-    if (rstat < o->tol_stat && req < o->tol_eq && rineq < o->tol_ineq && rcomp < o->tol_comp) { status = 0; break; }
+    if (P->rti && it == 1) { status = 0; break; }   /* SQP_RTI: one QP and its full step */
+    if (!P->rti && rstat < o->tol_stat && req < o->tol_eq && rineq < o->tol_ineq && rcomp < o->tol_comp) {
+      status = 0;
+      break;
+    }
     if (it >= o->max_iter) { status = 2; break; }
     int qit = 0;
     const int qs = fqp(P, &qit);
@@ -690,15 +892,18 @@ static void fsqp(fprob_t* P, vboc_result_t* res) {
       if (k < N) for (int i = 0; i < nx; ++i) s->wpi[i] = fwupd(s->wpi[i], s->qpi[i]);
       for (int i = 0; i < fnz(P, k); ++i) lmax = fmax(lmax, fmax(s->ql[i], s->qu[i]));
     }
+    if (P->nn) lmax = fmax(lmax, fmax(P->hql, P->hqu));
     for (int j = 0; j < P->ne; ++j) P->wnu[j] = fwupd(P->wnu[j], P->qnu[j]);
     P->wbnd = fwupd(P->wbnd, lmax);
-    const double phi0 = fmerit(P, 0.0);
     double alpha = 1.0;
-    for (;;) {
-      const double pa = fmerit(P, alpha);
-      if (pa < phi0) break;
-      if (alpha * o->alpha_reduction < o->alpha_min) break;
-      alpha *= o->alpha_reduction;
+    if (!P->rti) {
+      const double phi0 = fmerit(P, 0.0);
+      for (;;) {
+        const double pa = fmerit(P, alpha);
+        if (pa < phi0) break;
+        if (alpha * o->alpha_reduction < o->alpha_min) break;
+        alpha *= o->alpha_reduction;
+      }
     }
     for (int k = 0; k <= N; ++k) {
       fstage_t* s = &P->st[k];
@@ -713,6 +918,10 @@ static void fsqp(fprob_t* P, vboc_result_t* res) {
       if (k < N) for (int i = 0; i < nx; ++i) s->pi[i] += alpha * (s->qpi[i] - s->pi[i]);
     }
     for (int j = 0; j < P->ne; ++j) P->tnu[j] += alpha * (P->qnu[j] - P->tnu[j]);
+    if (P->nn) {
+      P->hll += alpha * (P->hql - P->hll);
+      P->hlu += alpha * (P->hqu - P->hlu);
+    }
     if (!isfinite(P->st[0].x[nx - 1])) { status = 1; break; }
   }
   res->status = status;
@@ -783,6 +992,69 @@ int vboc_oracle_ft_solve_batch(int nq, int B, int Nmax, const int* N, const doub
                                        ubu + (size_t)b * nq, lbx0 + (size_t)b * nxr, ubx0 + (size_t)b * nxr,
                                        lbxe + (size_t)b * nxr, ubxe + (size_t)b * nxr, opts, x_out + xo,
                                        u_out + uo, res + b);
+    if (r == -2) { res[b].status = 5; res[b].sqp_iter = 0; res[b].qp_iter = 0; res[b].cost = NAN; }
+    else if (r) err |= 1;
+  }
+  return err ? -1 : 0;
+}
+
+/* Safe-MPC OCP_solve (HardTerm, :163-181): x_0 fixed, boxes, tracking cost, terminal NN row, SQP or SQP_RTI.
+   x [N + 1][2 nq] and u [N][nq] without the dt column; hrow (may be NULL) gets h(x_N) of the result. */
+int vboc_oracle_mpc_solve(int nq, int N, double h, const double* x0, const double* x_guess, const double* u_guess,
+                          const double* xlb, const double* xub, const double* ulb, const double* uub,
+                          const double* xNlb, const double* xNub, const double* W, const double* We,
+                          const double* yref, const double* yref_e, double cs, const vboc_mpc_nn_t* nn, int rti,
+                          const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* hrow) {
+  if (nq < 1 || nq > FQ || N < 1) return -1;
+  const int n2 = 2 * nq, nx = n2 + 1, nu = nq;
+  for (int i = 0; i < n2; ++i) if (!(xlb[i] < xub[i]) || !(xNlb[i] < xNub[i])) return -2;
+  for (int a = 0; a < nu; ++a) if (!(ulb[a] < uub[a])) return -2;
+  if (nn && !(nn->lh <= nn->uh)) return -2;
+  fprob_t P;
+  memset(&P, 0, sizeof(P));
+  P.nq = nq; P.nx = nx; P.nu = nu; P.N = N; P.o = *opts;
+  for (int i = 0; i < n2; ++i) {
+    P.xlb[i] = xlb[i]; P.xub[i] = xub[i]; P.xNlb[i] = xNlb[i]; P.xNub[i] = xNub[i];
+    P.x0lb[i] = P.x0ub[i] = x0[i];
+  }
+  P.xlb[n2] = P.xNlb[n2] = -INFINITY; P.xub[n2] = P.xNub[n2] = INFINITY;   /* dt: pinned by x_0 and the dynamics */
+  P.x0lb[n2] = P.x0ub[n2] = h;
+  for (int a = 0; a < nu; ++a) { P.ulb[a] = ulb[a]; P.uub[a] = uub[a]; }
+  P.track = 1; P.rti = rti; P.cs = cs; P.nn = nn;
+  for (int i = 0; i < n2; ++i) { P.wq[i] = W[i]; P.yr[i] = yref[i]; P.we[i] = We[i]; P.yre[i] = yref_e[i]; }
+  for (int a = 0; a < nu; ++a) { P.wq[nx + a] = W[n2 + a]; P.yr[nx + a] = yref[n2 + a]; }
+  P.st = (fstage_t*)calloc((size_t)N + 1, sizeof(fstage_t));
+  if (!P.st) return -3;
+  for (int k = 0; k <= N; ++k) {
+    for (int i = 0; i < n2; ++i) P.st[k].x[i] = x_guess[k * n2 + i];
+    P.st[k].x[n2] = h;
+    if (k < N) for (int a = 0; a < nu; ++a) P.st[k].u[a] = u_guess[k * nu + a];
+  }
+  for (int i = 0; i < n2; ++i) P.st[0].x[i] = x0[i];
+  fsqp(&P, res);
+  for (int k = 0; k <= N; ++k) {
+    for (int i = 0; i < n2; ++i) x_out[k * n2 + i] = P.st[k].x[i];
+    if (k < N) for (int a = 0; a < nu; ++a) u_out[k * nu + a] = P.st[k].u[a];
+  }
+  if (hrow) *hrow = nn ? nn_row(nn, nq, P.st[N].x, NULL) : 0.0;
+  free(P.st);
+  return 0;
+}
+
+int vboc_oracle_mpc_solve_batch(int nq, int B, int N, double h, const double* x0, const double* x_guess,
+                                const double* u_guess, const double* xlb, const double* xub, const double* ulb,
+                                const double* uub, const double* xNlb, const double* xNub, const double* W,
+                                const double* We, const double* yref, const double* yref_e, double cs,
+                                const vboc_mpc_nn_t* nn, int rti, const vboc_opts_t* opts, int nthreads,
+                                double* x_out, double* u_out, vboc_result_t* res, double* hrow) {
+  const int n2 = 2 * nq;
+  int err = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(| : err)
+  for (int b = 0; b < B; ++b) {
+    const size_t xo = (size_t)b * (N + 1) * n2, uo = (size_t)b * N * nq;
+    const int r = vboc_oracle_mpc_solve(nq, N, h, x0 + (size_t)b * n2, x_guess + xo, u_guess + uo, xlb, xub, ulb,
+                                        uub, xNlb, xNub, W, We, yref, yref_e, cs, nn, rti, opts, x_out + xo,
+                                        u_out + uo, res + b, hrow ? hrow + b : NULL);
     if (r == -2) { res[b].status = 5; res[b].sqp_iter = 0; res[b].qp_iter = 0; res[b].cost = NAN; }
     else if (r) err |= 1;
   }

@@ -156,3 +156,80 @@ def slsqp_free_time(b, i, maxiter=500, start=None):
     r = minimize(lambda z: c @ z, z0, jac=lambda z: c, bounds=bounds, constraints=[dict(type="eq", fun=eq, jac=eqjac)],
                  method="SLSQP", options=dict(maxiter=maxiter, ftol=1e-12))
     return r.fun, bool(r.success), float(np.abs(eq(r.x)).max()), X(r.x)[0]
+
+
+def slsqp_mpc(spec, x0, start, params=None, mean=0.0, std=1.0, maxiter=300):
+    """The Safe-MPC OCP (VBOC/Safe MPC/triplependulum_class_vboc.py:91-240, vboc_amd.safempc.MpcSpec) as an
+    independent NLP for scipy SLSQP: decision vector (u_0..u_{N-1}, x_1..x_N), x_0 fixed, equality constraints
+    x_{k+1} = RK4(x_k, u_k; time_step) of the 6-state model (golden-pinned oracle.rk4 / rk4_sens), boxes, and
+    with params the terminal row h(x_N) = NN(x_N) - max(|x_N[2:]|, 1e-3) >= 0 (vboc_amd.safempc.nn_row, its
+    gradient by central differences).  Objective: the LINEAR_LS cost with stage costs scaled by spec.cost_scale.
+    start = (x [N+1, 6], u [N, 3]).  Returns (x, u, cost, scipy result)."""
+    from vboc_amd.safempc import nn_row
+    N, h, nx, nu = spec.N, spec.time_step, 6, 3
+    x0 = np.asarray(x0, dtype=np.float64)
+    W, We, yr, yre, cs = spec.W, spec.W_e, spec.yref, spec.yref_e, spec.cost_scale
+    nv = N * nu + N * nx
+
+    def unpack(z):
+        return z[:N * nu].reshape(N, nu), np.vstack([x0, z[N * nu:].reshape(N, nx)])
+
+    def cost(z):
+        U, X = unpack(z)
+        c = 0.0
+        for k in range(N):
+            d = np.r_[X[k], U[k]] - yr
+            c += cs * 0.5 * float(d @ (W * d))
+        d = X[N] - yre
+        return c + 0.5 * float(d @ (We * d))
+
+    def grad(z):
+        U, X = unpack(z)
+        g = np.zeros(nv)
+        for k in range(N):
+            d = np.r_[X[k], U[k]] - yr
+            g[k * nu:(k + 1) * nu] = cs * W[nx:] * d[nx:]
+            if k > 0:
+                g[N * nu + (k - 1) * nx:N * nu + k * nx] += cs * W[:nx] * d[:nx]
+        g[N * nu + (N - 1) * nx:] += We * (X[N] - yre)
+        return g
+
+    def eq(z):
+        U, X = unpack(z)
+        return np.concatenate([X[k + 1] - oracle.rk4(3, h, X[k], U[k]) for k in range(N)])
+
+    def eqjac(z):
+        U, X = unpack(z)
+        J = np.zeros((N * nx, nv))
+        for k in range(N):
+            _, A, B = oracle.rk4_sens(3, h, X[k], U[k])
+            r = slice(k * nx, (k + 1) * nx)
+            J[r, k * nu:(k + 1) * nu] = -B
+            if k > 0:
+                J[r, N * nu + (k - 1) * nx:N * nu + k * nx] = -A
+            J[r, N * nu + k * nx:N * nu + (k + 1) * nx] += np.eye(nx)
+        return J
+
+    cons = [dict(type="eq", fun=eq, jac=eqjac)]
+    if params is not None:
+        def row(z):
+            return np.array([nn_row(params, mean, std, unpack(z)[1][N])])
+
+        def rowjac(z):
+            xN = unpack(z)[1][N]
+            J = np.zeros((1, nv))
+            for j in range(nx):
+                e = np.zeros(nx)
+                e[j] = 1e-6
+                J[0, N * nu + (N - 1) * nx + j] = (nn_row(params, mean, std, xN + e) -
+                                                   nn_row(params, mean, std, xN - e)) / 2e-6
+            return J
+        cons.append(dict(type="ineq", fun=row, jac=rowjac))
+    bounds = [(spec.umin[a], spec.umax[a]) for _ in range(N) for a in range(nu)]
+    bounds += [(spec.xmin[j], spec.xmax[j]) for _ in range(N) for j in range(nx)]
+    xs, us = start
+    z0 = np.r_[np.asarray(us, dtype=np.float64).ravel(), np.asarray(xs, dtype=np.float64)[1:].ravel()]
+    r = minimize(cost, z0, jac=grad, bounds=bounds, constraints=cons, method="SLSQP",
+                 options=dict(maxiter=maxiter, ftol=1e-14))
+    U, X = unpack(r.x)
+    return X, U, cost(r.x), r

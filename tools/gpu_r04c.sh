@@ -4,7 +4,8 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:-r04c}; mkdir -p $O
 cd $R &&
-timeout -k 10 600 python3 -u -m pytest tests/test_dg_device.py -m gpu -v --timeout 300 --timeout-method thread -k "parked or fixture or streamed" > $O/pytest_dg.log 2>&1; echo "pytest_dg exit $?"
+timeout -k 10 600 python3 -u -m pytest tests/test_dg_device.py -m gpu -v --timeout 300 --timeout-method thread -k "parked or fixture or streamed" > $O/pytest_dg.log 2>&1
+rc=$?; echo "pytest_dg exit $rc"; [ $rc -le 1 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp &&
 timeout -k 10 300 python3 $R/tools/dg_probe.py --B 60000 --groups 0 --park 1 0 --save $O/stats60k > $O/probe_park.jsonl 2> $O/probe_park.err && cat $O/probe_park.jsonl &&
 VBOC_LIB=$R/vboc_amd/variants/libvboc_amd_aclpass.so timeout -k 10 200 python3 $R/tools/dg_probe.py --B 60000 --groups 0 --park 1 > $O/probe_aclpass.jsonl 2> $O/probe_aclpass.err && cat $O/probe_aclpass.jsonl &&
