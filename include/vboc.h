@@ -25,6 +25,9 @@
  *                             state machine of VBOC/triplependulum_vboc.py:19-370 (fan-out :399-405) /
  *                             VBOC/doublependulum_vboc.py:19-403, with its OCP_solve calls (:110,262) and
  *                             twin-integrator steps (:346-353), run on the device
+ *   vboc_mpc_solve_batch   <- one OCPtriplependulumHardTerm.OCP_solve(x0, x_sol_guess, u_sol_guess) per problem:
+ *                             Safe MPC with the VBOC network as terminal constraint (VBOC/Safe MPC/
+ *                             triplependulum_class_vboc.py:91-240; drivers hard_terminal_constraints/3dof_sym.py)
  *   vboc_set_path_constraint <- model.con_h_expr + constraints.lh / uh of the Cartesian double pendulum
  *                             (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160)
  *   vboc_destroy           <- solver object destruction (acados_template __del__ -> free)
@@ -266,6 +269,37 @@ typedef struct {
   int* qp_iter;
 } vboc_hjr_batch_t;
 int vboc_hjr_solve_batch(vboc_handle h, const vboc_hjr_batch_t* batch, void* stream);
+
+/* Safe MPC with the VBOC network as terminal constraint: OCPtriplependulumHardTerm.OCP_solve(x0, x_sol_guess,
+ * u_sol_guess) (VBOC/Safe MPC/triplependulum_class_vboc.py:163-181; the OCP :91-161, the row :197-240) for every
+ * x0 of a batch, one problem per wave (ft.h, the free-time solver with the tracking cost and the terminal row):
+ * model MODELtriplependulum on N intervals of h = time_step; LINEAR_LS cost 1/2 |[x; u] - yref|^2_W (stages,
+ * times cost_scale) + 1/2 |x_N - yref_e|^2_We, Gauss-Newton Hessian; x_0 fixed; path boxes lbx/ubx, lbu/ubu,
+ * terminal box lbx_e/ubx_e; row lh <= NN(x_N) - max(|x_N[2:]|, 1e-3) <= uh with NeuralNetDIR(2nq, hidden, 1)
+ * (hidden 0: no row); rti 1 = SQP_RTI (one QP, the full step; status 0 or 4), 0 = SQP with the handle's options.
+ * Device pointers except the OCP's constant vectors W, We, yref, yref_e (host); asynchronous on `stream`.  The
+ * handle: nq = 3, nmax >= N.
+ *   x0[B][2nq], x_guess[B][N+1][2nq], u_guess[B][N][nq]; lbx..ubx_e [2nq] / [nq], W[3nq], We[2nq], yref[3nq],
+ *   yref_e[2nq]; W0[hidden][2nq], b0[hidden], W1[hidden][hidden], b1[hidden], W2[hidden], b2[1] (FP64 copies of
+ *   model.parameters()); outputs status[B], x_out[B][N+1][2nq], u_out[B][N][nq], cost[B], sqp_iter[B],
+ *   qp_iter[B], h_out[B] (the row at the result's x_N; may be NULL).  hidden <= 512. */
+typedef struct {
+  int B, N, rti, hidden;
+  double h, cost_scale;
+  const double *x0, *x_guess, *u_guess;
+  const double *lbx, *ubx, *lbu, *ubu, *lbx_e, *ubx_e;
+  const double *W, *We, *yref, *yref_e;   /* host */
+  const double *W0, *b0, *W1, *b1, *W2, *b2;
+  double mean, std, lh, uh;
+  int* status;
+  double* x_out;
+  double* u_out;
+  double* cost;
+  int* sqp_iter;
+  int* qp_iter;
+  double* h_out;
+} vboc_mpc_batch_t;
+int vboc_mpc_solve_batch(vboc_handle h, const vboc_mpc_batch_t* batch, void* stream);
 
 /* Device time of the last vboc_solve_batch* call's solver kernel in milliseconds (HIP events on
  * the call's stream) and the number of kernel launches it used. */

@@ -307,3 +307,29 @@ def test_device_testing_set_at_scale():
     assert X.shape[0] >= 0.99 * 10000
     assert (X[:, :3] >= sysd.q_min - 1e-9).all() and (X[:, :3] <= sysd.q_max + 1e-9).all()
     assert (np.abs(X[:, 3:]) <= sysd.v_max + 1e-6).all()
+
+
+@pytest.mark.gpu
+def test_handle_refuses_calls_while_an_async_launch_runs():
+    """while a vboc_data_generation_async launch runs on a handle, the entry points that would reuse its
+    buffers refuse (VbocError); after data_generation_wait the handle works again, for consecutive launches too."""
+    import torch
+    from vboc_amd import lib
+    s = lib.Solver(3, 120)
+    ids = torch.arange(0, 256, dtype=torch.int64, device="cuda:0")
+    a = s.data_generation_device(ids)
+    b = s.data_generation_device(ids)                    # a second synchronous launch on the same handle
+    assert torch.equal(a["row_cnt"], b["row_cnt"])
+    s.set_option("wave_groups", 0)
+    flags = torch.zeros(256, dtype=torch.int32, device="cuda:0")
+    cancel = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    out = s.data_generation_device(ids, done_flag=flags, cancel=cancel, wait=False)
+    assert s.get_option("dg_busy") == 1.0
+    with pytest.raises(lib.VbocError, match="still running"):
+        s.set_option("wave_groups", 0)
+    with pytest.raises(lib.VbocError, match="still running"):
+        s.data_generation_device(ids)
+    s.data_generation_wait(out)
+    assert s.get_option("dg_busy") == 0.0
+    s.set_option("wave_groups", 0)
+    assert torch.equal(out["row_cnt"], a["row_cnt"])

@@ -92,3 +92,112 @@ def test_rti_is_one_qp_with_the_full_step():
     x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, rti=True)
     assert (r["status"] == 0).all() and (r["sqp_iter"] == 1).all() and (r["qp_iter"] > 0).all()
     assert (x[:, 0] == x0).all()
+
+
+def _oracle_solve(sp, P, rti):
+    def solve(x0, xg, ug):
+        x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, rti=rti)
+        return dict(status=r["status"], x=x, u=u)
+    return solve
+
+
+def _oracle_rk4(sp):
+    return lambda X, U: np.stack([oracle.rk4(3, sp.time_step, X[i], U[i]) for i in range(X.shape[0])])
+
+
+def test_closed_loop_driver_on_the_oracle():
+    """vboc_amd.safempc.simulate_batch (the reference's simulate(p), hard_terminal_constraints/3dof_sym.py:15-72)
+    over a batch: the same per-problem result as running each problem alone, and the plant follows the applied
+    controls."""
+    from vboc_amd.safempc import simulate_batch
+    P = _net()
+    sp, x0, xg, ug = _states(4, seed=3)
+    x0[:, 3:] = 0.0                                   # the drivers start at rest (x0[:nu] = data[p])
+    xg = np.repeat(x0[:, None, :], sp.N + 1, 1)
+    res, simX, solves = simulate_batch(_oracle_solve(sp, P, True), _oracle_rk4(sp), sp, x0, xg, ug, tot_steps=12)
+    assert solves >= 4 and (res >= 0).all() and (res <= 11).all()
+    for b in range(2):
+        r1, X1, _ = simulate_batch(_oracle_solve(sp, P, True), _oracle_rk4(sp), sp, x0[b:b + 1], xg[b:b + 1],
+                                   ug[b:b + 1], tot_steps=12)
+        assert r1[0] == res[b]
+        np.testing.assert_array_equal(X1[0], simX[b])
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU: vboc_mpc_solve_batch (ft.h with the tracking cost and the terminal row) against the oracle
+# ------------------------------------------------------------------------------------------------
+def _gpu(sp, P, x0, xg, ug, rti, max_iter=None):
+    import torch
+    from vboc_amd import lib
+    s = lib.Solver(3, sp.N)
+    s.set_option("levenberg_marquardt", sp.lm)
+    s.set_option("nlp_solver_tol_stat", 1e-6)
+    s.set_option("qp_solver_tol_stat", 1e-8)
+    if max_iter:
+        s.set_option("nlp_solver_max_iter", max_iter)
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device="cuda:0")
+    prm = [T(p) for p in P] if P is not None else None
+    out = s.mpc_solve_device(sp, T(x0), T(xg), T(ug), prm, MEAN, STD, rti=rti)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_row", [False, True])
+def test_gpu_rti_matches_oracle(with_row):
+    """SQP_RTI (the Safe-MPC drivers' mode) on 128 states: status, the QP's iteration count and the step agree with
+    the oracle (the network's sums run in another order on the GPU: rounding level)."""
+    P = _net() if with_row else None
+    sp, x0, xg, ug = _states(128, seed=5)
+    g = _gpu(sp, P, x0, xg, ug, rti=True)
+    x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, rti=True)
+    assert (g["status"] == r["status"]).mean() >= 0.98
+    assert (g["qp_iter"] == r["qp_iter"]).mean() >= 0.95
+    ok = (g["status"] == 0) & (r["status"] == 0)
+    assert ok.mean() >= 0.9
+    assert np.abs(g["u"][ok] - u[ok]).max() < 1e-6 and np.median(np.abs(g["x"][ok] - x[ok]).max(axis=(1, 2))) < 1e-9
+    if with_row:
+        assert np.abs(g["h"][ok] - h[ok]).max() < 1e-8
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_row", [False, True])
+def test_gpu_sqp_matches_oracle(with_row):
+    """Full SQP (nlp_solver_max_iter 200) on 96 states at the section-3 bars: status >= 98 %, SQP iterations >= 95 %,
+    cost and x_N of problems converged on both: median <= 1e-9, max <= 2e-3 (relative to the cost)."""
+    P = _net() if with_row else None
+    sp, x0, xg, ug = _states(96, seed=7)
+    g = _gpu(sp, P, x0, xg, ug, rti=False, max_iter=200)
+    o = oracle.default_opts(lm=sp.lm, tol_stat=1e-6, qp_tol_stat=1e-8, max_iter=200)
+    x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, opts=o)
+    assert (g["status"] == r["status"]).mean() >= 0.98, (g["status"], r["status"])
+    assert (g["sqp_iter"] == r["sqp_iter"]).mean() >= 0.95, (g["sqp_iter"], r["sqp_iter"])
+    both = (g["status"] == 0) & (r["status"] == 0)
+    assert both.sum() >= 40
+    dc = np.abs(g["cost"] - r["cost"])[both] / np.abs(r["cost"][both])
+    dx = np.abs(g["x"][:, -1] - x[:, -1]).max(axis=1)[both]
+    assert np.median(dc) <= 1e-9 and dc.max() <= 2e-3, (np.median(dc), dc.max())
+    assert np.median(dx) <= 1e-9 and dx.max() <= 2e-3
+
+
+@pytest.mark.gpu
+def test_gpu_closed_loop_matches_oracle():
+    """The Safe-MPC closed loop (simulate_batch, SQP_RTI, 60 steps) of 48 initial states at rest on the GPU drop-in
+    class against the same driver on the oracle: the same stopping step for >= 95 % of the states."""
+    from vboc_amd.safempc import OCPtriplependulumHardTerm, simulate_batch
+    from vboc_amd import lib
+    P = _net()
+    sp, x0, xg, ug = _states(48, seed=9)
+    x0[:, 3:] = 0.0
+    xg = np.repeat(x0[:, None, :], sp.N + 1, 1)
+    ocp = OCPtriplependulumHardTerm("SQP_RTI", sp.time_step, sp.tot_time, P, MEAN, STD)
+    rk4 = lambda X, U: lib.rk4_host(3, sp.time_step, X, U)
+    rg, Xg, _ = simulate_batch(ocp.solve_batch, rk4, sp, x0, xg, ug, tot_steps=60)
+    ro, Xo, _ = simulate_batch(_oracle_solve(sp, P, True), _oracle_rk4(sp), sp, x0, xg, ug, tot_steps=60)
+    assert (rg == ro).mean() >= 0.95, (rg, ro)
+    same = rg == ro
+    assert np.abs(Xg[same] - Xo[same]).max() < 1e-6
+    # the drop-in batch-of-one call gives the batched call's result
+    st = ocp.OCP_solve(x0[0], xg[0], ug[0])
+    r = ocp.solve_batch(x0[:1], xg[:1], ug[:1])
+    assert st == r["status"][0] and np.array_equal(ocp.ocp_solver.get(3, "x"), r["x"][0, 3])

@@ -40,6 +40,20 @@ struct FtL {
   static constexpr long long region_doubles(int nmax) { return (long long)REC * (nmax + 1); }
 };
 
+// The Safe-MPC tracking OCP on this solver (vboc_mpc_solve_batch; VBOC/Safe MPC/triplependulum_class_vboc.py:91-240,
+// restated in oracle/vboc_oracle_ft.c vboc_oracle_mpc_solve): LINEAR_LS cost with its Gauss-Newton Hessian
+// (weights wq on [x; u], we at N, stage costs times cs), the dt column pinned by x_0, the terminal row
+// lh <= NN(x_N) - max(|x_N[2:]|, 1e-3) <= uh (NeuralNetDIR(2 nq, hid, 1); W1T = W1 transposed, for coalesced loads),
+// and SQP_RTI.  on == 0: the free-time OCP above, unchanged.
+constexpr int FT_NN_MAX = 512;
+struct MpcArgs {
+  int on, rti, hid;
+  double wq[10], yr[10], we[7], yre[7], cs;
+  const double *W0, *b0, *W1, *W1T, *b1, *W2, *b2;
+  double mean, std, lh, uh;
+  double* hrow;   // [B] h(x_N) of each result (nullptr: not written)
+};
+
 template <int NQ>
 struct FtShared {
   static constexpr int NX = FtL<NQ>::NX, NU = FtL<NQ>::NU;
@@ -49,6 +63,9 @@ struct FtShared {
   double tnu[NX], wnu[NX], qnu[NX], nun[NX], S[NX * NX], lin_e[NX];
   double wbnd, rs;
   int qp_fail;
+  // Safe-MPC terminal row: value, gradient, QP slacks / duals, their affine directions, the NLP multipliers
+  double hv, hg[NX], hL, hU, htl, htu, hql, hqu, hr0l, hr0u, hatl, hatu, haql, haqu, hll, hlu;
+  double nn1[FT_NN_MAX], nn2[FT_NN_MAX];   // hidden activations / backward weights of the row's network
 };
 
 __device__ __forceinline__ double ft_wmax(double v) {
@@ -161,13 +178,95 @@ __device__ __forceinline__ void ft_chol_solve(const double* L, int m, double* b)
 template <int NQ>
 struct Ft {
   using L = FtL<NQ>;
-  static constexpr int NX = L::NX, NU = L::NU, NZ = L::NZ;
+  static constexpr int NX = L::NX, NU = L::NU, NZ = L::NZ, N2 = 2 * NQ;
   FtShared<NQ>& sh;
   double* g;     // this workgroup's stage records
   const Opts& o;
   int t;
+  const MpcArgs& mp;
 
-  __device__ Ft(FtShared<NQ>& s_, double* g_, const Opts& o_, int t_) : sh(s_), g(g_), o(o_), t(t_) {}
+  __device__ Ft(FtShared<NQ>& s_, double* g_, const Opts& o_, int t_, const MpcArgs& mp_)
+      : sh(s_), g(g_), o(o_), t(t_), mp(mp_) {}
+
+  // ---- Safe-MPC terminal row (all lanes; x uniform): h(x) = NN(z(x)) - vn(x), grad (NX, uniform) if asked ----
+  // Hidden unit i of a layer lives on lane i mod 64; layer 2 streams W1T row by row (64 consecutive doubles per
+  // load across the wave), the backward pass W1 row by row; the few reductions are shuffles.
+  __device__ double nn_row(const double* x, double* grad) {
+    const int H = mp.hid;
+    double ss = 0.0;
+    for (int j = 2; j < N2; ++j) ss += x[j] * x[j];    // norm_2(x[2:]): theta_3 included, as the reference
+    const double nrm = sqrt(ss), vn = nrm > 1e-3 ? nrm : 1e-3;
+    double z[N2];
+    for (int j = 0; j < NQ; ++j) z[j] = (x[j] - mp.mean) / mp.std;
+    for (int j = NQ; j < N2; ++j) z[j] = x[j] / vn;
+    __syncthreads();   // the buffers may still be read by a previous evaluation
+    for (int i = t; i < H; i += 64) {
+      double a = 0.0;
+      for (int j = 0; j < N2; ++j) a += mp.W0[i * N2 + j] * z[j];
+      a += mp.b0[i];
+      sh.nn1[i] = a > 0.0 ? a : 0.0;
+    }
+    __syncthreads();
+    constexpr int MQ = FT_NN_MAX / 64;
+    double acc[MQ];
+    for (int m = 0; m < MQ; ++m) acc[m] = 0.0;
+    for (int j = 0; j < H; ++j) {
+      const double a1 = sh.nn1[j];
+      const double* row = mp.W1T + (long long)j * H;
+      for (int m = 0; m < MQ; ++m) {
+        const int i = t + 64 * m;
+        if (i < H) acc[m] += row[i] * a1;
+      }
+    }
+    double out = 0.0;
+    for (int m = 0; m < MQ; ++m) {
+      const int i = t + 64 * m;
+      if (i < H) {
+        const double a2 = acc[m] + mp.b1[i];
+        if (a2 > 0.0) out += mp.W2[i] * a2;
+        sh.nn2[i] = a2 > 0.0 ? mp.W2[i] : 0.0;   // backward weights W2 [a2 > 0]
+      }
+    }
+    out = ft_wsum(out) + mp.b2[0];
+    if (grad) {
+      __syncthreads();
+      double gz[N2];
+      for (int j = 0; j < N2; ++j) gz[j] = 0.0;
+      for (int m = 0; m < MQ; ++m) {   // g1[j] = sum_i W1[i][j] w_i for the lane's j, then through layer 1
+        const int j = t + 64 * m;
+        if (j >= H) continue;
+        double g1 = 0.0;
+        for (int i = 0; i < H; ++i) g1 += mp.W1[(long long)i * H + j] * sh.nn2[i];
+        if (sh.nn1[j] > 0.0)
+          for (int q = 0; q < N2; ++q) gz[q] += g1 * mp.W0[j * N2 + q];
+      }
+      for (int q = 0; q < N2; ++q) gz[q] = ft_wsum(gz[q]);
+      double dvn[N2];
+      for (int j = 0; j < N2; ++j) dvn[j] = (nrm > 1e-3 && j >= 2) ? x[j] / nrm : 0.0;
+      for (int j = 0; j < N2; ++j) {
+        double v = j < NQ ? gz[j] / mp.std : gz[j] / vn;
+        for (int q = NQ; q < N2; ++q) v -= gz[q] * x[q] / (vn * vn) * dvn[j];
+        grad[j] = v - dvn[j];
+      }
+      grad[N2] = 0.0;   // the pinned dt column
+    }
+    return out - vn;
+  }
+  __device__ __forceinline__ double hq(int k, int i) const {   // Gauss-Newton Hessian diagonal of the tracking cost
+    if (!mp.on) return 0.0;
+    if (k == sh.N) return mp.we[i];
+    return mp.cs * mp.wq[k == 0 ? (i < sh.nf0 ? sh.f0[i] : NX + (i - sh.nf0)) : i];
+  }
+  __device__ __forceinline__ double track(int k, const double* x, const double* u) const {
+    double c = 0.0;
+    if (k == sh.N) {
+      for (int i = 0; i < NX; ++i) { const double d = x[i] - mp.yre[i]; c += mp.we[i] * d * d; }
+      return 0.5 * c;
+    }
+    for (int i = 0; i < NX; ++i) { const double d = x[i] - mp.yr[i]; c += mp.wq[i] * d * d; }
+    for (int a = 0; a < NU; ++a) { const double d = u[a] - mp.yr[NX + a]; c += mp.wq[NX + a] * d * d; }
+    return 0.5 * mp.cs * c;
+  }
 
   __device__ __forceinline__ double* rec(int k) const { return g + (long long)k * L::REC; }
   __device__ __forceinline__ int nz(int k) const { return k == 0 ? sh.nf0 + NU : (k == sh.N ? NX : NX + NU); }
@@ -177,19 +276,26 @@ struct Ft {
     if (k == 0) {
       if (i < sh.nf0) { const int c = sh.f0[i]; v = r[L::X + c]; lb = sh.x0lb[c]; ub = sh.x0ub[c]; }
       else { v = r[L::U + i - sh.nf0]; lb = sh.ulb[i - sh.nf0]; ub = sh.uub[i - sh.nf0]; }
-      return true;
+      return !(isinf(lb) && isinf(ub));
     }
     if (k == sh.N) {
       v = r[L::X + i];
       if (sh.fix[i]) { lb = -INFINITY; ub = INFINITY; return false; }
       lb = sh.xNlb[i]; ub = sh.xNub[i];
-      return true;
+      return !(isinf(lb) && isinf(ub));
     }
     if (i < NX) { v = r[L::X + i]; lb = sh.xlb[i]; ub = sh.xub[i]; }
     else { v = r[L::U + i - NX]; lb = sh.ulb[i - NX]; ub = sh.uub[i - NX]; }
-    return true;
+    return !(isinf(lb) && isinf(ub));   // a free component: the Safe-MPC model's pinned dt
   }
   __device__ __forceinline__ double grad(int k, int i) const {
+    if (mp.on) {   // W ([x; u] - yref) at the current iterate
+      double v, lb, ub;
+      (void)comp(k, i, v, lb, ub);
+      if (k == sh.N) return mp.we[i] * (v - mp.yre[i]);
+      const int w = k == 0 ? (i < sh.nf0 ? sh.f0[i] : NX + (i - sh.nf0)) : i;
+      return mp.cs * mp.wq[w] * (v - mp.yr[w]);
+    }
     if (k == 0) return i < sh.nf0 ? sh.c0[sh.f0[i]] : 0.0;
     if (k == sh.N) return 0.0;
     return i < NX ? sh.cp[i] : 0.0;
@@ -221,6 +327,9 @@ struct Ft {
       sh.c0[2 * NQ] = p[NQ];
       sh.cp[2 * NQ] = p[NQ];
       sh.wbnd = 0.0;
+      sh.hll = sh.hlu = 0.0;
+      sh.hv = 0.0;
+      for (int i = 0; i < NX; ++i) sh.hg[i] = 0.0;
       sh.bad = bad;
     }
     __syncthreads();
@@ -241,6 +350,10 @@ struct Ft {
 
   __device__ double cost() const {
     double c = 0.0;
+    if (mp.on) {
+      for (int k = t; k <= sh.N; k += 64) c += track(k, rec(k) + L::X, rec(k) + L::U);
+      return ft_wsum(c);
+    }
     for (int k = t; k < sh.N; k += 64) {
       const double* r = rec(k);
       for (int i = 0; i < NX; ++i) c += (k == 0 ? sh.c0[i] : sh.cp[i]) * r[L::X + i];
@@ -259,6 +372,13 @@ struct Ft {
         for (int a = 0; a < NU; ++a) uo[(long long)k * NU + a] = r[L::U + a];
     }
     const double c = cost();
+    if (mp.on && mp.hrow) {
+      __syncthreads();
+      double xN[NX];
+      for (int i = 0; i < NX; ++i) xN[i] = rec(N)[L::X + i];
+      const double hv = mp.hid > 0 ? nn_row(xN, nullptr) : 0.0;
+      if (t == 0) mp.hrow[pid] = hv;
+    }
     if (t == 0) {
       in.status[pid] = status;
       in.cost[pid] = c;
@@ -284,6 +404,16 @@ struct Ft {
       }
     }
     __syncthreads();
+    if (mp.hid > 0) {   // the terminal row's value and gradient at x_N
+      double xN[NX], gr[NX];
+      for (int i = 0; i < NX; ++i) xN[i] = rec(N)[L::X + i];
+      const double hv = nn_row(xN, gr);
+      if (t == 0) {
+        sh.hv = hv;
+        for (int i = 0; i < NX; ++i) sh.hg[i] = gr[i];
+      }
+      __syncthreads();
+    }
   }
 
   __device__ void residuals(double& rstat, double& req, double& rineq, double& rcomp) const {
@@ -310,6 +440,7 @@ struct Ft {
         } else {
           gr -= rp[L::PI + i];
           for (int j = 0; j < sh.ne; ++j) if (sh.ei[j] == i) gr += sh.tnu[j];
+          if (mp.hid > 0) gr += sh.hg[i] * (sh.hlu - sh.hll);
         }
         st = fmax(st, fabs(gr));
         if (boxed) {
@@ -317,6 +448,10 @@ struct Ft {
           cp = fmax(cp, fmax(fabs(r[L::LL + i] * (v - lb)), fabs(r[L::LU + i] * (ub - v))));
         }
       }
+    }
+    if (mp.hid > 0 && t == 0) {
+      in = fmax(in, fmax(mp.lh - sh.hv, sh.hv - mp.uh));
+      cp = fmax(cp, fmax(fabs(sh.hll * (sh.hv - mp.lh)), fabs(sh.hlu * (mp.uh - sh.hv))));
     }
     rstat = ft_wmax(st); req = ft_wmax(eq); rineq = ft_wmax(in); rcomp = ft_wmax(cp);
   }
@@ -337,6 +472,11 @@ struct Ft {
     const double* rN = rec(N);
     for (int i = 0; i < NX * NX; ++i) { Pm[i] = 0.0; Pi[i] = 0.0; }
     for (int i = 0; i < NX; ++i) { Pm[i * NX + i] = rN[L::H + i]; p[i] = rN[L::G + i]; lin[i] = 0.0; }
+    if (mp.hid > 0) {   // the terminal row's barrier: sigma c c'
+      const double sig = sh.hql / sh.htl + sh.hqu / sh.htu;
+      for (int i = 0; i < NX; ++i)
+        for (int j = 0; j < NX; ++j) Pm[i * NX + j] += sig * sh.hg[i] * sh.hg[j];
+    }
     for (int j = 0; j < ne; ++j) Pi[sh.ei[j] * ne + j] = 1.0;
     if (factor) {
       for (int i = 0; i < NX * NX; ++i) sh.S[i] = 0.0;
@@ -522,6 +662,19 @@ struct Ft {
     return true;
   }
 
+  // Newton directions of the terminal row's slacks / duals (oracle frow_dir; lane 0, after newton())
+  __device__ void row_dir(double rs, double smu, double& dtl, double& dtu, double& dql, double& dqu) const {
+    const double* rN = rec(sh.N);
+    double cd = 0.0;
+    for (int i = 0; i < NX; ++i) cd += sh.hg[i] * rN[L::D + i];
+    const double rl = rs * sh.hr0l, ru = rs * sh.hr0u;
+    const double rcl = smu - sh.htl * sh.hql - sh.hatl * sh.haql, rcu = smu - sh.htu * sh.hqu - sh.hatu * sh.haqu;
+    dtl = cd + rl;
+    dtu = ru - cd;
+    dql = (rcl - sh.hql * dtl) / sh.htl;
+    dqu = (rcu - sh.hqu * dtu) / sh.htu;
+  }
+
   // ---- interior-point QP ------------------------------------------------------------------------
   // returns 0 converged, 1 max-iter, -1 failure; iterations in qit
   __device__ int qp(int& qit) {
@@ -546,8 +699,27 @@ struct Ft {
         nb += 2.0;
       }
     }
-    const double nbox = ft_wsum(nb);
+    double nbox = ft_wsum(nb);
     __syncthreads();
+    const bool row = mp.hid > 0;
+    if (row) {   // terminal row: slacks from the initial c'dz_N, clipped to ipm_push (infeasible start)
+      if (t == 0) {
+        const double* rN = rec(N);
+        double gd = 0.0;
+        for (int i = 0; i < NX; ++i) gd += sh.hg[i] * rN[L::DZ + i];
+        sh.hL = mp.lh - sh.hv;
+        sh.hU = mp.uh - sh.hv;
+        sh.htl = fmax(gd - sh.hL, o.push);
+        sh.htu = fmax(sh.hU - gd, o.push);
+        sh.hql = o.mu0 / sh.htl;
+        sh.hqu = o.mu0 / sh.htu;
+        sh.hr0l = gd - sh.hL - sh.htl;
+        sh.hr0u = sh.hU - gd - sh.htu;
+        sh.hatl = sh.hatu = sh.haql = sh.haqu = 0.0;
+      }
+      nbox += 2.0;
+      __syncthreads();
+    }
     double e00 = 0.0, rd0 = 0.0;
     for (int k = t; k <= N; k += 64) {
       double* r = rec(k);
@@ -572,8 +744,10 @@ struct Ft {
         }
       }
       for (int i = 0; i < nz(k); ++i)
-        rd0 = fmax(rd0, fabs(rho * r[L::DZ + i] + grad(k, i) - r[L::QL + i] + r[L::QU + i]));
+        rd0 = fmax(rd0, fabs((rho + hq(k, i)) * r[L::DZ + i] + grad(k, i) - r[L::QL + i] + r[L::QU + i] +
+                             ((row && k == N) ? sh.hg[i] * (sh.hqu - sh.hql) : 0.0)));
     }
+    if (row && t == 0) e00 = fmax(e00, fmax(fabs(sh.hr0l), fabs(sh.hr0u)));
     e00 = ft_wmax(e00);
     rd0 = ft_wmax(rd0);
     if (t == 0) {
@@ -591,6 +765,7 @@ struct Ft {
           mu += (r[L::DZ + i] - r[L::LB + i]) * r[L::QL + i] + (r[L::UB + i] - r[L::DZ + i]) * r[L::QU + i];
         }
       }
+      if (row && t == 0) mu += sh.htl * sh.hql + sh.htu * sh.hqu;
       mu = ft_wsum(mu) / nbox;
       if (!isfinite(mu)) { status = -1; break; }
       const double rs = sh.rs;
@@ -599,14 +774,21 @@ struct Ft {
       for (int k = t; k <= N; k += 64) {
         double* r = rec(k);
         for (int i = 0; i < nz(k); ++i) {
-          double Hh = rho;
-          const double gg = rho * r[L::DZ + i] + grad(k, i);
+          const double hh = rho + hq(k, i);
+          double Hh = hh;
+          const double gg = hh * r[L::DZ + i] + grad(k, i);
           if (isfinite(r[L::LB + i]))
             Hh += r[L::QL + i] / (r[L::DZ + i] - r[L::LB + i]) + r[L::QU + i] / (r[L::UB + i] - r[L::DZ + i]);
           r[L::H + i] = Hh; r[L::G + i] = gg;
         }
       }
       __syncthreads();
+      if (row && t == 0) {   // the row's predictor term c gamma in the terminal gradient
+        sh.hatl = sh.hatu = sh.haql = sh.haqu = 0.0;
+        const double gam = sh.hql * (rs * sh.hr0l) / sh.htl - sh.hqu * (rs * sh.hr0u) / sh.htu;
+        double* rN = rec(N);
+        for (int i = 0; i < NX; ++i) rN[L::G + i] += sh.hg[i] * gam;
+      }
       if (!newton(true)) { status = -1; break; }
       FtRatio ma{1.0, 1.0};
       for (int k = t; k <= N; k += 64) {
@@ -621,6 +803,12 @@ struct Ft {
           ma.add(tl, d); ma.add(tu, -d); ma.add(ql, dll); ma.add(qu, dlu);
         }
       }
+      if (row && t == 0) {
+        double dtl, dtu, dql, dqu;
+        row_dir(rs, 0.0, dtl, dtu, dql, dqu);
+        sh.hatl = dtl; sh.hatu = dtu; sh.haql = dql; sh.haqu = dqu;
+        ma.add(sh.htl, dtl); ma.add(sh.htu, dtu); ma.add(sh.hql, dql); ma.add(sh.hqu, dqu);
+      }
       const double aa = ma.reduce();
       double muaff = 0.0;
       for (int k = t; k <= N; k += 64) {
@@ -633,6 +821,8 @@ struct Ft {
           muaff += (tl + aa * d) * (ql + aa * dll) + (tu - aa * d) * (qu + aa * dlu);
         }
       }
+      if (row && t == 0)
+        muaff += (sh.htl + aa * sh.hatl) * (sh.hql + aa * sh.haql) + (sh.htu + aa * sh.hatu) * (sh.hqu + aa * sh.haqu);
       muaff = ft_wsum(muaff) / nbox;
       double sig = muaff / mu;
       sig = sig * sig * sig;
@@ -647,10 +837,17 @@ struct Ft {
           const double d = r[L::DAFF + i], ql = r[L::QL + i], qu = r[L::QU + i];
           const double dll = -ql - ql * d * itl, dlu = -qu + qu * d * itu;
           const double rl = smu - tl * ql - d * dll, ru = smu - tu * qu + d * dlu;
-          r[L::G + i] = rho * r[L::DZ + i] + grad(k, i) - ql - rl * itl + qu + ru * itu;
+          r[L::G + i] = (rho + hq(k, i)) * r[L::DZ + i] + grad(k, i) - ql - rl * itl + qu + ru * itu;
         }
       }
       __syncthreads();
+      if (row && t == 0) {   // the row's Mehrotra-corrected term
+        const double rl = rs * sh.hr0l, ru = rs * sh.hr0u;
+        const double rcl = smu - sh.htl * sh.hql - sh.hatl * sh.haql, rcu = smu - sh.htu * sh.hqu - sh.hatu * sh.haqu;
+        const double gam = -sh.hql + sh.hqu - (rcl - sh.hql * rl) / sh.htl + (rcu - sh.hqu * ru) / sh.htu;
+        double* rN = rec(N);
+        for (int i = 0; i < NX; ++i) rN[L::G + i] += sh.hg[i] * gam;
+      }
       if (!newton(false)) { status = -1; break; }
       FtRatio mx{1.0, o.tau};
       for (int k = t; k <= N; k += 64) {
@@ -664,6 +861,11 @@ struct Ft {
           const double dll = (rl - ql * d) * itl, dlu = (ru + qu * d) * itu;
           mx.add(tl, d); mx.add(tu, -d); mx.add(ql, dll); mx.add(qu, dlu);
         }
+      }
+      double rdtl = 0.0, rdtu = 0.0, rdql = 0.0, rdqu = 0.0;
+      if (row && t == 0) {
+        row_dir(rs, smu, rdtl, rdtu, rdql, rdqu);
+        mx.add(sh.htl, rdtl); mx.add(sh.htu, rdtu); mx.add(sh.hql, rdql); mx.add(sh.hqu, rdqu);
       }
       const double alpha = fmin(1.0, o.tau * mx.reduce());
       for (int k = t; k <= N; k += 64) {
@@ -682,6 +884,10 @@ struct Ft {
         }
       }
       if (t == 0) {
+        if (row) {
+          sh.htl += alpha * rdtl; sh.htu += alpha * rdtu;
+          sh.hql += alpha * rdql; sh.hqu += alpha * rdqu;
+        }
         for (int j = 0; j < ne; ++j) sh.qnu[j] += alpha * (sh.nun[j] - sh.qnu[j]);
         sh.rs = rs * (1.0 - alpha);
       }
@@ -693,7 +899,10 @@ struct Ft {
     if (t == 0) {
       double lam[NX];
       const double* rN = rec(N);
-      for (int i = 0; i < NX; ++i) lam[i] = rho * rN[L::DZ + i] - rN[L::QL + i] + rN[L::QU + i];
+      for (int i = 0; i < NX; ++i) {
+        lam[i] = (rho + hq(N, i)) * rN[L::DZ + i] + grad(N, i) - rN[L::QL + i] + rN[L::QU + i];
+        if (row) lam[i] += sh.hg[i] * (sh.hqu - sh.hql);
+      }
       for (int j = 0; j < ne; ++j) lam[sh.ei[j]] += sh.qnu[j];
       for (int k = N - 1; k >= 0; --k) {
         double* r = rec(k);
@@ -701,7 +910,7 @@ struct Ft {
         if (k == 0) break;
         double ln[NX];
         for (int i = 0; i < NX; ++i) {
-          double s = rho * r[L::DZ + i] + grad(k, i) - r[L::QL + i] + r[L::QU + i];
+          double s = (rho + hq(k, i)) * r[L::DZ + i] + grad(k, i) - r[L::QL + i] + r[L::QU + i];
           for (int q = 0; q < NX; ++q) s += r[L::A + q * NX + i] * lam[q];
           ln[i] = s;
         }
@@ -733,7 +942,7 @@ struct Ft {
       for (int a = 0; a < NU; ++a) u[a] = r[L::U + a] + alpha * r[L::DZ + NX + a];
   }
 
-  __device__ double merit(double alpha) const {
+  __device__ double merit(double alpha) {
     const int N = sh.N;
     double val = 0.0, viol = 0.0;
     for (int k = t; k <= N; k += 64) {
@@ -747,16 +956,25 @@ struct Ft {
       double xk[NX], uk[NU], xn[NX], un[NU], phi[NX];
       if (k < N) {
         state_at(k, alpha, xk, uk);
-        for (int i = 0; i < NX; ++i) val += (k == 0 ? sh.c0[i] : sh.cp[i]) * xk[i];
+        if (mp.on) val += track(k, xk, uk);
+        else for (int i = 0; i < NX; ++i) val += (k == 0 ? sh.c0[i] : sh.cp[i]) * xk[i];
         ft_rk4_sens<NQ>(xk, uk, phi, nullptr, nullptr);
         state_at(k + 1, alpha, xn, un);
         for (int i = 0; i < NX; ++i) val += r[L::WPI + i] * fabs(phi[i] - xn[i]);
       } else {
         state_at(N, alpha, xn, un);
+        if (mp.on) val += track(N, xn, un);
         for (int j = 0; j < sh.ne; ++j) val += sh.wnu[j] * fabs(xn[sh.ei[j]] - sh.ev[j]);
       }
     }
-    return ft_wsum(val) + sh.wbnd * ft_wsum(viol);
+    double hviol = 0.0;
+    if (mp.hid > 0) {   // the terminal row's violation at the trial state, weighted like the boxes
+      double xN[NX], uN[NU];
+      state_at(N, alpha, xN, uN);
+      const double hv = nn_row(xN, nullptr);
+      hviol = fmax(0.0, mp.lh - hv) + fmax(0.0, hv - mp.uh);
+    }
+    return ft_wsum(val) + sh.wbnd * (ft_wsum(viol) + hviol);
   }
 
   __device__ void weights() {
@@ -771,6 +989,7 @@ struct Ft {
         }
       for (int i = 0; i < nz(k); ++i) lmax = fmax(lmax, fmax(r[L::QL + i], r[L::QU + i]));
     }
+    if (mp.hid > 0 && t == 0) lmax = fmax(lmax, fmax(sh.hql, sh.hqu));
     lmax = ft_wmax(lmax);
     if (t == 0) {
       for (int j = 0; j < sh.ne; ++j) {
@@ -799,8 +1018,13 @@ struct Ft {
       if (k < N)
         for (int i = 0; i < NX; ++i) r[L::PI + i] += alpha * (r[L::QPI + i] - r[L::PI + i]);
     }
-    if (t == 0)
+    if (t == 0) {
       for (int j = 0; j < sh.ne; ++j) sh.tnu[j] += alpha * (sh.qnu[j] - sh.tnu[j]);
+      if (mp.hid > 0) {
+        sh.hll += alpha * (sh.hql - sh.hll);
+        sh.hlu += alpha * (sh.hqu - sh.hlu);
+      }
+    }
     __syncthreads();
   }
 
@@ -812,20 +1036,24 @@ struct Ft {
       double rstat, req, rineq, rcomp;
       residuals(rstat, req, rineq, rcomp);
       if (!isfinite(rstat) || !isfinite(req)) { status = 1; break; }
-      if (rstat < o.tol_stat && req < o.tol_eq && rineq < o.tol_ineq && rcomp < o.tol_comp) { status = 0; break; }
+      const bool rti = mp.on && mp.rti;
+      if (rti && it == 1) { status = 0; break; }   // SQP_RTI: one QP and its full step
+      if (!rti && rstat < o.tol_stat && req < o.tol_eq && rineq < o.tol_ineq && rcomp < o.tol_comp) { status = 0; break; }
       if (it >= o.max_iter) { status = 2; break; }
       int qit = 0;
       const int qs = qp(qit);
       qtot += qit;
       if (qs < 0) { status = 4; break; }
       weights();
-      const double phi0 = merit(0.0);
       double alpha = 1.0;
-      for (;;) {
-        const double pa = merit(alpha);
-        if (pa < phi0) break;
-        if (alpha * o.alpha_red < o.alpha_min) break;
-        alpha *= o.alpha_red;
+      if (!rti) {
+        const double phi0 = merit(0.0);
+        for (;;) {
+          const double pa = merit(alpha);
+          if (pa < phi0) break;
+          if (alpha * o.alpha_red < o.alpha_min) break;
+          alpha *= o.alpha_red;
+        }
       }
       apply(alpha);
       if (!isfinite(rec(0)[L::X + NX - 1])) { status = 1; break; }
@@ -837,11 +1065,11 @@ struct Ft {
 // one workgroup = one wave = one problem at a time; workgroups pull problem ids until none are left
 template <int NQ>
 __global__ __launch_bounds__(64) void k_ft(Opts o, Inputs in, double* regions, long long region_doubles,
-                                           unsigned* head) {
+                                           unsigned* head, MpcArgs mp) {
   __shared__ FtShared<NQ> sh;
   __shared__ int job;
   const int t = (int)threadIdx.x;
-  Ft<NQ> F(sh, regions + (long long)blockIdx.x * region_doubles, o, t);
+  Ft<NQ> F(sh, regions + (long long)blockIdx.x * region_doubles, o, t, mp);
   for (;;) {
     if (t == 0) job = (int)atomicAdd(head, 1u);
     __syncthreads();

@@ -1518,6 +1518,9 @@ struct vboc_solver {
   bool hc_wave = true;              // constrained problems on the wave solver (k_wave<NQ, false, true>)
   void* dg_spec = nullptr;          // their pool (events, results, control words, queue)
   size_t dg_spec_bytes = 0;
+  // Safe-MPC batches (vboc_mpc_solve_batch): the free-time solver's inputs with the dt column, W1 transposed
+  void* mpc_buf = nullptr;
+  size_t mpc_bytes = 0;
   // parked first solves of the data-generation loop (dg.h): their results and the two resume queues
   bool dg_park = true;
   int dg_park_window = 0;           // 0: parked problems wait until the new ones run out
@@ -1619,7 +1622,7 @@ static hipError_t launch_round(vboc_solver* h, dim3 grid, dim3 block, hipStream_
 
 // free-time solver: a persistent grid of one-wave workgroups, each with its own stage-record region
 template <int NQ>
-static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st) {
+static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st, const MpcArgs& mp = MpcArgs{}) {
   const long long rd = FtL<NQ>::region_doubles(in.nmax);
   long long groups = in.B < 1024 ? in.B : 1024;
   const size_t need = (size_t)groups * (size_t)rd * sizeof(double);
@@ -1630,7 +1633,7 @@ static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st) {
     if (hipMalloc(&h->ft_regions, need) != hipSuccess) return -1;
     h->ft_bytes = need;
   }
-  hipLaunchKernelGGL(k_ft<NQ>, dim3((unsigned)groups), dim3(64), 0, st, h->o, in, h->ft_regions, rd, h->head);
+  hipLaunchKernelGGL(k_ft<NQ>, dim3((unsigned)groups), dim3(64), 0, st, h->o, in, h->ft_regions, rd, h->head, mp);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1841,6 +1844,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->tt_jobs) (void)hipFree(h->tt_jobs);
   if (h->dg_spec) (void)hipFree(h->dg_spec);
   if (h->dg_park_buf) (void)hipFree(h->dg_park_buf);
+  if (h->mpc_buf) (void)hipFree(h->mpc_buf);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   for (auto ev : h->pev) (void)hipEventDestroy(ev);
@@ -2203,6 +2207,114 @@ static int solve_host(vboc_handle h, const vboc_batch_t* b, bool ft) {
   return VBOC_OK;
 }
 
+// a Safe-MPC batch as free-time inputs: x [q, v, h] (the dt column pinned by x_0), bounds with a free dt on the path
+__global__ void k_mpc_prep(int B, int N, int nq, double hstep, const double* __restrict__ x0,
+                           const double* __restrict__ xg6, const double* lbx, const double* ubx, const double* lbu,
+                           const double* ubu, const double* lbxe, const double* ubxe, double* xg7, double* lbx7,
+                           double* ubx7, double* lbu_b, double* ubu_b, double* lbx0, double* ubx0, double* lbxe7,
+                           double* ubxe7, double* p, int* Nb) {
+  const int n2 = 2 * nq, nx = n2 + 1;
+  const long long tot = (long long)B * (N + 1);
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot; e += (long long)gridDim.x * blockDim.x) {
+    const long long b = e / (N + 1);
+    for (int i = 0; i < n2; ++i) xg7[e * nx + i] = xg6[e * n2 + i];
+    xg7[e * nx + n2] = hstep;
+    if (e % (N + 1) == 0) {
+      Nb[b] = N;
+      for (int i = 0; i < n2; ++i) {
+        lbx7[b * nx + i] = lbx[i]; ubx7[b * nx + i] = ubx[i];
+        lbxe7[b * nx + i] = lbxe[i]; ubxe7[b * nx + i] = ubxe[i];
+        lbx0[b * nx + i] = ubx0[b * nx + i] = x0[b * n2 + i];
+      }
+      lbx7[b * nx + n2] = lbxe7[b * nx + n2] = -INFINITY;
+      ubx7[b * nx + n2] = ubxe7[b * nx + n2] = INFINITY;
+      lbx0[b * nx + n2] = ubx0[b * nx + n2] = hstep;
+      for (int a = 0; a < nq; ++a) { lbu_b[b * nq + a] = lbu[a]; ubu_b[b * nq + a] = ubu[a]; }
+      for (int a = 0; a <= nq; ++a) p[b * (nq + 1) + a] = 0.0;
+    }
+  }
+}
+__global__ void k_mpc_strip(long long tot, int nq, const double* __restrict__ xo7, double* __restrict__ xo6) {
+  const int n2 = 2 * nq, nx = n2 + 1;
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot; e += (long long)gridDim.x * blockDim.x)
+    for (int i = 0; i < n2; ++i) xo6[e * n2 + i] = xo7[e * nx + i];
+}
+__global__ void k_transpose(int H, const double* __restrict__ a, double* __restrict__ at) {
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < (long long)H * H; e += (long long)gridDim.x * blockDim.x)
+    at[(e % H) * H + e / H] = a[e];
+}
+
+int vboc_mpc_solve_batch(vboc_handle h, const vboc_mpc_batch_t* b, void* stream) {
+  const std::string W = "vboc_mpc_solve_batch";
+  if (busy(h, "vboc_mpc_solve_batch")) return VBOC_ERR_ARG;
+  if (!h || !b) return fail(VBOC_ERR_ARG, W + ": NULL argument");
+  if (h->nq != 3) return fail(VBOC_ERR_UNSUPPORTED, W + ": the Safe-MPC OCP is the triple pendulum's (nq = 3)");
+  if (h->o.hc) return fail(VBOC_ERR_UNSUPPORTED, W + ": no path constraint in the Safe-MPC OCP (clear it first)");
+  if (b->B < 0 || b->N < 1 || b->N > h->nmax) return fail(VBOC_ERR_ARG, W + ": needs B >= 0 and 1 <= N <= nmax");
+  if (b->hidden < 0 || b->hidden > FT_NN_MAX) return fail(VBOC_ERR_ARG, W + ": hidden must be in [0, 512]");
+  if (!(b->h > 0.0)) return fail(VBOC_ERR_ARG, W + ": the time step must be positive");
+  if (b->B == 0) { h->launches = 0; return VBOC_OK; }
+  const void* ptrs[] = {b->x0, b->x_guess, b->u_guess, b->lbx, b->ubx, b->lbu, b->ubu, b->lbx_e, b->ubx_e, b->W,
+                        b->We, b->yref, b->yref_e, b->status, b->x_out, b->u_out, b->cost, b->sqp_iter, b->qp_iter};
+  for (const void* q : ptrs)
+    if (!q) return fail(VBOC_ERR_ARG, W + ": NULL array in batch");
+  if (b->hidden > 0 && (!b->W0 || !b->b0 || !b->W1 || !b->b1 || !b->W2 || !b->b2))
+    return fail(VBOC_ERR_ARG, W + ": NULL network parameter");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  constexpr int NQ = 3, NX = 2 * NQ + 1, NU = NQ;
+  const size_t B = (size_t)b->B, N = (size_t)b->N, H = (size_t)b->hidden;
+  const size_t dbl = B * (N + 1) * NX * 2 + B * NX * 6 + B * NU * 2 + B * (NQ + 1) + H * H;
+  const size_t need = dbl * sizeof(double) + B * sizeof(int) + 512;
+  if (need > h->mpc_bytes) {
+    if (h->mpc_buf) (void)hipFree(h->mpc_buf);
+    h->mpc_buf = nullptr;
+    h->mpc_bytes = 0;
+    if (hipMalloc(&h->mpc_buf, need) != hipSuccess) return fail(VBOC_ERR_NOMEM, W + ": hipMalloc of the batch inputs");
+    h->mpc_bytes = need;
+  }
+  double* d = (double*)h->mpc_buf;
+  auto take = [&](size_t n) { double* r = d; d += (n + 1) & ~(size_t)1; return r; };
+  double* xg7 = take(B * (N + 1) * NX);
+  double* xo7 = take(B * (N + 1) * NX);
+  double *lbx7 = take(B * NX), *ubx7 = take(B * NX), *lbx0 = take(B * NX), *ubx0 = take(B * NX);
+  double *lbxe7 = take(B * NX), *ubxe7 = take(B * NX), *lbu_b = take(B * NU), *ubu_b = take(B * NU);
+  double* pp = take(B * (NQ + 1));
+  double* w1t = take(H * H);
+  int* Nb = (int*)d;
+  hipLaunchKernelGGL(k_mpc_prep, dim3(256), dim3(256), 0, st, b->B, b->N, NQ, b->h, b->x0, b->x_guess, b->lbx, b->ubx,
+                     b->lbu, b->ubu, b->lbx_e, b->ubx_e, xg7, lbx7, ubx7, lbu_b, ubu_b, lbx0, ubx0, lbxe7, ubxe7, pp,
+                     Nb);
+  MpcArgs mp{};
+  mp.on = 1; mp.rti = b->rti ? 1 : 0; mp.hid = b->hidden; mp.cs = b->cost_scale;
+  const double *Wh = b->W, *Weh = b->We, *yr = b->yref, *yre = b->yref_e;   // host constants
+  for (int i = 0; i < 2 * NQ; ++i) { mp.wq[i] = Wh[i]; mp.yr[i] = yr[i]; mp.we[i] = Weh[i]; mp.yre[i] = yre[i]; }
+  mp.wq[2 * NQ] = mp.yr[2 * NQ] = mp.we[2 * NQ] = mp.yre[2 * NQ] = 0.0;   // the pinned dt column carries no cost
+  for (int a = 0; a < NU; ++a) { mp.wq[NX + a] = Wh[2 * NQ + a]; mp.yr[NX + a] = yr[2 * NQ + a]; }
+  if (b->hidden > 0) {
+    hipLaunchKernelGGL(k_transpose, dim3(256), dim3(256), 0, st, b->hidden, b->W1, w1t);
+    mp.W0 = b->W0; mp.b0 = b->b0; mp.W1 = b->W1; mp.W1T = w1t; mp.b1 = b->b1; mp.W2 = b->W2; mp.b2 = b->b2;
+    mp.mean = b->mean; mp.std = b->std; mp.lh = b->lh; mp.uh = b->uh;
+  }
+  mp.hrow = b->h_out;
+  Inputs in;
+  in.B = b->B; in.nmax = b->N; in.N = Nb;
+  in.xg = xg7; in.ug = b->u_guess; in.p = pp; in.lbx = lbx7; in.ubx = ubx7; in.lbu = lbu_b; in.ubu = ubu_b;
+  in.lbx0 = lbx0; in.ubx0 = ubx0; in.lbxe = lbxe7; in.ubxe = ubxe7;
+  in.status = b->status; in.xo = xo7; in.uo = b->u_out; in.cost = b->cost; in.sqp_iter = b->sqp_iter;
+  in.qp_iter = b->qp_iter; in.head = h->head;
+  HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
+  HIPCHK(hipEventRecord(h->ev0, st));
+  const int rc = launch_ft<NQ>(h, in, st, mp);
+  if (rc == -1) return fail(VBOC_ERR_NOMEM, W + ": hipMalloc of the stage regions");
+  if (rc) return fail(VBOC_ERR_HIP, W + ": " + hipGetErrorString(hipGetLastError()));
+  HIPCHK(hipEventRecord(h->ev1, st));
+  hipLaunchKernelGGL(k_mpc_strip, dim3(256), dim3(256), 0, st, (long long)(B * (N + 1)), NQ, xo7, b->x_out);
+  HIPCHK(hipGetLastError());
+  h->launches = 1;
+  return VBOC_OK;
+}
+
 int vboc_solve_batch_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, false); }
 int vboc_solve_batch_ft_host(vboc_handle h, const vboc_batch_t* b) { return solve_host(h, b, true); }
 
@@ -2347,6 +2459,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
     const size_t pneed = qbytes + sizeof(double) * (size_t)stride * (size_t)b->B;
     if (pneed > h->dg_park_bytes) {
       if (h->dg_park_buf) (void)hipFree(h->dg_park_buf);
+  if (h->mpc_buf) (void)hipFree(h->mpc_buf);
       h->dg_park_buf = nullptr;
       h->dg_park_bytes = 0;
       if (hipMalloc(&h->dg_park_buf, pneed) != hipSuccess)
@@ -2457,7 +2570,6 @@ int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream) {
   h->coop_count = b->B;
   HIPCHK(hipMemcpyAsync(h->host_done, h->head, 14 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  h->dg_busy = false;
   const unsigned* c = h->host_done;
   if (c[3]) return fail(VBOC_ERR_ARG, "vboc_testing_test: a horizon passed the handle's nmax");
   if (c[1] != (unsigned)b->B) return fail(VBOC_ERR_HIP, "vboc_testing_test: not every problem finished");
@@ -2469,6 +2581,7 @@ static int dg_wait(vboc_handle h, vboc_dg_batch_t* b, hipStream_t st) {
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipMemcpyAsync(h->host_done, h->head, 14 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  h->dg_busy = false;   // the launch has ended: the handle's buffers are free again
   const unsigned* c = h->host_done;
   b->rows_used = (long long)(((unsigned long long)c[5] << 32) | c[4]);
   b->spec_solves = (long long)(((unsigned long long)c[11] << 32) | c[10]);

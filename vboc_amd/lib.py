@@ -22,7 +22,7 @@ EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", 
            "vboc_rk4_sens_batch_host", "vboc_last_kernel_ms",
            "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_data_generation_async",
            "vboc_data_generation_wait", "vboc_testing", "vboc_testing_test", "vboc_hjr_solve_batch",
-           "vboc_set_path_constraint",
+           "vboc_set_path_constraint", "vboc_mpc_solve_batch",
            "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
@@ -68,6 +68,16 @@ class TtBatch(ctypes.Structure):
                 ("draw_stream", ctypes.c_int), ("tol", ctypes.c_double), ("dt", ctypes.c_double),
                 ("xlo", ctypes.c_double * 8), ("xhi", ctypes.c_double * 8), ("ulim", ctypes.c_double * 4),
                 ("rows", ctypes.c_void_p), ("row_cnt", ctypes.c_void_p), ("stats", ctypes.c_void_p)]
+
+
+class MpcBatch(ctypes.Structure):
+    """vboc_mpc_batch_t (include/vboc.h): Safe-MPC OCP_solve batch (W, We, yref, yref_e are host arrays)."""
+    _fields_ = [("B", ctypes.c_int), ("N", ctypes.c_int), ("rti", ctypes.c_int), ("hidden", ctypes.c_int),
+                ("h", ctypes.c_double), ("cost_scale", ctypes.c_double)] + \
+               [(n, ctypes.c_void_p) for n in ("x0", "x_guess", "u_guess", "lbx", "ubx", "lbu", "ubu", "lbx_e", "ubx_e",
+                                               "W", "We", "yref", "yref_e", "W0", "b0", "W1", "b1", "W2", "b2")] + \
+               [(n, ctypes.c_double) for n in ("mean", "std", "lh", "uh")] + \
+               [(n, ctypes.c_void_p) for n in ("status", "x_out", "u_out", "cost", "sqp_iter", "qp_iter", "h_out")]
 
 
 # per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
@@ -124,6 +134,7 @@ def load():
     lib.vboc_hjr_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(HjrBatch), ctypes.c_void_p]
     lib.vboc_testing.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_int, ctypes.c_void_p]
     lib.vboc_testing_test.argtypes = [ctypes.c_void_p, ctypes.POINTER(TtBatch), ctypes.c_void_p]
+    lib.vboc_mpc_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(MpcBatch), ctypes.c_void_p]
     lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
@@ -352,6 +363,42 @@ class Solver:
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         _check(self.lib.vboc_hjr_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
         out["_keep"] = W
+        return out
+
+    def mpc_solve_device(self, spec, x0, x_guess, u_guess, params=None, mean=0.0, std=1.0, rti=False, lh=0.0,
+                         uh=1e6, stream=None):
+        """OCPtriplependulumHardTerm.OCP_solve (vboc_mpc_solve_batch, ft.h) for every row of the float64 cuda tensor
+        x0 [B, 6]: guesses [B, N+1, 6] / [B, N, 3] (cuda, float64), spec a safempc.MpcSpec, params the NeuralNetDIR
+        weights as float64 cuda tensors (None: no terminal row).  Returns a dict of device tensors: status, x, u, cost,
+        sqp_iter, qp_iter, h (the row at the result's x_N)."""
+        import torch
+        B, N = x0.shape[0], spec.N
+        for t_ in (x0, x_guess, u_guess):
+            assert t_.is_cuda and t_.dtype == torch.float64 and t_.is_contiguous()
+        assert tuple(x_guess.shape) == (B, N + 1, 6) and tuple(u_guess.shape) == (B, N, 3)
+        dev = x0.device
+        f64 = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)
+        bnd = [f64(a) for a in (spec.xmin, spec.xmax, spec.umin, spec.umax, spec.xmin, spec.xmax)]
+        host = [np.ascontiguousarray(a, dtype=np.float64) for a in (spec.W, spec.W_e, spec.yref, spec.yref_e)]
+        out = dict(status=torch.empty(B, dtype=torch.int32, device=dev), x=torch.empty_like(x_guess),
+                   u=torch.empty_like(u_guess), cost=torch.empty(B, dtype=torch.float64, device=dev),
+                   sqp_iter=torch.empty(B, dtype=torch.int32, device=dev),
+                   qp_iter=torch.empty(B, dtype=torch.int32, device=dev), h=torch.zeros(B, dtype=torch.float64, device=dev))
+        W = [p_.contiguous() for p_ in params] if params is not None else []
+        for w in W:
+            assert w.is_cuda and w.dtype == torch.float64
+        b = MpcBatch(B=B, N=N, rti=int(bool(rti)), hidden=W[0].shape[0] if W else 0, h=spec.time_step,
+                     cost_scale=spec.cost_scale, x0=x0.data_ptr(), x_guess=x_guess.data_ptr(), u_guess=u_guess.data_ptr(),
+                     mean=float(mean), std=float(std), lh=float(lh), uh=float(uh),
+                     **{n: t_.data_ptr() for n, t_ in zip(("lbx", "ubx", "lbu", "ubu", "lbx_e", "ubx_e"), bnd)},
+                     **{n: a.ctypes.data for n, a in zip(("W", "We", "yref", "yref_e"), host)},
+                     **{n: w.data_ptr() for n, w in zip(("W0", "b0", "W1", "b1", "W2", "b2"), W)},
+                     status=out["status"].data_ptr(), x_out=out["x"].data_ptr(), u_out=out["u"].data_ptr(),
+                     cost=out["cost"].data_ptr(), sqp_iter=out["sqp_iter"].data_ptr(),
+                     qp_iter=out["qp_iter"].data_ptr(), h_out=out["h"].data_ptr())
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        _check(self.lib.vboc_mpc_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        out["_keep"] = (bnd, host, W)
         return out
 
     def kernel_stats(self):
