@@ -211,13 +211,14 @@ class DirTrainer:
         self.active.fill_(True)
         self.fits += 1
         steps = 0
+        # Each fit draws from a generator of its own, seeded from the trainer's seed and the fit's index, in both
+        # modes (so a captured fit equals the eager one).  A captured fit's graph is the only one that registers
+        # it: re-registering one generator with a second graph after the first was destroyed is the pattern that
+        # ran in the round-3 fault (profiles/r03f_vboc_loop_fault.log), and nothing of a
+        # destroyed graph is referenced by the next one.
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(self.seed * 1_000_003 + self.fits)
         if self.graphs:
-            # Each captured fit draws from a generator of its own (seeded from the trainer's seed and the fit's
-            # index) that only that graph registers: re-registering one generator with a second graph after the
-            # first was destroyed is the pattern that ran in the round-3 fault (profiles/r03f_vboc_loop_fault.log,
-            # DESIGN.md section 11), and nothing of a destroyed graph is referenced by the next one.
-            gen = torch.Generator(device=self.device)
-            gen.manual_seed(self.seed * 1_000_003 + self.fits)
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
             with torch.cuda.stream(s):                      # warm-up outside capture (allocations)
@@ -236,7 +237,7 @@ class DirTrainer:
             del g
         else:
             while bool(self.active.item()):
-                self._step(F, X, y, n, n_new)
+                self._step(F, X, y, n, n_new, gen)
                 steps += 1
         self.total_steps += steps
         return dict(iterations=int(self.it.item()) - 1, val=float(self.val.item()), launched=steps)
