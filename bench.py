@@ -436,9 +436,12 @@ def run(args, engine_factory=None):
         ms = 1e3 / DG_CLOCK_HZ
         tail = {"critical_problem_ms": round(float((t1s - t0s).max()) * ms, 1),
                 "mean_problem_ms": round(float((t1s - t0s).mean()) * ms, 2),
-                "queue_drained_ms": round(float(t0s.max() - t0s.min()) * ms, 1),
+                "new_problems_drained_ms": round(float(t0s.max() - t0s.min()) * ms, 1),
+                "queue_drained_ms": round(float(st[:, 9].max() - t0s.min()) * ms, 1),
                 "last_finish_ms": round(float(t1s.max() - t0s.min()) * ms, 1),
-                "note": "last timed launch, device real-time clock from the first problem's start"}
+                "note": "last timed launch, device real-time clock from the first problem's start; queue_drained = "
+                        "the last job (a new problem or a parked one's resume) taken"}
+        tail["after_drain_share"] = round(1.0 - tail["queue_drained_ms"] / max(tail["last_finish_ms"], 1e-9), 3)
     sqp = np.concatenate(rec["sqp"]) if rec["sqp"] else np.zeros(1)
     ok = np.concatenate(rec["status"]) if rec["status"] else np.zeros(1)
     if beat is not None:
@@ -496,7 +499,7 @@ def run(args, engine_factory=None):
                 "boundary_problems_per_s": round(rd["problems"] / rd["wall_s"], 2),
                 "wall_s": round(rd["wall_s"], 2), "kernel_ms": round(rd["kernel_ms"], 1),
                 "critical_problem_ms": round(float((st[:, 6] - st[:, 5]).max()) * ms, 1),
-                "queue_drained_ms": round(float(st[:, 5].max() - st[:, 5].min()) * ms, 1),
+                "queue_drained_ms": round(float(st[:, 9].max() - st[:, 5].min()) * ms, 1),
                 "note": "the warmup launch: W x B problems as ONE round (5 x 20k = configs[2]'s 100k states at the "
                         "driver's command), wall time incl. the first launch; rank 0's shard"}
     if world > 1:

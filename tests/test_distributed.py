@@ -114,7 +114,8 @@ class OracleEngine:
         cnt = np.array([-1 if s is None else len(s) for s in samples])
         rows = np.array([row for s in samples if s for row in s], dtype=np.float64).reshape(-1, 2 * self.nq)
         off = np.concatenate([[0], np.cumsum(np.maximum(cnt, 0))[:-1]])
-        stats = np.zeros((len(ids), 9))
+        from vboc_amd.lib import DG_STATS
+        stats = np.zeros((len(ids), len(DG_STATS)))
         stats[0, 0], stats[0, 1] = st["solves"], st["rk4"]
         T = self.torch.as_tensor
         return dict(rows_all=T(rows), row_off=T(off.astype(np.int64)), row_cnt=T(cnt.astype(np.int32)), stats=T(stats))

@@ -67,7 +67,8 @@ def _plain_fit(trainer_seed, F, nq, hidden, k, it_max, n_new=0, init=None):
         model.load_state_dict(init)
     opt = torch.optim.Adam(model.parameters(), lr=1e-3)
     crit = nn.MSELoss()
-    gen = torch.Generator().manual_seed(trainer_seed)
+    from vboc_amd.learn import DirTrainer
+    gen = torch.Generator().manual_seed(DirTrainer.fit_seed(trainer_seed, 1))   # the trainer's first fit
     Ft = torch.tensor(F, dtype=torch.float32)
     n = F.shape[0]
     it, val = 1, max(F[:, 2 * nq])

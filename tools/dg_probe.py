@@ -5,7 +5,7 @@ The bench's timed launch is 400k problems; its rate is the bulk rate (every resi
   kernel_ms     the whole launch (HIP events)
   bulk          solves per second while the queue still feeds every wave: solves of the problems that ended
                 inside [t_first + 5 % of the drain time, queue drained] / that window (device real-time clock)
-  drained_ms    when the last problem started; last_ms when the last one finished
+  drained_ms    when the last job (new problem or parked resume) was taken; last_ms when the last problem finished
   digest        sha1 of the per-problem rows / counts / solve statistics (variants that claim the same results
                 must reproduce the product's digest)
 Run once per library (VBOC_LIB=<variant .so>) and resident-problem count (--groups).
@@ -35,14 +35,17 @@ def main():
     ap.add_argument("--groups", type=int, nargs="*", default=[0])
     ap.add_argument("--park", type=int, nargs="*", default=[1],
                     help="dg_park option values to run (1: parked first solves, the product default; 0: off)")
+    ap.add_argument("--window", type=int, nargs="*", default=[2],
+                    help="dg_spec_window option values to run (2: the product default; 0: off)")
     ap.add_argument("--save", default=None, help="write the per-problem stats (lib.DG_STATS) of each launch to "
                                                  "<save>_g<groups>.npy (scheduling studies)")
     a = ap.parse_args()
     s = lib.Solver(a.nq, 120, device=0)
     ids = torch.arange(a.first, a.first + a.B, dtype=torch.int64, device="cuda:0")
-    for g, pk in [(g, pk) for pk in a.park for g in a.groups]:
+    for g, pk, wn in [(g, pk, wn) for wn in a.window for pk in a.park for g in a.groups]:
         s.set_option("wave_groups", g)
         s.set_option("dg_park", pk)
+        s.set_option("dg_spec_window", wn)
         t = time.time()
         out = s.data_generation_device(ids)
         torch.cuda.synchronize()
@@ -51,7 +54,7 @@ def main():
         st = out["stats"].cpu().numpy()
         t0, t1 = st[:, 5], st[:, 6]
         base = t0.min()
-        drained = t0.max() - base
+        drained = st[:, 9].max() - base          # the last job taken (a new problem or a parked resume)
         lo = base + 0.05 * drained
         hi = base + drained
         inwin = (t1 >= lo) & (t1 <= hi)
@@ -61,17 +64,18 @@ def main():
         h.update(out["row_cnt"].cpu().numpy().tobytes())
         h.update(st[:, [0, 1, 2, 3, 4, 7, 8]].tobytes())
         rec = {"lib": os.path.basename(os.environ.get("VBOC_LIB") or "libvboc_amd.so"), "nq": a.nq, "B": a.B,
-               "groups": int(s.get_option("last_groups")), "park": pk, "kernel_ms": round(ms, 1), "wall_s": round(wall, 2),
+               "groups": int(s.get_option("last_groups")), "park": pk, "window": wn, "kernel_ms": round(ms, 1), "wall_s": round(wall, 2),
                "solves": int(st[:, 0].sum()), "solves_per_s": round(float(st[:, 0].sum()) / (ms / 1e3), 1),
                "bulk_solves_per_s": round(bulk, 1) if bulk else None,
                "drained_ms": round(drained / lib.DG_CLOCK_HZ * 1e3, 1),
                "last_ms": round((t1.max() - base) / lib.DG_CLOCK_HZ * 1e3, 1),
                "stage_ipm_iters_per_s": round(float(st[:, 4].sum()) / (ms / 1e3), 1),
                "tflops": round(dg_flops(a.nq, st) / (ms / 1e3) / 1e12, 4),
+               "spec_solves": int(out.get("spec_solves", -1)), "spec_used": int(out.get("spec_used", -1)),
                "digest": h.hexdigest()}
         print(json.dumps(rec), flush=True)
         if a.save:
-            np.save(f"{a.save}_g{rec['groups']}_p{pk}.npy", st)
+            np.save(f"{a.save}_g{rec['groups']}_p{pk}_w{wn}.npy", st)
 
 
 if __name__ == "__main__":

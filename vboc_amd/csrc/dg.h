@@ -76,6 +76,12 @@ struct DgJobs {
   unsigned* spec_q_tail;          // queue: entries pushed / popped
   unsigned* spec_q_head;
   unsigned long long* spec_count; // [0] speculative solves run by other waves, [1] of them used
+  // the eager window (see "Speculative restarts"): the next spec_window attempts of a chain also go to this queue,
+  // which every wave serves before new or parked problems; 0 switches it off
+  int spec_window;
+  int* spec_eq;                   // [spec_events * DG_SPEC_JOBS] like spec_q
+  unsigned* spec_eq_tail;
+  unsigned* spec_eq_head;
   // parked first solves (see "Parked first solves" below); park_res == nullptr switches parking off
   double* park_res;               // [count][park_stride]: status, cost, sqp, qp, t0, then x [N + 1][nx + 1], u [N][nu]
   int park_stride;
@@ -93,15 +99,16 @@ constexpr int DG_SPEC_HDR = 48;   // doubles of an event's snapshot header
 
 // per-problem statistics: OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, and
 // the wave's start / end time of the problem (s_memrealtime, 100 MHz constant clock)
-// and the first solve's status and SQP iterations
-enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST1, DG_IT1, DG_NSTAT };
+// and the first solve's status and SQP iterations, and when a wave took the problem's last job (its start, or
+// its resume when it was parked: the last of these over a launch is when the job queues drained)
+enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST1, DG_IT1, DG_TQ, DG_NSTAT };
 
 template <int NQ>
 struct DgState {
   int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, spec_ev,
       spec_base, resumed;
   double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
-  double sqp, nsqp, nqp, t0, st1, it1;
+  double sqp, nsqp, nqp, t0, st1, it1, tq;
   double ran[2], store_ic[4], xsym[2 * NQ];
 };
 
@@ -303,6 +310,7 @@ struct Dg {
     job = job_;
     pid = J.ids[job];
     s->t0 = (double)__builtin_amdgcn_s_memrealtime();
+    s->tq = s->t0;
     const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max, eps = J.eps;
     s->phase = HEXT; s->N = J.N_start; s->ext = 0; s->f = 0; s->at_limit = 0; s->N_test = 0; s->ver = 0;
     s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0;
@@ -542,6 +550,14 @@ struct Dg {
     }
     s->spec_ev = ev;
     s->spec_base = att;
+    for (int j = 1; j <= J.spec_window && j <= nj; ++j) push_eager(ev, j);
+  }
+  // job j of event ev to the eager queue (lane 0; the header and the lazy queue entry are already published)
+  __device__ __forceinline__ void push_eager(int ev, int j) const {
+    if (t == 0) {
+      const unsigned q = atomicAdd(J.spec_eq_tail, 1u);
+      st_flag(&J.spec_eq[q], ev * (DG_SPEC_JOBS + 1) + j + 1);
+    }
   }
   // the owner takes job j's result (solved by another wave) as its own solve of the current attempt
   __device__ __forceinline__ void take_result(int ev, int j, int N) {
@@ -635,6 +651,8 @@ struct Dg {
         const int ev = s->spec_ev;
         const int j = att - s->spec_base;
         if (ev >= 0 && j >= 1 && j <= DG_SPEC_JOBS && j <= 10 - s->spec_base) {
+          // the owner moves on to job j: the eager window moves with it
+          if (J.spec_window > 0 && j + J.spec_window <= 10 - s->spec_base) push_eager(ev, j + J.spec_window);
           if (!claim(ev, j)) {            // another wave solves / solved this attempt: take its result
             take_result(ev, j, N);
             return 2;
@@ -863,6 +881,7 @@ struct Dg {
       st[DG_T1] = (double)__builtin_amdgcn_s_memrealtime();
       st[DG_ST1] = s->st1;
       st[DG_IT1] = s->it1;
+      st[DG_TQ] = s->tq;
     }
     publish(job);
   }
@@ -978,10 +997,40 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
   const bool park = J->park_res != nullptr;
   for (;;) {
     int mode = 0, idx = 0, ev = 0, jj = 0, code = 0;
+    // 0. the eager window: a queued attempt of a running chain that its owner reaches within spec_window attempts
+    //    goes before every problem (the failing chains are the launch's critical paths; the window bounds the
+    //    solves a chain that succeeds early wastes)
+    if (spec && J->spec_window > 0) {
+      int got = -1;
+      if (t == 0) {
+        const unsigned h = __hip_atomic_load(J->spec_eq_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned hh = h;
+        if (h < __hip_atomic_load(J->spec_eq_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+            __hip_atomic_compare_exchange_strong(J->spec_eq_head, &hh, h + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          int e;
+          while ((e = ld_flag(&J->spec_eq[h])) == 0) __builtin_amdgcn_s_sleep(2);
+          after_flag();
+          const int ev_ = (e - 1) / (DG_SPEC_JOBS + 1), jj_ = (e - 1) % (DG_SPEC_JOBS + 1);
+          if (ld_flag(&J->spec_cancel[ev_]) == 0 &&
+              atomicCAS(&J->spec_claim[ev_ * (DG_SPEC_JOBS + 1) + jj_], 0, 1) == 0)
+            got = e - 1;
+        }
+      }
+      got = dg_bcast(got);
+      if (got >= 0) {
+        after_flag();
+        ev = got / (DG_SPEC_JOBS + 1);
+        jj = got % (DG_SPEC_JOBS + 1);
+        dg_spec_prepare<NQ>(J, inp, wg, t, ev, jj);
+        mode = 2;
+        code = 1;
+      }
+    }
     // 0. near the end of the problem queue (spec_early), a queued restart job of a running chain goes before a new
     //    problem: the chains that make the launch tail start getting help before the last problems are handed out
     int pre = 0;
-    if (spec && J->spec_early > 0) {
+    if (mode == 0 && spec && J->spec_early > 0) {
       if (t == 0) {
         const unsigned nx = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (nx < (unsigned)count && nx + (unsigned)J->spec_early >= (unsigned)count)
@@ -991,7 +1040,7 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
       pre = dg_bcast(pre);
     }
     // 1. the next problem: a new one, or a parked one once the new ones run out or park_window parked ones wait
-    if (!pre) {
+    if (mode == 0 && !pre) {
       int got = -1, res = 0;
       if (t == 0) {
         const bool more = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)count;
@@ -1331,6 +1380,7 @@ struct Ts {
       st[DG_T1] = (double)__builtin_amdgcn_s_memrealtime();
       st[DG_ST1] = s->st1;
       st[DG_IT1] = s->it1;
+      st[DG_TQ] = s->t0;
     }
     if (!s->fail && t < NX) J.rows[off * NX + t] = xo(0)[t];
     __syncthreads();
@@ -1547,6 +1597,7 @@ struct Tt {
       st[DG_T1] = (double)__builtin_amdgcn_s_memrealtime();
       st[DG_ST1] = s->st1;
       st[DG_IT1] = s->it1;
+      st[DG_TQ] = s->t0;
     }
     if (ok && t < NXR) J.rows[(long long)job * NXR + t] = xo(0)[t];
     __syncthreads();

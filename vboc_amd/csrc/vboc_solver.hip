@@ -1512,6 +1512,7 @@ struct vboc_solver {
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
   int dg_spec_early = 0;            // restart jobs before new problems once this few problems are left (0: only after)
+  int dg_spec_window = 2;           // eager window: a chain's next attempts that go before every problem (dg.h)
   int dg_spec_min_ext = 0;          // (-DVBOC_SPEC_MIN_EXT builds) restart jobs only from this extension solve on
   double* wave_hc = nullptr;        // path-constraint rows of the wave solver, one region per workgroup
   long long wave_hc_doubles = 0;
@@ -1882,6 +1883,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "dg_fail_mod") h->dg_fail_mod = (int)v;
   else if (s == "dg_speculate") h->dg_speculate = v != 0.0;
   else if (s == "dg_spec_early") h->dg_spec_early = v > 0.0 ? (int)v : 0;
+  else if (s == "dg_spec_window") h->dg_spec_window = v > 0.0 ? (v < 9.0 ? (int)v : 9) : 0;
   else if (s == "dg_park") h->dg_park = v != 0.0;
   else if (s == "dg_park_window") h->dg_park_window = v > 0.0 ? (int)v : 0;
   else if (s == "dg_park_hi") h->dg_park_hi = v > 0.0 ? (int)v : 0;
@@ -1924,6 +1926,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
   else if (s == "dg_speculate") *v = h->dg_speculate ? 1.0 : 0.0;
   else if (s == "dg_spec_early") *v = (double)h->dg_spec_early;
+  else if (s == "dg_spec_window") *v = (double)h->dg_spec_window;
   else if (s == "dg_park") *v = h->dg_park ? 1.0 : 0.0;
   else if (s == "dg_park_window") *v = (double)h->dg_park_window;
   else if (s == "dg_park_hi") *v = (double)h->dg_park_hi;
@@ -2415,7 +2418,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   J.done_flag = done_flag; J.cancel = cancel;
   // counters: [0] job queue, [1] finished problems, [2..3] error flags, [4..5] rows used (u64),
   // [6] speculation events, [7] / [8] restart-job queue tail / head, [10..13] speculative solves run / used (u64),
-  // [16..17] / [18..19] parked-job queue tails / heads
+  // [16..17] / [18..19] parked-job queue tails / heads, [20] / [21] eager restart-job queue tail / head
   J.next = h->head; J.done = h->head + 1; J.err = h->head + 2; J.rows_next = (unsigned long long*)(h->head + 4);
   J.spec_ev_next = h->head + 6; J.spec_q_tail = h->head + 7; J.spec_q_head = h->head + 8;
   J.spec_count = (unsigned long long*)(h->head + 10);
@@ -2424,13 +2427,14 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
 #ifdef VBOC_SPEC_MIN_EXT
   J.spec_min_ext = h->dg_spec_min_ext;
 #endif
-  J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = nullptr;
+  J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = J.spec_eq = nullptr;
+  J.spec_window = 0; J.spec_eq_tail = h->head + 20; J.spec_eq_head = h->head + 21;
   size_t spec_ctl = 0;
   if (h->dg_speculate && !testing) {
     const int E = b->B < 8192 ? b->B : 8192;
     const long long res = 4 + (long long)(nm + 1) * NXR + (long long)nm * NU;
     const long long stride = DG_SPEC_HDR + DG_SPEC_JOBS * res;
-    spec_ctl = sizeof(int) * ((size_t)E * (2 * (DG_SPEC_JOBS + 1) + 1 + DG_SPEC_JOBS));
+    spec_ctl = sizeof(int) * ((size_t)E * (2 * (DG_SPEC_JOBS + 1) + 1 + 2 * DG_SPEC_JOBS));
     const size_t sneed = spec_ctl + sizeof(double) * (size_t)E * (size_t)stride + 256;
     if (sneed > h->dg_spec_bytes) {
       if (h->dg_spec) (void)hipFree(h->dg_spec);
@@ -2444,7 +2448,9 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
     J.spec_claim = ci; ci += (size_t)E * (DG_SPEC_JOBS + 1);
     J.spec_done = ci; ci += (size_t)E * (DG_SPEC_JOBS + 1);
     J.spec_cancel = ci; ci += E;
-    J.spec_q = ci;
+    J.spec_q = ci; ci += (size_t)E * DG_SPEC_JOBS;
+    J.spec_eq = ci;
+    J.spec_window = h->dg_spec_window;
     J.spec = (double*)((char*)h->dg_spec + ((spec_ctl + 255) & ~(size_t)255));
     J.spec_events = E; J.spec_stride = (int)stride;
     HIPCHK(hipMemsetAsync(h->dg_spec, 0, spec_ctl, st));
@@ -2459,7 +2465,6 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
     const size_t pneed = qbytes + sizeof(double) * (size_t)stride * (size_t)b->B;
     if (pneed > h->dg_park_bytes) {
       if (h->dg_park_buf) (void)hipFree(h->dg_park_buf);
-  if (h->mpc_buf) (void)hipFree(h->mpc_buf);
       h->dg_park_buf = nullptr;
       h->dg_park_bytes = 0;
       if (hipMalloc(&h->dg_park_buf, pneed) != hipSuccess)

@@ -217,7 +217,7 @@ class DirTrainer:
         # ran in the round-3 fault (profiles/r03f_vboc_loop_fault.log), and nothing of a
         # destroyed graph is referenced by the next one.
         gen = torch.Generator(device=self.device)
-        gen.manual_seed(self.seed * 1_000_003 + self.fits)
+        gen.manual_seed(self.fit_seed(self.seed, self.fits))
         if self.graphs:
             s = torch.cuda.Stream(self.device)
             s.wait_stream(torch.cuda.current_stream(self.device))
@@ -241,6 +241,11 @@ class DirTrainer:
                 steps += 1
         self.total_steps += steps
         return dict(iterations=int(self.it.item()) - 1, val=float(self.val.item()), launched=steps)
+
+    @staticmethod
+    def fit_seed(seed, fit):
+        """The seed of the minibatch generator of a trainer's fit number `fit` (1, 2, ...)."""
+        return seed * 1_000_003 + fit
 
     @torch.no_grad()
     def predict(self, Xin, batch=1 << 15):
