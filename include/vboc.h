@@ -174,10 +174,11 @@ int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const dou
  *   row_off[B], row_cnt[B]  block of problem b; row_cnt -1 = the reference returns None
  *   ic[B][4], ic_slot[B]    double pendulum store_ic and its tuple position (1 success, 2 failure);
  *                       may be NULL for the triple
- *   stats[B][10]        OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, start and
+ *   stats[B][11]        OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, start and
  *                       end time of the problem on its wave (device real-time clock, 100 MHz ticks), the
  *                       first solve's status and SQP iterations, and when a wave took the problem's last job
- *                       (its start, or its resume when its first solve was parked)
+ *                       (its start, or its resume when its first solve was parked), and how many of its
+ *                       solves were speculative restarts solved by other waves
  *   rows_used           OUT: rows written
  *   spec_solves, spec_used  OUT: speculative restarts (below)
  * Requires N_start + 12 <= nmax of the handle.
@@ -246,7 +247,7 @@ typedef struct {
   double ulim[4];           /* |u| <= ulim (nq entries) */
   double* rows;             /* device [B][2nq + 1]: x0 with the dt column (row_cnt 1) */
   int* row_cnt;             /* device [B]: 1, or -1 for None */
-  double* stats;            /* device [B][10]: as vboc_dg_batch_t.stats */
+  double* stats;            /* device [B][11]: as vboc_dg_batch_t.stats */
 } vboc_tt_batch_t;
 
 int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream);

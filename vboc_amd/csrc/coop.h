@@ -375,10 +375,23 @@ struct Coop {
   // Issued as inline asm: with the builtin, the compiler cannot tell the ring slots apart inside the one
   // dynamic LDS array and drains every in-flight DMA (vmcnt(0)) before each ds_read of the ring.  The asm
   // op is invisible to the compiler's own VMEM count, which can then only over-wait, never under-wait.
+  // TAG: 1 factor, 2 vector pass, 4 forward sweep, 8 costate (measurement builds: -DVBOC_SBASE_DMA converts every
+  // ring to the SGPR-base form, -DVBOC_SBASE_MASK=<mask> only the rings in the mask)
+  template <int TAG>
   __device__ __forceinline__ void dma(int k, int lo, int W, int dst, int part) const {
     const int nc = W / 2;
     const int c = part * 64 + t < nc ? part * 64 + t : nc - 1;
-#ifndef VBOC_SBASE_DMA
+#ifndef VBOC_SBASE_MASK
+#ifdef VBOC_SBASE_DMA
+#define VBOC_SBASE_MASK 15
+#else
+#define VBOC_SBASE_MASK 0
+#endif
+#endif
+    if constexpr ((VBOC_SBASE_MASK & TAG) != 0) {
+      dma_s(g + (long long)k * REC, 8u * (unsigned)(lo + 2 * c), dst + part * 128);
+      return;
+    }
     // per-lane 64-bit addresses.  The SGPR-base form (dma_s, -DVBOC_SBASE_DMA) gives the pendulum chains the same
     // bits, but deterministically broke the UR5 instantiation (k_wave<4>: 24 % status agreement with the oracle,
     // tools/ur5_bisect.sh, profiles/r03z_ur5_sgpr_base_dma_bisect.log) for a reason not found; the grouped
@@ -390,9 +403,6 @@ struct Coop {
                  : "=&s"(keep)
                  : "v"(src), "s"(lds)
                  : "memory");
-#else
-    dma_s(g + (long long)k * REC, 8u * (unsigned)(lo + 2 * c), dst + part * 128);
-#endif
   }
   // the same with a wave-uniform base (SGPR pair) and a per-lane byte offset: no per-lane 64-bit address
   // arithmetic in the recursions' loops (the lane offsets are computed once per pass)
@@ -1056,7 +1066,7 @@ struct Coop {
     constexpr int P = L::P_FAC;
     auto fdma = [&](int j) {
       const int kk = N - 1 - j >= 0 ? N - 1 - j : 0;
-      UNR for (int part = 0; part < P; ++part) dma(kk, 0, L::W_FAC, fslot(j % L::NSF), part);
+      UNR for (int part = 0; part < P; ++part) dma<1>(kk, 0, L::W_FAC, fslot(j % L::NSF), part);
     };
     __syncthreads();   // before any DMA is in flight: this barrier's fence would drain them
     settle();
@@ -1184,7 +1194,7 @@ struct Coop {
     constexpr int P = L::P_FAC;
     auto fdma = [&](int j) {
       const int kk = N - 1 - j >= 0 ? N - 1 - j : 0;
-      UNR for (int part = 0; part < P; ++part) dma(kk, 0, L::W_FAC, fslot(j % L::NSF), part);
+      UNR for (int part = 0; part < P; ++part) dma<1>(kk, 0, L::W_FAC, fslot(j % L::NSF), part);
     };
     // loop-invariant per-lane constants.  A lane without a G / H operand reads the zeroed LDS words (ZERO,
     // absolute: slot base multiplier 0), never the slot's tail: the tail holds whatever the record's next
@@ -1486,7 +1496,7 @@ struct Coop {
     constexpr int PV = L::P_VEC;
     auto vdma = [&](int j) {
       const int kk = N - 1 - j >= 1 ? N - 1 - j : 1;
-      UNR for (int part = 0; part < PV; ++part) dma(kk, L::LO_VEC, L::W_VEC, vslot(j % L::NSV), part);
+      UNR for (int part = 0; part < PV; ++part) dma<2>(kk, L::LO_VEC, L::W_VEC, vslot(j % L::NSV), part);
     };
     auto vld = [&](int kb, double (&acl)[NX], double& cc, double& pe) {
       const int i = t < NX ? t : NX - 1;
@@ -1696,7 +1706,7 @@ struct Coop {
     constexpr int PW = L::P_FWD;
     auto wdma = [&](int j) {
       const int kk = 1 + j < N ? 1 + j : N - 1;
-      UNR for (int part = 0; part < PW; ++part) dma(kk, L::LO_FWD, L::W_FWD, vslot(j % L::NSV), part);
+      UNR for (int part = 0; part < PW; ++part) dma<4>(kk, L::LO_FWD, L::W_FWD, vslot(j % L::NSV), part);
     };
     auto fld = [&](int kb, double (&acl)[NX], double& cc) {
       const int i = t < NX ? t : NX - 1;
@@ -1876,7 +1886,7 @@ struct Coop {
     constexpr int PC = L::P_COS;
     auto cdma = [&](int j) {
       const int kk = N - 1 - j >= 1 ? N - 1 - j : 1;
-      UNR for (int part = 0; part < PC; ++part) dma(kk, 0, L::W_COS, vslot(j % L::NSV), part);
+      UNR for (int part = 0; part < PC; ++part) dma<8>(kk, 0, L::W_COS, vslot(j % L::NSV), part);
     };
     auto cterms = [&](int kb, double (&ac)[NX], double& cc) {
       const int i = t < NX ? t : NX - 1;

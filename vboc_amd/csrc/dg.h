@@ -100,13 +100,14 @@ constexpr int DG_SPEC_HDR = 48;   // doubles of an event's snapshot header
 // per-problem statistics: OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, and
 // the wave's start / end time of the problem (s_memrealtime, 100 MHz constant clock)
 // and the first solve's status and SQP iterations, and when a wave took the problem's last job (its start, or
-// its resume when it was parked: the last of these over a launch is when the job queues drained)
-enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST1, DG_IT1, DG_TQ, DG_NSTAT };
+// its resume when it was parked: the last of these over a launch is when the job queues drained), and how many of
+// its solves were speculative restarts solved by other waves
+enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST1, DG_IT1, DG_TQ, DG_TAKEN, DG_NSTAT };
 
 template <int NQ>
 struct DgState {
   int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, spec_ev,
-      spec_base, resumed;
+      spec_base, resumed, taken;
   double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
   double sqp, nsqp, nqp, t0, st1, it1, tq;
   double ran[2], store_ic[4], xsym[2 * NQ];
@@ -313,7 +314,7 @@ struct Dg {
     s->tq = s->t0;
     const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max, eps = J.eps;
     s->phase = HEXT; s->N = J.N_start; s->ext = 0; s->f = 0; s->at_limit = 0; s->N_test = 0; s->ver = 0;
-    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0;
+    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0; s->taken = 0;
     s->resumed = 0;
     s->sqp = 0.0; s->nsqp = 0.0; s->nqp = 0.0; s->cost = 1e6;
     int di = 0;
@@ -573,6 +574,7 @@ struct Dg {
     ((int*)in.sqp_iter)[wg] = (int)ld_coh(r + 2);
     ((int*)in.qp_iter)[wg] = (int)ld_coh(r + 3);
     request(N);
+    s->taken += 1;
     if (t == 0) atomicAdd(&J.spec_count[1], 1ull);
     __syncthreads();
   }
@@ -882,6 +884,7 @@ struct Dg {
       st[DG_ST1] = s->st1;
       st[DG_IT1] = s->it1;
       st[DG_TQ] = s->tq;
+      st[DG_TAKEN] = (double)s->taken;
     }
     publish(job);
   }
@@ -1381,6 +1384,7 @@ struct Ts {
       st[DG_ST1] = s->st1;
       st[DG_IT1] = s->it1;
       st[DG_TQ] = s->t0;
+      st[DG_TAKEN] = 0.0;
     }
     if (!s->fail && t < NX) J.rows[off * NX + t] = xo(0)[t];
     __syncthreads();
@@ -1598,6 +1602,7 @@ struct Tt {
       st[DG_ST1] = s->st1;
       st[DG_IT1] = s->it1;
       st[DG_TQ] = s->t0;
+      st[DG_TAKEN] = 0.0;
     }
     if (ok && t < NXR) J.rows[(long long)job * NXR + t] = xo(0)[t];
     __syncthreads();

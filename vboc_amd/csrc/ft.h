@@ -190,8 +190,12 @@ struct Ft {
 
   // ---- Safe-MPC terminal row (all lanes; x uniform): h(x) = NN(z(x)) - vn(x), grad (NX, uniform) if asked ----
   // Hidden unit i of a layer lives on lane i mod 64; layer 2 streams W1T row by row (64 consecutive doubles per
-  // load across the wave), the backward pass W1 row by row; the few reductions are shuffles.
+  // load across the wave), the backward pass W1 row by row.  The arithmetic is the oracle's (oracle/vboc_oracle_ft.c
+  // nn_row) operation for operation: no contraction, every sum in the oracle's order - the two sums over hidden
+  // units (the output and d out / d z) run serially over LDS on every lane (a few thousand cycles per evaluation,
+  // once per SQP iteration and line-search trial), so the row and its gradient are bit-identical to the oracle's.
   __device__ double nn_row(const double* x, double* grad) {
+#pragma clang fp contract(off)
     const int H = mp.hid;
     double ss = 0.0;
     for (int j = 2; j < N2; ++j) ss += x[j] * x[j];    // norm_2(x[2:]): theta_3 included, as the reference
@@ -218,29 +222,41 @@ struct Ft {
         if (i < H) acc[m] += row[i] * a1;
       }
     }
-    double out = 0.0;
     for (int m = 0; m < MQ; ++m) {
       const int i = t + 64 * m;
-      if (i < H) {
-        const double a2 = acc[m] + mp.b1[i];
-        if (a2 > 0.0) out += mp.W2[i] * a2;
-        sh.nn2[i] = a2 > 0.0 ? mp.W2[i] : 0.0;   // backward weights W2 [a2 > 0]
-      }
+      if (i < H) sh.nn2[i] = acc[m] + mp.b1[i];   // layer-2 pre-activations
     }
-    out = ft_wsum(out) + mp.b2[0];
+    __syncthreads();
+    double out = 0.0;
+    for (int i = 0; i < H; ++i) {                 // the oracle's sequential sum (LDS / W2 reads broadcast)
+      const double a2 = sh.nn2[i];
+      if (a2 > 0.0) out += mp.W2[i] * a2;
+    }
+    out += mp.b2[0];
     if (grad) {
       __syncthreads();
-      double gz[N2];
-      for (int j = 0; j < N2; ++j) gz[j] = 0.0;
-      for (int m = 0; m < MQ; ++m) {   // g1[j] = sum_i W1[i][j] w_i for the lane's j, then through layer 1
+      for (int i = t; i < H; i += 64) sh.nn2[i] = sh.nn2[i] > 0.0 ? mp.W2[i] : 0.0;   // W2 [a2 > 0]
+      __syncthreads();
+      double g1[MQ];
+      for (int m = 0; m < MQ; ++m) {   // g1[j] = sum_i W1[i][j] w_i (i ascending) for the lane's j
         const int j = t + 64 * m;
+        g1[m] = 0.0;
         if (j >= H) continue;
-        double g1 = 0.0;
-        for (int i = 0; i < H; ++i) g1 += mp.W1[(long long)i * H + j] * sh.nn2[i];
-        if (sh.nn1[j] > 0.0)
-          for (int q = 0; q < N2; ++q) gz[q] += g1 * mp.W0[j * N2 + q];
+        for (int i = 0; i < H; ++i) g1[m] += mp.W1[(long long)i * H + j] * sh.nn2[i];
       }
-      for (int q = 0; q < N2; ++q) gz[q] = ft_wsum(gz[q]);
+      __syncthreads();
+      for (int m = 0; m < MQ; ++m) {
+        const int j = t + 64 * m;
+        if (j < H) sh.nn2[j] = g1[m];
+      }
+      __syncthreads();
+      double gz[N2];
+      for (int q = 0; q < N2; ++q) gz[q] = 0.0;
+      for (int i = 0; i < H; ++i) {                // through layer 1, i ascending as the oracle
+        if (!(sh.nn1[i] > 0.0)) continue;
+        const double gi = sh.nn2[i];
+        for (int q = 0; q < N2; ++q) gz[q] += gi * mp.W0[i * N2 + q];
+      }
       double dvn[N2];
       for (int j = 0; j < N2; ++j) dvn[j] = (nrm > 1e-3 && j >= 2) ? x[j] / nrm : 0.0;
       for (int j = 0; j < N2; ++j) {
