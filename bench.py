@@ -442,6 +442,7 @@ def run(args, engine_factory=None):
                 "note": "last timed launch, device real-time clock from the first problem's start; queue_drained = "
                         "the last job (a new problem or a parked one's resume) taken"}
         tail["after_drain_share"] = round(1.0 - tail["queue_drained_ms"] / max(tail["last_finish_ms"], 1e-9), 3)
+        tail["stage_ipm_iters"] = float(st[:, 4].sum())   # sum of N x QP iterations over the launch's solves
     sqp = np.concatenate(rec["sqp"]) if rec["sqp"] else np.zeros(1)
     ok = np.concatenate(rec["status"]) if rec["status"] else np.zeros(1)
     if beat is not None:

@@ -174,11 +174,12 @@ int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const dou
  *   row_off[B], row_cnt[B]  block of problem b; row_cnt -1 = the reference returns None
  *   ic[B][4], ic_slot[B]    double pendulum store_ic and its tuple position (1 success, 2 failure);
  *                       may be NULL for the triple
- *   stats[B][11]        OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, start and
+ *   stats[B][13]        OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, start and
  *                       end time of the problem on its wave (device real-time clock, 100 MHz ticks), the
  *                       first solve's status and SQP iterations, and when a wave took the problem's last job
  *                       (its start, or its resume when its first solve was parked), and how many of its
- *                       solves were speculative restarts solved by other waves
+ *                       solves were speculative restarts solved by other waves, the ticks it waited for them and
+ *                       the sum over them of (job start - the chain's first failure)
  *   rows_used           OUT: rows written
  *   spec_solves, spec_used  OUT: speculative restarts (below)
  * Requires N_start + 12 <= nmax of the handle.
@@ -188,7 +189,7 @@ int vboc_rk4_sens_batch_host(int nq, int B, double T, const double* x, const dou
  * the sequential chain.  Only solves the problem consumes count in stats.  They run on waves the problem queue
  * no longer feeds; solver option "dg_spec_early" = n (default 0) lets queued restart jobs go before new problems
  * once at most n problems are left (measured: no gain at n = 5 % of the queue, -10 % when always on).  Solver
- * option "dg_spec_window" = w (default 2, 0..9): the w attempts after the one the problem is solving go before
+ * option "dg_spec_window" = w (default 0 = off, 0..9): the w attempts after the one the problem is solving go before
  * every new or parked problem (a chain that succeeds early wastes at most w solves). */
 typedef struct {
   int B;
@@ -247,7 +248,7 @@ typedef struct {
   double ulim[4];           /* |u| <= ulim (nq entries) */
   double* rows;             /* device [B][2nq + 1]: x0 with the dt column (row_cnt 1) */
   int* row_cnt;             /* device [B]: 1, or -1 for None */
-  double* stats;            /* device [B][11]: as vboc_dg_batch_t.stats */
+  double* stats;            /* device [B][13]: as vboc_dg_batch_t.stats */
 } vboc_tt_batch_t;
 
 int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream);

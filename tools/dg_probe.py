@@ -35,8 +35,8 @@ def main():
     ap.add_argument("--groups", type=int, nargs="*", default=[0])
     ap.add_argument("--park", type=int, nargs="*", default=[1],
                     help="dg_park option values to run (1: parked first solves, the product default; 0: off)")
-    ap.add_argument("--window", type=int, nargs="*", default=[2],
-                    help="dg_spec_window option values to run (2: the product default; 0: off)")
+    ap.add_argument("--window", type=int, nargs="*", default=[0],
+                    help="dg_spec_window option values to run (0: off, the product default)")
     ap.add_argument("--save", default=None, help="write the per-problem stats (lib.DG_STATS) of each launch to "
                                                  "<save>_g<groups>.npy (scheduling studies)")
     a = ap.parse_args()

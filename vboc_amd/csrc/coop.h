@@ -415,7 +415,19 @@ struct Coop {
     // s_nop 4: an "s" operand fresh from readfirstlane / v_readlane, read by a VMEM instruction as its base, needs
     // 5 wait states that hipcc does not insert in front of inline asm (cdna_hip_programming.md, inline asm rules)
     unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+    // (measurement builds: -DVBOC_DMAS_PRE / -DVBOC_DMAS_POST = 16 extra wait states before the block / after the load)
+#ifdef VBOC_DMAS_PRE
+#define VBOC_DMAS_PRE_S "s_nop 7\n\ts_nop 7\n\t"
+#else
+#define VBOC_DMAS_PRE_S ""
+#endif
+#ifdef VBOC_DMAS_POST
+#define VBOC_DMAS_POST_S "s_nop 7\n\ts_nop 7\n\t"
+#else
+#define VBOC_DMAS_POST_S ""
+#endif
+    asm volatile(VBOC_DMAS_PRE_S "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                 VBOC_DMAS_POST_S "s_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(voff), "s"(bs), "s"(lds)
                  : "memory");
@@ -443,7 +455,12 @@ struct Coop {
   // retire every ordinary VMEM op in a way the compiler's waitcnt pass sees (the builtin, vmcnt(0)):
   // called before a ring's first DMA, so no loop-carried register is still "pending" in the pass's
   // bookkeeping - otherwise it re-waits vmcnt(0) inside the loop and drains the ring every stage
-  __device__ __forceinline__ static void settle() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+  __device__ __forceinline__ static void settle() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#ifdef VBOC_RING_ACQ
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // measurement builds: invalidate the vector L1 first
+#endif
+  }
   // write fields [LO, HI) of a factor slot back to stage k's record: exactly one VMEM op
   template <int LO, int HI>
   __device__ __forceinline__ void ring_wb(int slot, int k) const {

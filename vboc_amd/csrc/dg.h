@@ -96,20 +96,23 @@ struct DgJobs {
 // leaves at most 9 further attempts to speculate on
 constexpr int DG_SPEC_JOBS = 9;
 constexpr int DG_SPEC_HDR = 48;   // doubles of an event's snapshot header
+constexpr int DG_SPEC_RH = 6;     // doubles of a job result's header: status, cost, sqp, qp, start, end (device clock)
 
 // per-problem statistics: OCP solves, twin steps, SQP iterations, sum N*sqp_iter, sum N*qp_iter, and
 // the wave's start / end time of the problem (s_memrealtime, 100 MHz constant clock)
 // and the first solve's status and SQP iterations, and when a wave took the problem's last job (its start, or
 // its resume when it was parked: the last of these over a launch is when the job queues drained), and how many of
-// its solves were speculative restarts solved by other waves
-enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST1, DG_IT1, DG_TQ, DG_TAKEN, DG_NSTAT };
+// its solves were speculative restarts solved by other waves, the ticks its wave waited for them, and the sum over
+// them of (job start - the chain's first failure)
+enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST1, DG_IT1, DG_TQ, DG_TAKEN, DG_WAIT, DG_LAG,
+             DG_NSTAT };
 
 template <int NQ>
 struct DgState {
   int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, spec_ev,
       spec_base, resumed, taken;
   double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
-  double sqp, nsqp, nqp, t0, st1, it1, tq;
+  double sqp, nsqp, nqp, t0, st1, it1, tq, wait, lag, tspec;
   double ran[2], store_ic[4], xsym[2 * NQ];
 };
 
@@ -314,7 +317,7 @@ struct Dg {
     s->tq = s->t0;
     const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max, eps = J.eps;
     s->phase = HEXT; s->N = J.N_start; s->ext = 0; s->f = 0; s->at_limit = 0; s->N_test = 0; s->ver = 0;
-    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0; s->taken = 0;
+    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0; s->taken = 0; s->wait = 0.0; s->lag = 0.0;
     s->resumed = 0;
     s->sqp = 0.0; s->nsqp = 0.0; s->nqp = 0.0; s->cost = 1e6;
     int di = 0;
@@ -511,11 +514,11 @@ struct Dg {
   // success.  Results are those of the sequential chain (same inputs, same deterministic solver); unused
   // speculative solves are counted apart (spec_count) and never in the solve statistics.
   enum : int { H_N = 0, H_JS, H_VS, H_QIS, H_QFS, H_RAN, H_QO = H_RAN + 2, H_IC, H_RNG = H_IC + 4, H_PID, H_NJOBS,
-               H_P, H_LB = H_P + NP, H_UB = H_LB + NXR, H_END = H_UB + NXR };
+               H_TS, H_P, H_LB = H_P + NP, H_UB = H_LB + NXR, H_END = H_UB + NXR };
   static_assert(H_END <= DG_SPEC_HDR, "event header");
   __device__ __forceinline__ double* spec_hdr(int ev) const { return J.spec + (long long)ev * J.spec_stride; }
   __device__ __forceinline__ double* spec_res(int ev, int j) const {
-    return spec_hdr(ev) + DG_SPEC_HDR + (long long)(j - 1) * (4 + (J.nmax + 1) * NXR + J.nmax * NU);
+    return spec_hdr(ev) + DG_SPEC_HDR + (long long)(j - 1) * (DG_SPEC_RH + (J.nmax + 1) * NXR + J.nmax * NU);
   }
   __device__ __forceinline__ bool claim(int ev, int j) const {
     int r = 0;
@@ -543,6 +546,7 @@ struct Dg {
     st_coh(h + H_RAN, s->ran[0]); st_coh(h + H_RAN + 1, s->ran[1]); st_coh(h + H_QO, s->q_init_oth);
     UNR for (int c = 0; c < 4; ++c) st_coh(h + H_IC + c, s->store_ic[c]);
     st_coh(h + H_RNG, s->rng_pos); st_coh(h + H_PID, (double)pid); st_coh(h + H_NJOBS, nj);
+    st_coh(h + H_TS, (double)__builtin_amdgcn_s_memrealtime());
     UNR for (int c = 0; c < NP; ++c) st_coh(h + H_P + c, P[c]);
     UNR for (int c = 0; c < NXR; ++c) { st_coh(h + H_LB + c, lb0[c]); st_coh(h + H_UB + c, ub0[c]); }
     if (t == 0) {
@@ -563,12 +567,15 @@ struct Dg {
   // the owner takes job j's result (solved by another wave) as its own solve of the current attempt
   __device__ __forceinline__ void take_result(int ev, int j, int N) {
     const int* dn = &J.spec_done[ev * (DG_SPEC_JOBS + 1) + j];
+    const double tw = (double)__builtin_amdgcn_s_memrealtime();
     while (ld_flag(dn) == 0) __builtin_amdgcn_s_sleep(8);
     after_flag();
     const double* r = spec_res(ev, j);
-    for (int e = t; e < (N + 1) * NXR; e += 64) ((double*)in.xo)[row(0) * NXR + e] = ld_coh(r + 4 + e);
+    s->wait += (double)__builtin_amdgcn_s_memrealtime() - tw;
+    s->lag += ld_coh(r + 4) - ld_coh(spec_hdr(ev) + H_TS);
+    for (int e = t; e < (N + 1) * NXR; e += 64) ((double*)in.xo)[row(0) * NXR + e] = ld_coh(r + DG_SPEC_RH + e);
     for (int e = t; e < N * NU; e += 64)
-      ((double*)in.uo)[((long long)wg * J.nmax) * NU + e] = ld_coh(r + 4 + (J.nmax + 1) * NXR + e);
+      ((double*)in.uo)[((long long)wg * J.nmax) * NU + e] = ld_coh(r + DG_SPEC_RH + (J.nmax + 1) * NXR + e);
     ((int*)in.status)[wg] = (int)ld_coh(r);
     ((double*)in.cost)[wg] = ld_coh(r + 1);
     ((int*)in.sqp_iter)[wg] = (int)ld_coh(r + 2);
@@ -581,6 +588,7 @@ struct Dg {
   // a free wave runs job j of event ev: the owner's restart state plus j perturbations, straight guess
   __device__ __forceinline__ void spec_prepare(int ev, int j) {
     const double* h = spec_hdr(ev);
+    s->tspec = (double)__builtin_amdgcn_s_memrealtime();
     const int N = (int)ld_coh(h + H_N);
     pid = (long long)ld_coh(h + H_PID);
     s->joint_sel = (int)ld_coh(h + H_JS); s->vel_sel = (int)ld_coh(h + H_VS);
@@ -600,10 +608,11 @@ struct Dg {
   __device__ __forceinline__ void spec_store(int ev, int j) {
     const int N = nreq();
     double* r = spec_res(ev, j);
-    for (int e = t; e < (N + 1) * NXR; e += 64) st_coh(r + 4 + e, xo(0)[e]);
-    for (int e = t; e < N * NU; e += 64) st_coh(r + 4 + (J.nmax + 1) * NXR + e, uo(0)[e]);
+    for (int e = t; e < (N + 1) * NXR; e += 64) st_coh(r + DG_SPEC_RH + e, xo(0)[e]);
+    for (int e = t; e < N * NU; e += 64) st_coh(r + DG_SPEC_RH + (J.nmax + 1) * NXR + e, uo(0)[e]);
     st_coh(r, (double)status()); st_coh(r + 1, in.cost[wg]);
     st_coh(r + 2, (double)in.sqp_iter[wg]); st_coh(r + 3, (double)in.qp_iter[wg]);
+    st_coh(r + 4, s->tspec); st_coh(r + 5, (double)__builtin_amdgcn_s_memrealtime());
     if (t == 0) {
       st_flag(&J.spec_done[ev * (DG_SPEC_JOBS + 1) + j], 1);
       atomicAdd(&J.spec_count[0], 1ull);
@@ -885,6 +894,8 @@ struct Dg {
       st[DG_IT1] = s->it1;
       st[DG_TQ] = s->tq;
       st[DG_TAKEN] = (double)s->taken;
+      st[DG_WAIT] = s->wait;
+      st[DG_LAG] = s->lag;
     }
     publish(job);
   }
@@ -1385,6 +1396,8 @@ struct Ts {
       st[DG_IT1] = s->it1;
       st[DG_TQ] = s->t0;
       st[DG_TAKEN] = 0.0;
+      st[DG_WAIT] = 0.0;
+      st[DG_LAG] = 0.0;
     }
     if (!s->fail && t < NX) J.rows[off * NX + t] = xo(0)[t];
     __syncthreads();
@@ -1603,6 +1616,8 @@ struct Tt {
       st[DG_IT1] = s->it1;
       st[DG_TQ] = s->t0;
       st[DG_TAKEN] = 0.0;
+      st[DG_WAIT] = 0.0;
+      st[DG_LAG] = 0.0;
     }
     if (ok && t < NXR) J.rows[(long long)job * NXR + t] = xo(0)[t];
     __syncthreads();

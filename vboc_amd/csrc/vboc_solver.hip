@@ -1512,7 +1512,7 @@ struct vboc_solver {
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
   int dg_spec_early = 0;            // restart jobs before new problems once this few problems are left (0: only after)
-  int dg_spec_window = 2;           // eager window: a chain's next attempts that go before every problem (dg.h)
+  int dg_spec_window = 0;           // eager window: a chain's next attempts that go before every problem (dg.h; off: measured slower)
   int dg_spec_min_ext = 0;          // (-DVBOC_SPEC_MIN_EXT builds) restart jobs only from this extension solve on
   double* wave_hc = nullptr;        // path-constraint rows of the wave solver, one region per workgroup
   long long wave_hc_doubles = 0;
@@ -2432,7 +2432,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   size_t spec_ctl = 0;
   if (h->dg_speculate && !testing) {
     const int E = b->B < 8192 ? b->B : 8192;
-    const long long res = 4 + (long long)(nm + 1) * NXR + (long long)nm * NU;
+    const long long res = DG_SPEC_RH + (long long)(nm + 1) * NXR + (long long)nm * NU;
     const long long stride = DG_SPEC_HDR + DG_SPEC_JOBS * res;
     spec_ctl = sizeof(int) * ((size_t)E * (2 * (DG_SPEC_JOBS + 1) + 1 + 2 * DG_SPEC_JOBS));
     const size_t sneed = spec_ctl + sizeof(double) * (size_t)E * (size_t)stride + 256;

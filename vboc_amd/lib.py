@@ -82,7 +82,7 @@ class MpcBatch(ctypes.Structure):
 
 # per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
 DG_STATS = ("solves", "rk4", "sqp_iter", "n_sqp_iter", "n_qp_iter", "t0", "t1", "first_status", "first_sqp_iter",
-            "t_last_job", "spec_taken")
+            "t_last_job", "spec_taken", "spec_wait", "spec_lag")
 DG_CLOCK_HZ = 100e6
 
 
