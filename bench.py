@@ -113,6 +113,31 @@ def pmc_traffic(kernel, problems=None):
     return d["traffic_bytes_per_launch"] / 1e9, src
 
 
+def dg_counters():
+    """The newest committed driver-shape counter summary of k_dg (profiles/*_k_dg_counters.json, tools/pmc_r04.py over
+    the rocprofv3 --pmc passes of tools/gpu_r04_pmc.sh): (summary dict, path) or (None, None)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_k_dg_counters.json")))
+    if not files:
+        return None, None
+    return json.load(open(files[-1])), os.path.relpath(files[-1], ROOT)
+
+
+def dg_bound_note(c, src):
+    """bound_note of the dg-loop line, computed from the committed counters (verdict r03 item 4)."""
+    w, m = c["wave_time_split"], c["memory_side"]
+    note = ("'mfma' = the FP64 compute roofline SURVEY.md 8(d) prices the path on (algorithmic FP64 flops); what the "
+            f"counters of the driver-shape launch show ({src}): waves {w['issuing']:.0%} issuing (VALU "
+            f"{w['issuing_valu']:.0%}, LDS {w['issuing_lds']:.0%}, SALU {w['issuing_salu']:.0%}), "
+            f"{w['issue_stalled_dependency_pipe']:.0%} stalled on a dependency or pipe, {w['waiting_s_waitcnt_barrier']:.0%} "
+            f"in s_waitcnt; FP64 MFMA busy {c['mfma_busy_share']:.1%}; memory side {m['tb_per_s']:.2f} TB/s "
+            f"({m['bytes_per_stage_ipm_iteration'] / 1e3:.1f} KB per stage-IPM-iteration, L2 hit {c['l2_hit_rate']:.0%})")
+    ab = c.get("bytes_ab")
+    if ab:
+        note += "; " + ab["summary"]
+    return note
+
+
 def dg_flops(nq, stats):
     """SURVEY 8(d) FP64 flops of a data-generation launch from its per-problem stats (lib.DG_STATS):
     sum over solves of N*(F_dyn*K_sqp + F_ipm*K_ipm + 8*C_f*K_sqp), plus 4*C_f per twin step."""
@@ -410,6 +435,11 @@ def run(args, engine_factory=None):
     else:
         pmc_name = ("k_dg" if dgl else "k_wave") + ("" if nq == 3 else f"_nq{nq}")
         traffic_gb, src = pmc_traffic(pmc_name, args.steps * B if dgl else None)
+        ctr, ctr_src = dg_counters() if (dgl and nq == 3) else (None, None)
+        if ctr is not None and rec["stats"] is not None:
+            # bytes per stage-IPM-iteration of the committed driver-shape counters x this launch's stage-IPM-iterations
+            traffic_gb = ctr["memory_side"]["bytes_per_stage_ipm_iteration"] * float(rec["stats"][:, 4].sum()) / 1e9
+            src = ctr_src + " (bytes per stage-IPM-iteration x this launch's)"
         avg_ms = rec["kernel_ms"] / max(1, rec["launches"])
         per_launch = local_flops / max(1, rec["launches"])
         tf = per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms else None
@@ -417,11 +447,9 @@ def run(args, engine_factory=None):
                     "unit": "TFLOP/s", "frac": round(tf / FP64_PEAK_TFLOPS, 5) if tf else None,
                     "traffic": round(traffic_gb, 4) if traffic_gb else None, "traffic_unit": "GB/launch",
                     "traffic_source": src,
-                    "bound_note": "'mfma' names the roofline that applies (FP64 compute: ~3.6 kflop per algorithmic "
-                                  "byte, far right of the ridge), not what binds: the SQ counters show a latency-bound "
-                                  "kernel (waves 31 % parked in s_waitcnt, 31 % dependency-stalled, 38 % issuing, "
-                                  "VALU 23 %; MFMA ~1 % busy) whose resident problems are capped by the 256 MiB MALL "
-                                  "(DESIGN.md section 5; profiles/r03_*)",
+                    "bound_note": dg_bound_note(ctr, ctr_src) if ctr is not None else
+                                  "'mfma' = the FP64 compute roofline SURVEY.md 8(d) prices the path on; no committed "
+                                  "driver-shape counters for this kernel",
                     "pipes": "FP64: Riccati factorisation on v_mfma_f64_16x16x4f64 (factor_mfma), the rest FP64 VALU; "
                              "peak = FP64 dense (vector = matrix on MI355X); latency-bound dependent recursions",
                     "algorithmic": "FP64 flops per launch, SURVEY.md 8(d): sum over solves of "
@@ -434,13 +462,17 @@ def run(args, engine_factory=None):
         st = rec["stats"]
         t0s, t1s = st[:, 5], st[:, 6]
         ms = 1e3 / DG_CLOCK_HZ
+        tqs = st[:, 9]
         tail = {"critical_problem_ms": round(float((t1s - t0s).max()) * ms, 1),
+                "longest_final_run_ms": round(float((t1s - tqs).max()) * ms, 1),
                 "mean_problem_ms": round(float((t1s - t0s).mean()) * ms, 2),
                 "new_problems_drained_ms": round(float(t0s.max() - t0s.min()) * ms, 1),
                 "queue_drained_ms": round(float(st[:, 9].max() - t0s.min()) * ms, 1),
                 "last_finish_ms": round(float(t1s.max() - t0s.min()) * ms, 1),
                 "note": "last timed launch, device real-time clock from the first problem's start; queue_drained = "
-                        "the last job (a new problem or a parked one's resume) taken"}
+                        "the last job (a new problem or a parked one's resume) taken; a problem's time (critical / mean) "
+                        "runs from its first solve to its end and includes the wait of a parked first solve, "
+                        "longest_final_run = the longest stretch from a problem's last job start to its end"}
         tail["after_drain_share"] = round(1.0 - tail["queue_drained_ms"] / max(tail["last_finish_ms"], 1e-9), 3)
         tail["stage_ipm_iters"] = float(st[:, 4].sum())   # sum of N x QP iterations over the launch's solves
     sqp = np.concatenate(rec["sqp"]) if rec["sqp"] else np.zeros(1)

@@ -165,18 +165,20 @@ def test_gpu_rti_matches_oracle(with_row):
 @pytest.mark.gpu
 @pytest.mark.parametrize("with_row", [False, True])
 def test_gpu_sqp_matches_oracle(with_row):
-    """Full SQP (nlp_solver_max_iter 200) on 96 states at the section-3 bars: status >= 98 %, SQP iterations >= 95 %,
-    cost and x_N of problems converged on both: median <= 1e-9, max <= 2e-3 (relative to the cost).  This OCP
-    converges slowly (merit backtracking on the 1e4-weighted tracking term): about 70 % of the states reach 200
-    iterations on both sides (status 2), so the cost / x_N bars also apply to those - the two runs' 200th iterates."""
+    """Full SQP (nlp_solver_max_iter 1000, the class's own setting, :153-161) on 96 states at the section-3 bars:
+    status >= 98 %, SQP iterations >= 95 %, cost and x_N of problems converged on both: median <= 1e-9, max <= 2e-3
+    (relative to the cost).  From these random states (any position in the box, |dtheta| <= 2) the SQP to
+    tol_stat 1e-6 stalls for about half of them: they reach 1000 iterations on both sides (status 2, the same
+    problems), so the cost / x_N bars also apply to those - the two runs' 1000th iterates.  (At a cap of 200, 2 of
+    96 problems that converge just before / after the 200th iteration on one side made the status bar 97.9 %.)"""
     P = _net() if with_row else None
     sp, x0, xg, ug = _states(96, seed=7)
-    g = _gpu(sp, P, x0, xg, ug, rti=False, max_iter=200)
-    o = oracle.default_opts(lm=sp.lm, tol_stat=1e-6, qp_tol_stat=1e-8, max_iter=200)
+    g = _gpu(sp, P, x0, xg, ug, rti=False, max_iter=1000)
+    o = oracle.default_opts(lm=sp.lm, tol_stat=1e-6, qp_tol_stat=1e-8, max_iter=1000)
     x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, opts=o)
     assert (g["status"] == r["status"]).mean() >= 0.98, (g["status"], r["status"])
     assert (g["sqp_iter"] == r["sqp_iter"]).mean() >= 0.95, (g["sqp_iter"], r["sqp_iter"])
-    for st_, least in ((0, 24), (2, 40)):
+    for st_, least in ((0, 30), (2, 40)):
         both = (g["status"] == st_) & (r["status"] == st_)
         assert both.sum() >= least, (st_, both.sum())
         dc = np.abs(g["cost"] - r["cost"])[both] / np.abs(r["cost"][both])
