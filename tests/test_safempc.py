@@ -166,8 +166,8 @@ def test_gpu_rti_matches_oracle(with_row):
 @pytest.mark.parametrize("with_row", [False, True])
 def test_gpu_sqp_matches_oracle(with_row):
     """Full SQP (nlp_solver_max_iter 1000, the class's own setting, :153-161) on 96 states at the section-3 bars:
-    status >= 98 %, SQP iterations >= 95 %, cost and x_N of problems converged on both: median <= 1e-9, max <= 2e-3
-    (relative to the cost).  From these random states (any position in the box, |dtheta| <= 2) the SQP to
+    status >= 98 %, SQP iterations >= 95 % or as close as the oracle is to itself under a 1e-15 perturbation (below),
+    cost and x_N of problems converged on both: median <= 1e-9, max <= 2e-3 (relative to the cost).  From these random states (any position in the box, |dtheta| <= 2) the SQP to
     tol_stat 1e-6 stalls for about half of them: they reach 1000 iterations on both sides (status 2, the same
     problems), so the cost / x_N bars also apply to those - the two runs' 1000th iterates.  (At a cap of 200, 2 of
     96 problems that converge just before / after the 200th iteration on one side made the status bar 97.9 %.)"""
@@ -177,7 +177,17 @@ def test_gpu_sqp_matches_oracle(with_row):
     o = oracle.default_opts(lm=sp.lm, tol_stat=1e-6, qp_tol_stat=1e-8, max_iter=1000)
     x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, opts=o)
     assert (g["status"] == r["status"]).mean() >= 0.98, (g["status"], r["status"])
-    assert (g["sqp_iter"] == r["sqp_iter"]).mean() >= 0.95, (g["sqp_iter"], r["sqp_iter"])
+    # The SQP-iteration bar, calibrated: on this OCP the converged iteration count moves with rounding - the oracle
+    # against ITSELF with the guess perturbed by 1e-15 (relative) agrees on 95 % (no row) / 74 % (row) of the
+    # problems, with equal status and final costs to 1e-16 (measured, round 4).  The GPU must be as close to the
+    # oracle as the oracle is to that perturbed copy of itself (5 points of slack).
+    xg2 = xg * (1 + 1e-15 * np.random.default_rng(0).standard_normal(xg.shape))
+    xg2[:, 0] = x0
+    _, _, r2, _ = oracle.mpc_solve_batch(sp, x0, xg2, ug, P, mean=MEAN, std=STD, opts=o)
+    self_agree = (r2["sqp_iter"] == r["sqp_iter"]).mean()
+    gpu_agree = (g["sqp_iter"] == r["sqp_iter"]).mean()
+    print(f"SQP-iteration agreement: GPU vs oracle {gpu_agree:.3f}, oracle vs 1e-15-perturbed oracle {self_agree:.3f}")
+    assert gpu_agree >= min(0.95, self_agree - 0.05), (gpu_agree, self_agree)
     for st_, least in ((0, 30), (2, 40)):
         both = (g["status"] == st_) & (r["status"] == st_)
         assert both.sum() >= least, (st_, both.sum())
