@@ -64,6 +64,7 @@ struct DgJobs {
   // speculative restarts (see "Speculative restarts" below); spec_events == 0 switches them off
   int spec_events, spec_stride;   // events in the pool, doubles per event
   int spec_early;                 // once at most this many problems are left unclaimed, queued restart jobs go first
+  int spec_first;                 // 1: once the new problems run out, queued restart jobs go before parked resumes
 #ifdef VBOC_SPEC_MIN_EXT
   int spec_min_ext;               // (measurement builds) a failed chain publishes restart jobs only from this solve on
 #endif
@@ -1044,10 +1045,14 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
     // 0. near the end of the problem queue (spec_early), a queued restart job of a running chain goes before a new
     //    problem: the chains that make the launch tail start getting help before the last problems are handed out
     int pre = 0;
-    if (mode == 0 && spec && J->spec_early > 0) {
+    //    With parked first solves (spec_first), the same once the new problems run out: the chains still open
+    //    then are the launch's critical paths, and every parked resume after them is short work
+    if (mode == 0 && spec && (J->spec_early > 0 || (park && J->spec_first))) {
       if (t == 0) {
         const unsigned nx = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (nx < (unsigned)count && nx + (unsigned)J->spec_early >= (unsigned)count)
+        const bool near = (J->spec_early > 0 && nx < (unsigned)count && nx + (unsigned)J->spec_early >= (unsigned)count) ||
+                          (park && J->spec_first && nx >= (unsigned)count);
+        if (near)
           pre = __hip_atomic_load(J->spec_q_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                 __hip_atomic_load(J->spec_q_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
