@@ -11,7 +11,11 @@ pair says why:
                test, the at-limit tests, the stop rule) flipped on a rounding-level difference;
   'status'   - the two solvers returned different statuses for the same request (a rounding-level difference
                that changed the SQP path enough to hit max_iter or a QP failure on one side only);
-  'value'    - same status, results differ beyond rounding (a genuine solver disagreement).
+  'optimum'  - same status 0, results differ beyond rounding, and each side's result is confirmed as a solution of the
+               request by an independent check (`verify`, e.g. the oracle warm-started from it converges back to it):
+               the two solvers reached two different local optima of the same nonconvex NLP after a rounding-level
+               difference early in a long SQP path;
+  'value'    - same status, results differ beyond rounding and not both confirmed (a genuine solver disagreement).
 Problems that end on the same path with the same result are 'same'."""
 import numpy as np
 
@@ -55,9 +59,9 @@ def _answers(nq, backend, reqs, nmax):
     return out
 
 
-def lockstep(nq, make_gen, ids, backend_a, backend_b, nmax=200):
+def lockstep(nq, make_gen, ids, backend_a, backend_b, nmax=200, verify=None):
     """make_gen(pid) -> a fresh generator.  Returns {pid: (kind, detail)} with kind in same / decision /
-    status / value (see the module doc) and the final results of copy A."""
+    status / optimum / value (see the module doc).  verify(request, solution) -> bool confirms a solution."""
     ga = {p: make_gen(p) for p in ids}
     gb = {p: make_gen(p) for p in ids}
     ra, rb, kind = {}, {}, {}
@@ -84,7 +88,9 @@ def lockstep(nq, make_gen, ids, backend_a, backend_b, nmax=200):
                     last[p] = "value"
             else:
                 c = _close_solve(aa[p], ab[p])
-                if c != "ok":
+                if c == "value" and verify is not None and verify(pa[p], aa[p]) and verify(pb[p], ab[p]):
+                    c = "optimum"
+                if c != "ok" and last[p] != "value":
                     last[p] = c
             done_a = done_b = False
             try:
