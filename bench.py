@@ -213,7 +213,8 @@ class GpuEngine:
         with open(path, "rb") as f:
             digest = hashlib.sha1(f.read()).hexdigest()
         return {"path": os.path.relpath(path, ROOT), "sha1": digest,
-                "variant": bool(os.environ.get("VBOC_LIB")), "resident_problems": int(self.solver.get_option("wave_groups"))}
+                "variant": bool(os.environ.get("VBOC_LIB")),
+                "resident_problems": int(self.solver.get_option("last_groups"))}   # of the last launch
 
 
 def cpu_baseline(nq, workload, B, seconds, threads):
