@@ -188,10 +188,13 @@ def test_device_loop_restart_branches_match_host_driver(nq):
 
 
 @pytest.mark.gpu
-def test_speculative_restarts_change_nothing():
+@pytest.mark.parametrize("opts", [{}, {"dg_spec_window": 2}, {"dg_spec_first": 1}, {"dg_park": 0}],
+                         ids=["default", "window2", "spec_first", "no_park"])
+def test_speculative_restarts_change_nothing(opts):
     """Speculative restarts (dg_speculate) only run later attempts early: with and without them the
-    device loop returns the same rows, counts and per-problem statistics (timing fields aside), here on
-    a batch where the failure injection makes many chains fail."""
+    device loop returns the same rows, counts and per-problem statistics (timing and speculation fields aside),
+    here on a batch where the failure injection makes many chains fail - also with the eager window, with restart
+    jobs before parked resumes, and without parking."""
     import torch
     from vboc_amd import lib
     ids = torch.arange(7000, 7000 + 512, dtype=torch.int64, device="cuda:0")
@@ -200,11 +203,14 @@ def test_speculative_restarts_change_nothing():
         s = lib.Solver(3, 120)
         s.set_option("dg_fail_mod", 3)
         s.set_option("dg_speculate", spec)
+        if spec:
+            for k, v in opts.items():
+                s.set_option(k, v)
         outs.append(s.data_generation_device(ids))
     a, b = outs
     assert a["spec_solves"] > 0 and b["spec_solves"] == 0
     assert torch.equal(a["row_cnt"], b["row_cnt"])
-    keep = [0, 1, 2, 3, 4, 7, 8]   # stats without the timing fields
+    keep = [0, 1, 2, 3, 4, 7, 8]   # stats without the timing / speculation fields
     assert torch.equal(a["stats"][:, keep], b["stats"][:, keep])
     cnt = a["row_cnt"].cpu().numpy()
     ra, rb = a["rows"].cpu().numpy(), b["rows"].cpu().numpy()
