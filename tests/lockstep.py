@@ -7,7 +7,7 @@ two answers are compared.  While both copies issue the same kind of request (sam
 answers that agree to rounding, the copies are on the same path.  When they part, the first differing answer
 pair says why:
   'decision' - every answer so far agreed to rounding (same status; |d cost| <= 1e-6 (1 + |cost|), |d x_0| <=
-               1e-6; twin steps to 1e-9): a tolerance decision of the state machine (the horizon-extension
+               1e-5; twin steps from the same inputs to 1e-9): a tolerance decision of the state machine (the horizon-extension
                test, the at-limit tests, the stop rule) flipped on a rounding-level difference;
   'status'   - the two solvers returned different statuses for the same request (a rounding-level difference
                that changed the SQP path enough to hit max_iter or a QP failure on one side only);
@@ -27,7 +27,10 @@ def _close_solve(a, b):
         return "status"
     if a.status != 0:
         return "ok"       # failed solves: the iterate is not a result
-    if abs(a.cost - b.cost) > 1e-6 * (1 + abs(b.cost)) or np.abs(a.x[0] - b.x[0]).max() > 1e-6:
+    # x_0 to 1e-5, the tolerance of the result comparison: a solve that stops at tol_stat 1e-3 after hundreds of
+    # SQP iterations (the widened fixture's long-tail problem 1464: 531 / 664 iterations) ends 1.2e-6 from the other
+    # solver's stop with the same cost to 2e-7
+    if abs(a.cost - b.cost) > 1e-6 * (1 + abs(b.cost)) or np.abs(a.x[0] - b.x[0]).max() > 1e-5:
         return "value"
     return "ok"
 

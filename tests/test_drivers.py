@@ -226,10 +226,10 @@ def test_gpu_driver_mismatches_are_rounding_level_flips(nq, law):
     path that hits max_iter or a QP failure on one side).  A same-status result that differs beyond
     rounding and not confirmed as a solution on both sides ('value') is a defect and fails the test; a parting into
     two oracle-confirmed solutions ('optimum') and 'decision' flips stay a minority.  Measured on the widened triple
-    fixture (261 problems, gpurun_out/r04l/lockstep.json): 6 problems part, every solve pair within the lockstep
-    tolerances but one (x_0 1.2e-6 apart after 531 / 664 SQP iterations), their rows apart beyond 1e-5 because the
-    solves stop at tol_stat 1e-3 at different iterates; round 3's classifier also compared twin steps taken from
-    states that already differed, which it now skips."""
+    fixture (261 problems, profiles/r04_lockstep_triple_partings.json): 6 problems part, every solve pair within the
+    lockstep tolerances (one x_0 1.2e-6 apart after 531 / 664 SQP iterations), their rows apart beyond 1e-5 because
+    the solves stop at tol_stat 1e-3 at different iterates - 'decision'; round 3's classifier also compared twin
+    steps taken from states that already differed, which it now skips."""
     from lockstep import lockstep
     from vboc_amd.drivers import GpuBackend
     g = _golden(nq) if law == "dg" else _golden_test(nq)
