@@ -389,6 +389,9 @@ struct Coop {
 #endif
 #endif
     if constexpr ((VBOC_SBASE_MASK & TAG) != 0) {
+#ifdef VBOC_SBASE_NOHOIST
+      asm volatile("" : "+s"(k));   // measurement builds: the stage base is computed here, not hoisted / spilled
+#endif
       dma_s(g + (long long)k * REC, 8u * (unsigned)(lo + 2 * c), dst + part * 128);
       return;
     }
