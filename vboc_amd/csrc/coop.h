@@ -259,6 +259,10 @@ __device__ __forceinline__ void tri(int u, int& i, int& j) {
 // register allocation and schedule close to the product build.
 __device__ unsigned long long g_wave_prof[16];
 __device__ unsigned g_dbg_cnt;
+// measurement builds (-DVBOC_VEC_DUMP): workgroup 0's first VBOC_VEC_DUMP_CALLS vector-pass outputs (the staged rows
+// XS[0..N][NX] and the stage-0 value), read back with vboc_debug_dump()
+__device__ double g_vdump[8][1024];
+__device__ unsigned g_vdump_calls;
 #ifdef VBOC_COOP_PROF
 #define CPROF_DECL unsigned long long cp0 = 0, cp1 = 0, cp2 = 0, cp3 = 0, cp4 = 0, cp5 = 0, cp6 = 0, cp7 = 0, cp8 = 0; \
   unsigned long long cp_t = __builtin_amdgcn_s_memtime();
@@ -1556,6 +1560,18 @@ struct Coop {
     }
     if (t < NX) s[L::PV + t] = pcur;
     __syncthreads();
+#ifdef VBOC_VEC_DUMP
+    if (blockIdx.x == 0) {
+      unsigned call = 0;
+      if (t == 0) call = atomicAdd(&g_vdump_calls, 1u);
+      call = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl((int)call, 0));
+      if (call < 8) {
+        for (int e = t; e < (N + 1) * NX && e < 1016; e += 64) g_vdump[call][e] = s[L::XS + e];
+        if (t < NX) g_vdump[call][1016 + t] = s[L::PV + t];
+      }
+      __syncthreads();
+    }
+#endif
     SPROF(1)
     // k_f = -Ru^-1 (g_u + B'v) per stage, lin = sum Y'k_f  (stage-parallel)
     double lin[NQ];

@@ -2098,6 +2098,16 @@ int vboc_debug_counters(unsigned long long* out16) {
   return VBOC_OK;
 }
 
+// measurement builds (-DVBOC_VEC_DUMP, coop.h): the dumped vector-pass outputs [8][1024] and the call count; both reset
+int vboc_debug_dump(double* out8k, unsigned* calls) {
+  if (!out8k || !calls) return fail(VBOC_ERR_ARG, "vboc_debug_dump: NULL argument");
+  HIPCHK(hipMemcpyFromSymbol(out8k, HIP_SYMBOL(g_vdump), 8 * 1024 * sizeof(double)));
+  HIPCHK(hipMemcpyFromSymbol(calls, HIP_SYMBOL(g_vdump_calls), sizeof(unsigned)));
+  const unsigned z = 0;
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_vdump_calls), &z, sizeof(z)));
+  return VBOC_OK;
+}
+
 int vboc_last_kernel_ms(vboc_handle h, double* ms, int* launches) {
   if (!h || !ms) return fail(VBOC_ERR_ARG, "vboc_last_kernel_ms: NULL argument");
   float f = 0.0f;
