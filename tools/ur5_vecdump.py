@@ -17,7 +17,7 @@ def main():
     from vboc_amd.ics import ur5_ics
     b = ur5_ics(np.arange(96))
     L = lib.load()
-    buf = (ctypes.c_double * (8 * 1024))()
+    buf = (ctypes.c_double * (8 * 1024 + 8 * 256))()
     calls = ctypes.c_uint()
     L.vboc_debug_dump(buf, ctypes.byref(calls))          # reset
     s = lib.Solver(4, int(np.max(b["N"])), slots=256)
@@ -25,8 +25,10 @@ def main():
     s.set_option("qp_solver_iter_max", 2)
     g = s.solve_host(b)
     L.vboc_debug_dump(buf, ctypes.byref(calls))
-    d = np.frombuffer(buf, dtype=np.float64).reshape(8, 1024).copy()
-    np.savez(sys.argv[1], dump=d, calls=calls.value, x=g["x"], u=g["u"], status=g["status"])
+    allb = np.frombuffer(buf, dtype=np.float64).copy()
+    d = allb[:8 * 1024].reshape(8, 1024)
+    d2 = allb[8 * 1024:].reshape(8, 256)
+    np.savez(sys.argv[1], dump=d, dump2=d2, calls=calls.value, x=g["x"], u=g["u"], status=g["status"])
     print(os.path.basename(os.environ.get("VBOC_LIB") or "libvboc_amd.so"), "calls", calls.value,
           "dump sums", [float(np.abs(d[i]).sum()) for i in range(min(calls.value, 8))], flush=True)
 

@@ -263,6 +263,7 @@ __device__ unsigned g_dbg_cnt;
 // XS[0..N][NX] and the stage-0 value), read back with vboc_debug_dump()
 __device__ double g_vdump[8][1024];
 __device__ unsigned g_vdump_calls;
+__device__ double g_vdump2[8][256];   // [0, W) the landed first slot, [W, 2W) the record's window read directly, pcur
 #ifdef VBOC_COOP_PROF
 #define CPROF_DECL unsigned long long cp0 = 0, cp1 = 0, cp2 = 0, cp3 = 0, cp4 = 0, cp5 = 0, cp6 = 0, cp7 = 0, cp8 = 0; \
   unsigned long long cp_t = __builtin_amdgcn_s_memtime();
@@ -1534,6 +1535,21 @@ struct Coop {
       UNR for (int d = 0; d < L::DV; ++d) vdma(d);
       vmwait<(L::DV - 1) * PV>();
       vld(vslot(0), acl, cc, pe);
+#ifdef VBOC_VEC_DUMP
+      if (blockIdx.x == 0) {
+        unsigned call = 0;
+        if (t == 0) call = __hip_atomic_load(&g_vdump_calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        call = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl((int)call, 0));
+        if (call < 8) {
+          const int k0 = N - 1 >= 1 ? N - 1 : 1;
+          for (int e = t; e < L::W_VEC; e += 64) {
+            g_vdump2[call][e] = s[vslot(0) + e];
+            g_vdump2[call][L::W_VEC + e] = st(k0, L::LO_VEC + e);
+          }
+          if (t < NX) g_vdump2[call][2 * L::W_VEC + t] = pcur;
+        }
+      }
+#endif
     }
     // p_{k+1} reaches every lane by readlane (lane q holds component q): the recursion's dependent chain
     // carries no LDS round trip

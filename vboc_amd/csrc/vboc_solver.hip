@@ -2098,11 +2098,13 @@ int vboc_debug_counters(unsigned long long* out16) {
   return VBOC_OK;
 }
 
-// measurement builds (-DVBOC_VEC_DUMP, coop.h): the dumped vector-pass outputs [8][1024] and the call count; both reset
+// measurement builds (-DVBOC_VEC_DUMP, coop.h): the dumped vector-pass outputs [8][1024], then [8][256] of the first
+// landed slot / its record window / pcur, and the call count (reset)
 int vboc_debug_dump(double* out8k, unsigned* calls) {
   if (!out8k || !calls) return fail(VBOC_ERR_ARG, "vboc_debug_dump: NULL argument");
   HIPCHK(hipMemcpyFromSymbol(out8k, HIP_SYMBOL(g_vdump), 8 * 1024 * sizeof(double)));
   HIPCHK(hipMemcpyFromSymbol(calls, HIP_SYMBOL(g_vdump_calls), sizeof(unsigned)));
+  HIPCHK(hipMemcpyFromSymbol(out8k + 8 * 1024, HIP_SYMBOL(g_vdump2), 8 * 256 * sizeof(double)));
   const unsigned z = 0;
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_vdump_calls), &z, sizeof(z)));
   return VBOC_OK;
