@@ -2229,6 +2229,20 @@ void k_wave(Work w, Opts o, Inputs in, SlotState ss, WaveJobs jb) {
   const int t = (int)threadIdx.x;
   Coop<NQ, FM, HC> C(smem, gptr(jb.regions) + (long long)blockIdx.x * jb.region_doubles, w, o, t);
   if constexpr (HC) C.gh = gptr(jb.hc) + (long long)blockIdx.x * jb.hc_doubles;
+#if defined(VBOC_LDS_ZERO) || defined(VBOC_LDS_NAN)
+  {   // measurement builds: fill the workgroup's LDS before the first job (uninitialised-LDS reads then show)
+    using LL = WaveLayout<NQ>;
+    const long long nm = jb.region_doubles / LL::REC - 1 - LL::SLACK;
+    const int n = LL::XS + (int)(nm + 1) * LL::NX;
+#ifdef VBOC_LDS_NAN
+    const double fill = __builtin_nan("");
+#else
+    const double fill = 0.0;
+#endif
+    for (int e = t; e < n; e += 64) smem[e] = fill;
+    __syncthreads();
+  }
+#endif
   for (;;) {
     unsigned idx = 0;
     if (t == 0) idx = atomicAdd(jb.next, 1u);
