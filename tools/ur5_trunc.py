@@ -23,6 +23,11 @@ def main():
     from vboc_amd import lib
     from vboc_amd.ics import ur5_ics
     out = sys.argv[1]
+    if "--pre" in sys.argv:     # run other kernels first (a triple first-solve batch): results that change with what
+        from vboc_amd.ics import data_generation_ics     # ran before point at a read of uninitialised registers
+        pre = lib.Solver(3, 120)
+        pre.solve_host(data_generation_ics(3, np.arange(4096)))
+        pre.close()
     b = ur5_ics(np.arange(96))
     save = {}
     for it, qp in CUTS:
