@@ -180,6 +180,7 @@ class GpuEngine:
         self.solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
         self.solver.set_option("dg_spec_early", getattr(args, "spec_early", 0))
         self.solver.set_option("dg_spec_first", getattr(args, "spec_first", 0))
+        self.solver.set_option("dg_spec_crit", getattr(args, "spec_crit", 0))
         if getattr(args, "wave_groups", 0):   # resident problems (default: sized to the 256 MiB MALL)
             self.solver.set_option("wave_groups", args.wave_groups)
         if getattr(args, "spec_min_ext", 0):   # measurement builds only (tools/spec_early_ab.sh, VBOC_LIB variant)
@@ -280,6 +281,8 @@ def parse(argv=None):
     ap.add_argument("--spec-first", type=int, default=0,
                     help="dg-loop: 1 = queued speculative restarts go before parked resumes once the new problems run "
                          "out (measured: mixed, off by default; DESIGN.md section 14)")
+    ap.add_argument("--spec-crit", type=int, default=0,
+                    help="dg-loop: 1 = the critical-path rule for speculative restarts (DESIGN.md section 14)")
     ap.add_argument("--spec-min-ext", type=int, default=0,
                     help="dg-loop: a failed horizon-extension chain publishes speculative restarts only from this solve on")
     ap.add_argument("--mode", choices=("wave", "lane"), default="wave",

@@ -188,8 +188,8 @@ def test_device_loop_restart_branches_match_host_driver(nq):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("opts", [{}, {"dg_spec_window": 2}, {"dg_spec_first": 1}, {"dg_park": 0}],
-                         ids=["default", "window2", "spec_first", "no_park"])
+@pytest.mark.parametrize("opts", [{}, {"dg_spec_window": 2}, {"dg_spec_first": 1}, {"dg_spec_crit": 1},
+                                  {"dg_park": 0}], ids=["default", "window2", "spec_first", "spec_crit", "no_park"])
 def test_speculative_restarts_change_nothing(opts):
     """Speculative restarts (dg_speculate) only run later attempts early: with and without them the
     device loop returns the same rows, counts and per-problem statistics (timing and speculation fields aside),

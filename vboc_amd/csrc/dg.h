@@ -80,6 +80,9 @@ struct DgJobs {
   // the eager window (see "Speculative restarts"): the next spec_window attempts of a chain also go to this queue,
   // which every wave serves before new or parked problems; 0 switches it off
   int spec_window;
+  int spec_crit;                  // 1: critical-path rule (a chain's remaining attempts go eager when they would end
+                                  //    after the job queues drain at the launch's rate so far)
+  unsigned long long* t_launch;   // the launch's first job start (device real-time clock), set by the first wave
   int* spec_eq;                   // [spec_events * DG_SPEC_JOBS] like spec_q
   unsigned* spec_eq_tail;
   unsigned* spec_eq_head;
@@ -111,9 +114,9 @@ enum : int { DG_SOLVES = 0, DG_RK4, DG_SQP, DG_NSQP, DG_NQP, DG_T0, DG_T1, DG_ST
 template <int NQ>
 struct DgState {
   int phase, N, ext, joint_sel, vel_sel, f, at_limit, N_test, ver, nrows, rng_pos, solves, rk4s, fail, spec_ev,
-      spec_base, resumed, taken;
+      spec_base, resumed, taken, crit;
   double cost, q_init_sel, q_fin_sel, q_init_oth, norm_old, norm_bef, norm_new;
-  double sqp, nsqp, nqp, t0, st1, it1, tq, wait, lag, tspec;
+  double sqp, nsqp, nqp, t0, st1, it1, tq, wait, lag, tspec, treq;
   double ran[2], store_ic[4], xsym[2 * NQ];
 };
 
@@ -298,6 +301,41 @@ struct Dg {
     }
     ((int*)in.N)[wg] = N;
     s->solves += 1;
+    s->treq = (double)__builtin_amdgcn_s_memrealtime();
+  }
+
+  // the critical-path rule: at a failed attempt of a chain, the rest of the chain run serially would take
+  // (10 - ext) x the attempt's duration; the job queues will drain in about (jobs left) x (elapsed / jobs taken).  If
+  // the chain would end after that, its remaining attempts go to the eager queue, once (waves take them before new or
+  // parked problems) - the chains that would set the launch's end get help, the ones with time to spare run alone.
+  __device__ __forceinline__ void crit_check(int ev) {
+    if (!J.spec_crit || J.spec_window > 0 || s->crit || ev < 0) return;   // (the window's pushes are enough)
+    const double now = (double)__builtin_amdgcn_s_memrealtime();
+    const double dur = now - s->treq;
+    int push = 0;
+    if (t == 0) {
+      const unsigned nx = __hip_atomic_load(J.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned taken_new = nx < (unsigned)J.count ? nx : (unsigned)J.count;
+      unsigned parked_wait = 0, resumed = 0;
+      if (J.park_res) {
+        UNR for (int q = 0; q < 2; ++q) {
+          const unsigned tl = __hip_atomic_load(&J.park_tail[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned hd = __hip_atomic_load(&J.park_head[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          parked_wait += tl - hd;
+          resumed += hd;
+        }
+      }
+      const double left = (double)(J.count - taken_new) + (double)parked_wait;
+      const double taken = (double)taken_new + (double)resumed;
+      const double t0 = (double)__hip_atomic_load(J.t_launch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const double queue = taken > 0.0 ? left * (now - t0) / taken : 0.0;
+      push = (10 - s->ext) * dur > queue ? 1 : 0;
+    }
+    push = __builtin_amdgcn_readfirstlane(__shfl(push, 0));
+    if (!push) return;
+    s->crit = 1;
+    const int nj = 10 - s->spec_base;
+    for (int j = (s->ext + 1) - s->spec_base + 1; j <= nj; ++j) push_eager(ev, j);
   }
 
   __device__ __forceinline__ void append(const double* x) {
@@ -318,7 +356,7 @@ struct Dg {
     s->tq = s->t0;
     const double q_min = J.q_min, q_max = J.q_max, v_max = J.v_max, v_min = -J.v_max, eps = J.eps;
     s->phase = HEXT; s->N = J.N_start; s->ext = 0; s->f = 0; s->at_limit = 0; s->N_test = 0; s->ver = 0;
-    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0; s->taken = 0; s->wait = 0.0; s->lag = 0.0;
+    s->nrows = 0; s->rng_pos = 0; s->solves = 0; s->rk4s = 0; s->fail = 0; s->spec_ev = -1; s->spec_base = 0; s->taken = 0; s->wait = 0.0; s->lag = 0.0; s->crit = 0;
     s->resumed = 0;
     s->sqp = 0.0; s->nsqp = 0.0; s->nqp = 0.0; s->cost = 1e6;
     int di = 0;
@@ -676,6 +714,7 @@ struct Dg {
 #endif
           spawn(att, N);
         }
+        crit_check(s->spec_ev);
       }
       straight_guess(N, qlb0());
     }
@@ -1010,12 +1049,17 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
   const int count = J->count;
   const bool spec = J->spec_events > 0;
   const bool park = J->park_res != nullptr;
+  if (spec && J->spec_crit && t == 0) {
+    unsigned long long z = 0;
+    __hip_atomic_compare_exchange_strong(J->t_launch, &z, (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                                         __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   for (;;) {
     int mode = 0, idx = 0, ev = 0, jj = 0, code = 0;
     // 0. the eager window: a queued attempt of a running chain that its owner reaches within spec_window attempts
     //    goes before every problem (the failing chains are the launch's critical paths; the window bounds the
     //    solves a chain that succeeds early wastes)
-    if (spec && J->spec_window > 0) {
+    if (spec && (J->spec_window > 0 || J->spec_crit)) {
       int got = -1;
       if (t == 0) {
         const unsigned h = __hip_atomic_load(J->spec_eq_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -1513,6 +1513,7 @@ struct vboc_solver {
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
   int dg_spec_early = 0;            // restart jobs before new problems once this few problems are left (0: only after)
   bool dg_spec_first = false;       // restart jobs before parked resumes once the new problems run out (dg.h)
+  bool dg_spec_crit = false;        // critical-path rule for the eager restart queue (dg.h crit_check)
   int dg_spec_window = 0;           // eager window: a chain's next attempts that go before every problem (dg.h; off: measured slower)
   int dg_spec_min_ext = 0;          // (-DVBOC_SPEC_MIN_EXT builds) restart jobs only from this extension solve on
   double* wave_hc = nullptr;        // path-constraint rows of the wave solver, one region per workgroup
@@ -1885,6 +1886,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "dg_speculate") h->dg_speculate = v != 0.0;
   else if (s == "dg_spec_early") h->dg_spec_early = v > 0.0 ? (int)v : 0;
   else if (s == "dg_spec_first") h->dg_spec_first = v != 0.0;
+  else if (s == "dg_spec_crit") h->dg_spec_crit = v != 0.0;
   else if (s == "dg_spec_window") h->dg_spec_window = v > 0.0 ? (v < 9.0 ? (int)v : 9) : 0;
   else if (s == "dg_park") h->dg_park = v != 0.0;
   else if (s == "dg_park_window") h->dg_park_window = v > 0.0 ? (int)v : 0;
@@ -1929,6 +1931,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "dg_speculate") *v = h->dg_speculate ? 1.0 : 0.0;
   else if (s == "dg_spec_early") *v = (double)h->dg_spec_early;
   else if (s == "dg_spec_first") *v = h->dg_spec_first ? 1.0 : 0.0;
+  else if (s == "dg_spec_crit") *v = h->dg_spec_crit ? 1.0 : 0.0;
   else if (s == "dg_spec_window") *v = (double)h->dg_spec_window;
   else if (s == "dg_park") *v = h->dg_park ? 1.0 : 0.0;
   else if (s == "dg_park_window") *v = (double)h->dg_park_window;
@@ -2433,7 +2436,8 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   J.done_flag = done_flag; J.cancel = cancel;
   // counters: [0] job queue, [1] finished problems, [2..3] error flags, [4..5] rows used (u64),
   // [6] speculation events, [7] / [8] restart-job queue tail / head, [10..13] speculative solves run / used (u64),
-  // [16..17] / [18..19] parked-job queue tails / heads, [20] / [21] eager restart-job queue tail / head
+  // [16..17] / [18..19] parked-job queue tails / heads, [20] / [21] eager restart-job queue tail / head,
+  // [22..23] the launch's first job start (u64, the critical-path rule)
   J.next = h->head; J.done = h->head + 1; J.err = h->head + 2; J.rows_next = (unsigned long long*)(h->head + 4);
   J.spec_ev_next = h->head + 6; J.spec_q_tail = h->head + 7; J.spec_q_head = h->head + 8;
   J.spec_count = (unsigned long long*)(h->head + 10);
@@ -2444,6 +2448,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
 #endif
   J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = J.spec_eq = nullptr;
   J.spec_window = 0; J.spec_eq_tail = h->head + 20; J.spec_eq_head = h->head + 21;
+  J.spec_crit = 0; J.t_launch = (unsigned long long*)(h->head + 22);   // [22..23]
   size_t spec_ctl = 0;
   if (h->dg_speculate && !testing) {
     const int E = b->B < 8192 ? b->B : 8192;
@@ -2466,6 +2471,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
     J.spec_q = ci; ci += (size_t)E * DG_SPEC_JOBS;
     J.spec_eq = ci;
     J.spec_window = h->dg_spec_window;
+    J.spec_crit = h->dg_spec_crit ? 1 : 0;
     J.spec = (double*)((char*)h->dg_spec + ((spec_ctl + 255) & ~(size_t)255));
     J.spec_events = E; J.spec_stride = (int)stride;
     HIPCHK(hipMemsetAsync(h->dg_spec, 0, spec_ctl, st));
