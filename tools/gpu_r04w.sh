@@ -10,3 +10,4 @@ timeout -k 10 300 python3 $R/tools/dg_probe.py --B 60000 --spec-crit 0 1 --save 
 timeout -k 10 300 python3 $R/tools/dg_probe.py --B 100000 --spec-crit 0 1 --save $O/s100k > $O/probe_100k.jsonl 2> $O/probe_100k.err; rc=$?; echo "100k exit $rc"; cat $O/probe_100k.jsonl | cut -c1-400; [ $rc -eq 0 ] || exit $rc
 cd $R
 timeout -k 10 420 python3 bench.py --steps 20 --warmup 5 --no-cpu --progress 30 --spec-crit 1 > $O/bench_crit.json 2> $O/bench_crit.err; rc=$?; echo "bench crit exit $rc"
+timeout -k 10 420 python3 bench.py --steps 20 --warmup 5 --no-cpu --progress 30 > $O/bench_default.json 2> $O/bench_default.err; echo "bench default exit $?"
