@@ -278,3 +278,50 @@ def mpc_solve_batch(spec, x0, x_guess, u_guess, params=None, mean=0.0, std=1.0, 
         raise RuntimeError(f"oracle mpc_solve_batch failed rc={rc}")
     del keep
     return x_out, u_out, res, hrow
+
+
+def _mpc_nn(params, mean, std, lh=0.0, uh=1e6):
+    keep = [np.ascontiguousarray(p, dtype=np.float64) for p in params]
+    return MpcNN(hid=keep[0].shape[0], mean=float(mean), std=float(std), lh=float(lh), uh=float(uh),
+                 **{n: p.ctypes.data for n, p in zip(("W0", "b0", "W1", "b1", "W2", "b2"), keep)}), keep
+
+
+def mpc_soft_solve_batch(spec, x0, x_guess, u_guess, params, mean, std, margin, Zl, zl=None, W=None, We=None,
+                         rti=True, opts=None, nthreads=None, lh=0.0, uh=1e6):
+    """OCPtriplependulumSoftTraj's OCP_solve (vboc_oracle_ft.c vboc_oracle_mpc_soft_solve_batch): the row
+    NN(x) (100 - margin) / 100 - vn(x) on every stage, soft lower sides with the per-problem per-stage weights Zl / zl
+    [B, N+1]; W [B, 9] / We [B, 6] per-problem stage weights (default: the spec's).  Returns (x, u, results, h(x_N))."""
+    x0, xg, ug = (np.ascontiguousarray(a, dtype=np.float64) for a in (x0, x_guess, u_guess))
+    B, N = x0.shape[0], spec.N
+    assert xg.shape == (B, N + 1, 6) and ug.shape == (B, N, 3)
+    Zl = np.ascontiguousarray(np.broadcast_to(np.asarray(Zl, dtype=np.float64), (B, N + 1)))
+    zl = np.zeros((B, N + 1)) if zl is None else np.ascontiguousarray(np.broadcast_to(np.asarray(zl, float), (B, N + 1)))
+    W = np.ascontiguousarray(np.broadcast_to(np.asarray(spec.W if W is None else W, float), (B, 9)))
+    We = np.ascontiguousarray(np.broadcast_to(np.asarray(spec.W_e if We is None else We, float), (B, 6)))
+    x_out, u_out = np.zeros_like(xg), np.zeros_like(ug)
+    res = np.zeros(B, dtype=RESULT_DTYPE)
+    hrow = np.zeros(B)
+    if opts is None:
+        opts = default_opts(lm=spec.lm, tol_stat=1e-6, qp_tol_stat=1e-8)
+    vec = [np.ascontiguousarray(a, dtype=np.float64) for a in (spec.xmin, spec.xmax, spec.umin, spec.umax, spec.xmin,
+                                                               spec.xmax)]
+    nnp, keep = _mpc_nn(params, mean, std, lh, uh)
+    rc = lib().vboc_oracle_mpc_soft_solve_batch(
+        3, B, N, ctypes.c_double(spec.time_step), _p(x0), _p(xg), _p(ug), *[_p(a) for a in vec], _p(W), _p(We),
+        _p(np.ascontiguousarray(spec.yref, dtype=np.float64)), _p(np.ascontiguousarray(spec.yref_e, dtype=np.float64)),
+        ctypes.c_double(spec.cost_scale), ctypes.byref(nnp), ctypes.c_double(float(margin)), _p(zl), _p(Zl),
+        int(bool(rti)), ctypes.byref(opts), int(nthreads or os.cpu_count()), _p(x_out), _p(u_out), _p(res), _p(hrow))
+    if rc != 0:
+        raise RuntimeError(f"oracle mpc_soft_solve_batch failed rc={rc}")
+    del keep
+    return x_out, u_out, res, hrow
+
+
+def mpc_row(x, params, mean, std, margin=-1.0):
+    """The Safe-MPC row at states x [B, 6] (vboc_oracle_mpc_row): margin >= 0 the SoftTraj (conservative) row."""
+    x = np.ascontiguousarray(np.atleast_2d(x), dtype=np.float64)
+    out = np.zeros(x.shape[0])
+    nnp, keep = _mpc_nn(params, mean, std)
+    lib().vboc_oracle_mpc_row(3, x.shape[0], _p(x), ctypes.byref(nnp), ctypes.c_double(float(margin)), _p(out))
+    del keep
+    return out

@@ -73,6 +73,26 @@ int vboc_oracle_mpc_solve_batch(int nq, int B, int N, double h, const double* x0
                                 const double* We, const double* yref, const double* yref_e, double cs,
                                 const vboc_mpc_nn_t* nn, int rti, const vboc_opts_t* opts, int nthreads,
                                 double* x_out, double* u_out, vboc_result_t* res, double* hrow);
+/* OCPtriplependulumSoftTraj (vboc_oracle_ft.c header): the row scaled by (100 - margin) / 100 on every stage 0..N,
+   soft lower sides with per-stage slack weights zl / Zl [N + 1] (zu = Zu = 0) */
+typedef struct {
+  double margin;
+  const double *zl, *Zl;
+} vboc_mpc_soft_t;
+int vboc_oracle_mpc_solve_soft(int nq, int N, double h, const double* x0, const double* x_guess,
+                               const double* u_guess, const double* xlb, const double* xub, const double* ulb,
+                               const double* uub, const double* xNlb, const double* xNub, const double* W,
+                               const double* We, const double* yref, const double* yref_e, double cs,
+                               const vboc_mpc_nn_t* nn, const vboc_mpc_soft_t* soft, int rti, const vboc_opts_t* opts,
+                               double* x_out, double* u_out, vboc_result_t* res, double* hrow);
+int vboc_oracle_mpc_soft_solve_batch(int nq, int B, int N, double h, const double* x0, const double* x_guess,
+                                     const double* u_guess, const double* xlb, const double* xub, const double* ulb,
+                                     const double* uub, const double* xNlb, const double* xNub, const double* W,
+                                     const double* We, const double* yref, const double* yref_e, double cs,
+                                     const vboc_mpc_nn_t* nn, double margin, const double* zl, const double* Zl,
+                                     int rti, const vboc_opts_t* opts, int nthreads, double* x_out, double* u_out,
+                                     vboc_result_t* res, double* hrow);
+void vboc_oracle_mpc_row(int nq, int B, const double* x, const vboc_mpc_nn_t* nn, double margin, double* out);
 /* HJR one-step OCP (vboc_oracle_hjr.c): x0 fixed, N = 1, terminal cost = logit 0 of NeuralNetCLS */
 void vboc_oracle_hjr_default_opts(int nq, vboc_opts_t* o);
 int vboc_oracle_hjr_solve_batch(int nq, int B, const double* x0, int h, const double* W0, const double* b0,

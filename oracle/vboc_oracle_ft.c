@@ -36,6 +36,18 @@
  *    infeasible start, sigma c c' in the terminal Riccati block); no constraint Hessian (Gauss-Newton);
  *  - SQP_RTI (the Safe-MPC driver's option, hard_terminal_constraints/3dof_sym.py:96): one linearisation, one QP,
  *    the full step; status 0, or 4 if the QP fails.
+ * and `OCPtriplependulumSoftTraj` (triplependulum_class_vboc.py:242-304; vboc_mpc_soft_t): the row scaled by the
+ * safety margin, h(x) = NN(z(x)) (100 - m) / 100 - vn(x), on EVERY stage 0..N (con_h_expr and con_h_expr_e), each row
+ * soft on its lower side (idxsh / idxsh_e) with a slack s_k >= 0 costing zl_k s_k + Zl_k s_k^2 / 2 (the drivers'
+ * cost_set(k, "Zl", ...) per stage, soft_traj_constraints/3dof_sym.py:102-105, receiding_hard_constraints/
+ * 3dof_sym.py:41-46); the upper side (uh = 1e6, zu = Zu = 0) is kept hard - it is never active.  In the QP the slack
+ * is a variable of its own (absolute value, so an RTI QP does not depend on the previous slack iterate) with a
+ * barrier on s >= 0; it is eliminated per stage in the Riccati recursion:
+ *     W = Zl + Sl + Ss (Sl = ql / tl, Ss = qs / s),   sigma = Su + Sl (Zl + Ss) / W   (the row's c c' weight),
+ *     gamma += Sl b / W with b = -(Zl s + zl - ql - qs) + rcl / tl + rcs / s - Sl rl  (the row's gradient term),
+ *     ds = (b - Sl c'd) / W,  dtl = c'd + ds + rl,  dqs = (rcs - qs ds) / s.
+ * In SQP mode the slacks are NLP variables (updated with the step, their cost and the soft rows' violation in the
+ * merit); the drivers run SQP_RTI.
  */
 #include <math.h>
 #include <stdlib.h>
@@ -55,6 +67,13 @@ typedef struct {
   double Lb[FZ], Ub[FZ], dz[FZ], ql[FZ], qu[FZ], e0[FX];
   double H[FZ], g[FZ], d[FZ], daff[FZ];
   double K[FU * FX], kf[FU], Lr[FZ * FZ], M[FZ * FX], Y[FZ * FX], Pe[FX], qpi[FX];
+  /* the Safe-MPC NN row of this stage (HardTerm: stage N only; SoftTraj: every stage): value, gradient, QP slacks /
+     duals of both sides, their affine directions, residual starts, the NLP multipliers; the soft lower side's slack
+     (QP value hs, dual hqs, affine directions), its NLP iterate sl / multiplier lsl and weights zl, Zl; hsig the
+     row's c c' weight in the factorisation */
+  double hv, hg[FX], hL, hU, htl, htu, hql, hqu, hr0l, hr0u, hatl, hatu, haql, haqu, hll, hlu;
+  double hs, hqs, has, haqs, sl, lsl, zl, Zl, hsig, hb, hW;
+  double hdtl, hdtu, hdql, hdqu, hds, hdqs;   /* the combined (corrector) directions of the iteration */
 } fstage_t;
 
 typedef struct {
@@ -73,13 +92,17 @@ typedef struct {
   int track, rti;
   double wq[FZ], yr[FZ], we[FX], yre[FX], cs;
   const vboc_mpc_nn_t* nn;
-  double hv, hg[FX], hL, hU, htl, htu, hql, hqu, hr0l, hr0u, hatl, hatu, haql, haqu, hll, hlu;
+  int soft;        /* SoftTraj: rows on every stage, soft lower sides, the row scaled by sm / 100 */
+  double sm;       /* 100 - safety_margin */
 } fprob_t;
+
+/* stage k carries the NN row */
+static int frow(const fprob_t* P, int k) { return P->nn && (P->soft || k == P->N); }
 
 /* ------------------------------------------------------------------------------------------ */
 /* the Safe-MPC terminal row h(x) = NN(z(x)) - vn(x) (nn_decisionfunction, :208-230) and grad    */
 /* ------------------------------------------------------------------------------------------ */
-static double nn_row(const vboc_mpc_nn_t* n, int nq, const double* x, double* grad) {
+static double nn_row(const vboc_mpc_nn_t* n, int nq, const double* x, double* grad, int soft, double sm) {
   const int nx = 2 * nq, H = n->hid;
   double ss = 0.0;
   for (int j = 2; j < nx; ++j) ss += x[j] * x[j];   /* norm_2(x[2:]) - theta_3 included, as the reference */
@@ -104,6 +127,7 @@ static double nn_row(const vboc_mpc_nn_t* n, int nq, const double* x, double* gr
     if (t > 0.0) out += n->W2[i] * t;
   }
   out += n->b2[0];
+  if (soft) out = out * sm / 100.0;   /* nn_decisionfunction_conservative: out*(100-safety_margin)/100 (:301) */
   if (grad) {
     /* d out / d z by reverse mode through the two ReLUs (derivative 0 at a kink) */
     double* g1 = (double*)calloc((size_t)H, sizeof(double));
@@ -118,6 +142,7 @@ static double nn_row(const vboc_mpc_nn_t* n, int nq, const double* x, double* gr
       for (int j = 0; j < nx; ++j) gz[j] += g1[i] * n->W0[i * nx + j];
     }
     free(g1);
+    if (soft) for (int j = 0; j < nx; ++j) gz[j] = gz[j] * sm / 100.0;
     /* chain rule through z(x) and vn(x) = max(|x[2:]|, 1e-3) */
     double dvn[2 * FQ] = {0};
     if (nrm > 1e-3) for (int j = 2; j < nx; ++j) dvn[j] = x[j] / nrm;
@@ -266,6 +291,8 @@ static double fcost(const fprob_t* P) {
   double c = 0.0;
   if (P->track) {
     for (int k = 0; k <= P->N; ++k) c += ftrack(P, k, P->st[k].x, k < P->N ? P->st[k].u : NULL);
+    if (P->soft)   /* the slacks' penalties (ACADOS' get_cost includes them) */
+      for (int k = 0; k <= P->N; ++k) c += P->st[k].zl * P->st[k].sl + 0.5 * P->st[k].Zl * P->st[k].sl * P->st[k].sl;
     return c;
   }
   for (int i = 0; i < P->nx; ++i) c += P->c0[i] * P->st[0].x[i];
@@ -291,9 +318,11 @@ static void flinearize(fprob_t* P) {
     for (int j = 0; j < P->nf0; ++j) s0->F0[i * m0 + j] = s0->A[i * nx + P->f0[j]];
     for (int a = 0; a < nu; ++a) s0->F0[i * m0 + P->nf0 + a] = s0->B[i * nu + a];
   }
-  if (P->nn) {   /* terminal row: value and gradient (the pinned dt column has none) */
-    memset(P->hg, 0, sizeof(P->hg));
-    P->hv = nn_row(P->nn, P->nq, P->st[P->N].x, P->hg);
+  for (int k = 0; k <= P->N; ++k) {   /* the rows: value and gradient (the pinned dt column has none) */
+    if (!frow(P, k)) continue;
+    fstage_t* s = &P->st[k];
+    memset(s->hg, 0, sizeof(s->hg));
+    s->hv = nn_row(P->nn, P->nq, s->x, s->hg, P->soft, P->sm);
   }
 }
 
@@ -321,7 +350,10 @@ static void fresiduals(const fprob_t* P, double* rstat, double* req, double* rin
       } else {
         gr -= P->st[N - 1].pi[i];
         for (int j = 0; j < P->ne; ++j) if (P->ei[j] == i) gr += P->tnu[j];
-        if (P->nn) gr += P->hg[i] * (P->hlu - P->hll);
+      }
+      if (frow(P, k)) {   /* the row's term on the state components of the stage's variables */
+        const int xi = k == 0 ? (i < P->nf0 ? P->f0[i] : -1) : (i < nx ? i : -1);
+        if (xi >= 0) gr += s->hg[xi] * (s->hlu - s->hll);
       }
       st = fmax(st, fabs(gr));
       if (boxed) {
@@ -330,9 +362,17 @@ static void fresiduals(const fprob_t* P, double* rstat, double* req, double* rin
       }
     }
   }
-  if (P->nn) {
-    in = fmax(in, fmax(P->nn->lh - P->hv, P->hv - P->nn->uh));
-    cp = fmax(cp, fmax(fabs(P->hll * (P->hv - P->nn->lh)), fabs(P->hlu * (P->nn->uh - P->hv))));
+  for (int k = 0; k <= N; ++k) {
+    if (!frow(P, k)) continue;
+    const fstage_t* s = &P->st[k];
+    const double sl = P->soft ? s->sl : 0.0;
+    in = fmax(in, fmax(P->nn->lh - (s->hv + sl), s->hv - P->nn->uh));
+    cp = fmax(cp, fmax(fabs(s->hll * (s->hv + sl - P->nn->lh)), fabs(s->hlu * (P->nn->uh - s->hv))));
+    if (P->soft) {   /* the slack: s >= 0, its stationarity Zl s + zl - lambda_row - lambda_s = 0 */
+      in = fmax(in, -sl);
+      cp = fmax(cp, fabs(s->lsl * sl));
+      st = fmax(st, fabs(s->Zl * sl + s->zl - s->hll - s->lsl));
+    }
   }
   *rstat = st; *req = eq; *rineq = in; *rcomp = cp;
 }
@@ -378,10 +418,10 @@ static int fnewton(fprob_t* P, int factor, double* nu_new) {
   fstage_t* sN = &P->st[N];
   memset(Pm, 0, sizeof(Pm));
   for (int i = 0; i < nx; ++i) { Pm[i * nx + i] = sN->H[i]; p[i] = sN->g[i]; }
-  if (P->nn) {   /* the terminal row's barrier: sigma c c' */
-    const double sig = P->hql / P->htl + P->hqu / P->htu;
+  if (frow(P, N)) {   /* the terminal row's barrier: sigma c c' */
+    const double sig = sN->hsig;
     for (int i = 0; i < nx; ++i)
-      for (int j = 0; j < nx; ++j) Pm[i * nx + j] += sig * P->hg[i] * P->hg[j];
+      for (int j = 0; j < nx; ++j) Pm[i * nx + j] += sig * sN->hg[i] * sN->hg[j];
   }
   memset(Pi, 0, sizeof(Pi));
   for (int j = 0; j < ne; ++j) Pi[P->ei[j] * ne + j] = 1.0;
@@ -455,9 +495,11 @@ static int fnewton(fprob_t* P, int factor, double* nu_new) {
             double t = 0; for (int q = 0; q < nx; ++q) t += s->A[q * nx + i] * Pm[q * nx + j];
             AP[i * nx + j] = t;
           }
+        const int rk = frow(P, k);
         for (int i = 0; i < nx; ++i)
           for (int j = 0; j < nx; ++j) {
             double t = (i == j) ? s->H[i] : 0.0;
+            if (rk) t += s->hsig * s->hg[i] * s->hg[j];   /* a path row's barrier: sigma c c' */
             for (int q = 0; q < nx; ++q) t += AP[i * nx + q] * s->A[q * nx + j];
             for (int a = 0; a < nu; ++a) t += Sux[a * nx + i] * s->K[a * nx + j];
             Pn[i * nx + j] = t;
@@ -564,21 +606,67 @@ static void fr_add(fratio_t* m, double t, double dt) {
   if (dt < 0.0 && t * m->d < m->n * (-dt)) { m->n = t; m->d = -dt; }
 }
 
-/* the terminal row's c'd over the stage-N step d */
-static double frow_dot(const fprob_t* P, const double* d) {
+/* the row's c'd over stage k's step d (its state components; stage 0: the free ones) */
+static double frow_dot(const fprob_t* P, int k, const double* d) {
+  const fstage_t* s = &P->st[k];
   double t = 0.0;
-  for (int i = 0; i < P->nx; ++i) t += P->hg[i] * d[i];
+  if (k == 0) {
+    for (int j = 0; j < P->nf0; ++j) t += s->hg[P->f0[j]] * d[j];
+    return t;
+  }
+  for (int i = 0; i < P->nx; ++i) t += s->hg[i] * d[i];
   return t;
 }
-/* Newton directions of the terminal row's slacks / duals (vboc_oracle.c hc_dir; smu = 0 and zero affine
-   directions give the predictor's) */
-static void frow_dir(const fprob_t* P, double smu, double* dtl, double* dtu, double* dql, double* dqu) {
-  const double cd = frow_dot(P, P->st[P->N].d), rl = P->rs * P->hr0l, ru = P->rs * P->hr0u;
-  const double rcl = smu - P->htl * P->hql - P->hatl * P->haql, rcu = smu - P->htu * P->hqu - P->hatu * P->haqu;
-  *dtl = cd + rl;
+/* the row's term c * v on the gradient of stage k's variables */
+static void frow_addgrad(const fprob_t* P, int k, double* g, double v) {
+  const fstage_t* s = &P->st[k];
+  if (k == 0) {
+    for (int j = 0; j < P->nf0; ++j) g[j] += s->hg[P->f0[j]] * v;
+    return;
+  }
+  for (int i = 0; i < P->nx; ++i) g[i] += s->hg[i] * v;
+}
+/* complementarity targets of the row's pairs: the predictor's (smu = 0, zero affine directions) or Mehrotra's */
+static void frow_rc(const fstage_t* s, double smu, double* rcl, double* rcu, double* rcs) {
+  *rcl = smu - s->htl * s->hql - s->hatl * s->haql;
+  *rcu = smu - s->htu * s->hqu - s->hatu * s->haqu;
+  *rcs = smu - s->hs * s->hqs - s->has * s->haqs;
+}
+/* the row's gradient term gamma for the targets rc (pred: the predictor's form), and (pred) its factorisation
+   weight sigma; a soft row also keeps its slack elimination b, W (header) */
+static double frow_gamma(const fprob_t* P, fstage_t* s, double rs, double rcl, double rcu, double rcs, int pred) {
+  const double rl = rs * s->hr0l, ru = rs * s->hr0u;
+  double gam;
+  if (pred) gam = s->hql * rl / s->htl - s->hqu * ru / s->htu;
+  else gam = -s->hql + s->hqu - (rcl - s->hql * rl) / s->htl + (rcu - s->hqu * ru) / s->htu;
+  if (P->soft) {
+    const double Sl = s->hql / s->htl, Ss = s->hqs / s->hs, W = s->Zl + Sl + Ss;
+    const double b = -(s->Zl * s->hs + s->zl - s->hql - s->hqs) + rcl / s->htl + rcs / s->hs - Sl * rl;
+    s->hW = W;
+    s->hb = b;
+    gam += Sl * b / W;
+    if (pred) s->hsig = s->hqu / s->htu + Sl * (s->Zl + Ss) / W;
+  } else if (pred) {
+    s->hsig = s->hql / s->htl + s->hqu / s->htu;
+  }
+  return gam;
+}
+/* Newton directions of the row's slacks / duals (and a soft row's slack / dual) from cd = c'd */
+static void frow_dirs(const fprob_t* P, const fstage_t* s, double cd, double rs, double rcl, double rcu, double rcs,
+                      double* dtl, double* dtu, double* dql, double* dqu, double* ds, double* dqs) {
+  const double rl = rs * s->hr0l, ru = rs * s->hr0u;
+  *ds = 0.0;
+  *dqs = 0.0;
+  if (P->soft) {
+    *ds = (s->hb - s->hql / s->htl * cd) / s->hW;
+    *dtl = cd + *ds + rl;
+  } else {
+    *dtl = cd + rl;
+  }
   *dtu = ru - cd;
-  *dql = (rcl - P->hql * *dtl) / P->htl;
-  *dqu = (rcu - P->hqu * *dtu) / P->htu;
+  *dql = (rcl - s->hql * *dtl) / s->htl;
+  *dqu = (rcu - s->hqu * *dtu) / s->htu;
+  if (P->soft) *dqs = (rcs - s->hqs * *ds) / s->hs;
 }
 
 static int fqp(fprob_t* P, int* iters) {
@@ -603,17 +691,29 @@ static int fqp(fprob_t* P, int* iters) {
     }
   }
   for (int j = 0; j < ne; ++j) P->qnu[j] = 0.0;
-  if (P->nn) {   /* terminal row: slacks from the initial c'dz_N, clipped to ipm_push (infeasible start) */
-    const double gd = frow_dot(P, P->st[N].dz);
-    P->hL = P->nn->lh - P->hv;
-    P->hU = P->nn->uh - P->hv;
-    P->htl = fmax(gd - P->hL, o->ipm_push);
-    P->htu = fmax(P->hU - gd, o->ipm_push);
-    P->hql = o->mu0 / P->htl;
-    P->hqu = o->mu0 / P->htu;
-    P->hr0l = gd - P->hL - P->htl;
-    P->hr0u = P->hU - gd - P->htu;
-    P->hatl = P->hatu = P->haql = P->haqu = 0.0;
+  for (int k = 0; k <= N; ++k) {
+    /* the rows: slacks from the initial c'dz, clipped to ipm_push (infeasible start); a soft row's slack starts at
+       the row's violation + ipm_push, so its lower side starts feasible */
+    if (!frow(P, k)) continue;
+    fstage_t* s = &P->st[k];
+    const double gd = frow_dot(P, k, s->dz);
+    s->hL = P->nn->lh - s->hv;
+    s->hU = P->nn->uh - s->hv;
+    double gs = gd;
+    s->hs = s->hqs = s->has = s->haqs = 0.0;
+    if (P->soft) {
+      s->hs = fmax(s->hL - gd, 0.0) + o->ipm_push;
+      s->hqs = o->mu0 / s->hs;
+      gs = gd + s->hs;
+      nbox += 1;
+    }
+    s->htl = fmax(gs - s->hL, o->ipm_push);
+    s->htu = fmax(s->hU - gd, o->ipm_push);
+    s->hql = o->mu0 / s->htl;
+    s->hqu = o->mu0 / s->htu;
+    s->hr0l = gs - s->hL - s->htl;
+    s->hr0u = s->hU - gd - s->htu;
+    s->hatl = s->hatu = s->haql = s->haqu = 0.0;
     nbox += 2;
   }
   double e00 = 0.0, rd0 = 0.0;
@@ -636,12 +736,17 @@ static int fqp(fprob_t* P, int* iters) {
     P->st[N].e0[j] = t;
     e00 = fmax(e00, fabs(t));
   }
-  if (P->nn) e00 = fmax(e00, fmax(fabs(P->hr0l), fabs(P->hr0u)));
+  for (int k = 0; k <= N; ++k)
+    if (frow(P, k)) e00 = fmax(e00, fmax(fabs(P->st[k].hr0l), fabs(P->st[k].hr0u)));
   for (int k = 0; k <= N; ++k) {
     const fstage_t* s = &P->st[k];
-    for (int i = 0; i < fnz(P, k); ++i)
+    const int rk = frow(P, k);
+    for (int i = 0; i < fnz(P, k); ++i) {
+      const int xi = k == 0 ? (i < P->nf0 ? P->f0[i] : -1) : (i < nx ? i : -1);
       rd0 = fmax(rd0, fabs((rho + fhq(P, k, i)) * s->dz[i] + fgrad(P, k, i) - s->ql[i] + s->qu[i] +
-                           ((P->nn && k == N) ? P->hg[i] * (P->hqu - P->hql) : 0.0)));
+                           ((rk && xi >= 0) ? s->hg[xi] * (s->hqu - s->hql) : 0.0)));
+    }
+    if (rk && P->soft) rd0 = fmax(rd0, fabs(s->Zl * s->hs + s->zl - s->hql - s->hqs));
   }
   P->rs = 1.0;
   int it, status = 1;
@@ -655,7 +760,12 @@ static int fqp(fprob_t* P, int* iters) {
         mu += (s->dz[i] - s->Lb[i]) * s->ql[i] + (s->Ub[i] - s->dz[i]) * s->qu[i];
       }
     }
-    if (P->nn) mu += P->htl * P->hql + P->htu * P->hqu;
+    for (int k = 0; k <= N; ++k) {
+      if (!frow(P, k)) continue;
+      const fstage_t* s = &P->st[k];
+      mu += s->htl * s->hql + s->htu * s->hqu;
+      if (P->soft) mu += s->hs * s->hqs;
+    }
     mu /= (double)nbox;
     if (!isfinite(mu)) { status = -1; break; }
     if (mu < o->qp_tol_comp && P->rs * rd0 < o->qp_tol_stat && P->rs * e00 < o->qp_tol_eq) { status = 0; break; }
@@ -669,10 +779,13 @@ static int fqp(fprob_t* P, int* iters) {
         s->H[i] = H; s->g[i] = g;
       }
     }
-    if (P->nn) {   /* the row's predictor term c gamma in the terminal gradient */
-      P->hatl = P->hatu = P->haql = P->haqu = 0.0;
-      const double gam = P->hql * (P->rs * P->hr0l) / P->htl - P->hqu * (P->rs * P->hr0u) / P->htu;
-      for (int i = 0; i < nx; ++i) P->st[N].g[i] += P->hg[i] * gam;
+    for (int k = 0; k <= N; ++k) {   /* the rows' predictor terms c gamma in the stage gradients */
+      if (!frow(P, k)) continue;
+      fstage_t* s = &P->st[k];
+      s->hatl = s->hatu = s->haql = s->haqu = s->has = s->haqs = 0.0;
+      double rcl, rcu, rcs;
+      frow_rc(s, 0.0, &rcl, &rcu, &rcs);
+      frow_addgrad(P, k, s->g, frow_gamma(P, s, P->rs, rcl, rcu, rcs, 1));
     }
     if (fnewton(P, 1, nu_new)) { status = -1; break; }
     fratio_t ma = {1.0, 1.0};
@@ -689,14 +802,21 @@ static int fqp(fprob_t* P, int* iters) {
         fr_add(&ma, s->qu[i], dlu);
       }
     }
-    if (P->nn) {
-      double dtl, dtu, dql, dqu;
-      frow_dir(P, 0.0, &dtl, &dtu, &dql, &dqu);
-      P->hatl = dtl; P->hatu = dtu; P->haql = dql; P->haqu = dqu;
-      fr_add(&ma, P->htl, dtl);
-      fr_add(&ma, P->htu, dtu);
-      fr_add(&ma, P->hql, dql);
-      fr_add(&ma, P->hqu, dqu);
+    for (int k = 0; k <= N; ++k) {
+      if (!frow(P, k)) continue;
+      fstage_t* s = &P->st[k];
+      double rcl, rcu, rcs, dtl, dtu, dql, dqu, ds, dqs;
+      frow_rc(s, 0.0, &rcl, &rcu, &rcs);
+      frow_dirs(P, s, frow_dot(P, k, s->d), P->rs, rcl, rcu, rcs, &dtl, &dtu, &dql, &dqu, &ds, &dqs);
+      s->hatl = dtl; s->hatu = dtu; s->haql = dql; s->haqu = dqu; s->has = ds; s->haqs = dqs;
+      fr_add(&ma, s->htl, dtl);
+      fr_add(&ma, s->htu, dtu);
+      fr_add(&ma, s->hql, dql);
+      fr_add(&ma, s->hqu, dqu);
+      if (P->soft) {
+        fr_add(&ma, s->hs, ds);
+        fr_add(&ma, s->hqs, dqs);
+      }
     }
     const double aa = ma.n / ma.d;
     double muaff = 0.0;
@@ -709,8 +829,12 @@ static int fqp(fprob_t* P, int* iters) {
         muaff += (tl + aa * d) * (s->ql[i] + aa * dll) + (tu - aa * d) * (s->qu[i] + aa * dlu);
       }
     }
-    if (P->nn)
-      muaff += (P->htl + aa * P->hatl) * (P->hql + aa * P->haql) + (P->htu + aa * P->hatu) * (P->hqu + aa * P->haqu);
+    for (int k = 0; k <= N; ++k) {
+      if (!frow(P, k)) continue;
+      const fstage_t* s = &P->st[k];
+      muaff += (s->htl + aa * s->hatl) * (s->hql + aa * s->haql) + (s->htu + aa * s->hatu) * (s->hqu + aa * s->haqu);
+      if (P->soft) muaff += (s->hs + aa * s->has) * (s->hqs + aa * s->haqs);
+    }
     muaff /= (double)nbox;
     double sig = muaff / mu;
     sig = sig * sig * sig;
@@ -726,11 +850,12 @@ static int fqp(fprob_t* P, int* iters) {
         s->g[i] = (rho + fhq(P, k, i)) * s->dz[i] + fgrad(P, k, i) - s->ql[i] - rl * itl + s->qu[i] + ru * itu;
       }
     }
-    if (P->nn) {   /* the row's Mehrotra-corrected term */
-      const double rl = P->rs * P->hr0l, ru = P->rs * P->hr0u;
-      const double rcl = smu - P->htl * P->hql - P->hatl * P->haql, rcu = smu - P->htu * P->hqu - P->hatu * P->haqu;
-      const double gam = -P->hql + P->hqu - (rcl - P->hql * rl) / P->htl + (rcu - P->hqu * ru) / P->htu;
-      for (int i = 0; i < nx; ++i) P->st[N].g[i] += P->hg[i] * gam;
+    for (int k = 0; k <= N; ++k) {   /* the rows' Mehrotra-corrected terms */
+      if (!frow(P, k)) continue;
+      fstage_t* s = &P->st[k];
+      double rcl, rcu, rcs;
+      frow_rc(s, smu, &rcl, &rcu, &rcs);
+      frow_addgrad(P, k, s->g, frow_gamma(P, s, P->rs, rcl, rcu, rcs, 0));
     }
     if (fnewton(P, 0, nu_new)) { status = -1; break; }
     fratio_t mx = {1.0, o->ipm_tau};
@@ -749,13 +874,21 @@ static int fqp(fprob_t* P, int* iters) {
         fr_add(&mx, s->qu[i], dlu);
       }
     }
-    double rdtl = 0, rdtu = 0, rdql = 0, rdqu = 0;
-    if (P->nn) {
-      frow_dir(P, smu, &rdtl, &rdtu, &rdql, &rdqu);
-      fr_add(&mx, P->htl, rdtl);
-      fr_add(&mx, P->htu, rdtu);
-      fr_add(&mx, P->hql, rdql);
-      fr_add(&mx, P->hqu, rdqu);
+    for (int k = 0; k <= N; ++k) {
+      if (!frow(P, k)) continue;
+      fstage_t* s = &P->st[k];
+      double rcl, rcu, rcs;
+      frow_rc(s, smu, &rcl, &rcu, &rcs);
+      frow_dirs(P, s, frow_dot(P, k, s->d), P->rs, rcl, rcu, rcs, &s->hdtl, &s->hdtu, &s->hdql, &s->hdqu, &s->hds,
+                &s->hdqs);
+      fr_add(&mx, s->htl, s->hdtl);
+      fr_add(&mx, s->htu, s->hdtu);
+      fr_add(&mx, s->hql, s->hdql);
+      fr_add(&mx, s->hqu, s->hdqu);
+      if (P->soft) {
+        fr_add(&mx, s->hs, s->hds);
+        fr_add(&mx, s->hqs, s->hdqs);
+      }
     }
     const double alpha = fmin(1.0, o->ipm_tau * (mx.n / mx.d));
     for (int k = 0; k <= N; ++k) {
@@ -772,9 +905,15 @@ static int fqp(fprob_t* P, int* iters) {
         s->dz[i] += alpha * d;
       }
     }
-    if (P->nn) {
-      P->htl += alpha * rdtl; P->htu += alpha * rdtu;
-      P->hql += alpha * rdql; P->hqu += alpha * rdqu;
+    for (int k = 0; k <= N; ++k) {
+      if (!frow(P, k)) continue;
+      fstage_t* s = &P->st[k];
+      s->htl += alpha * s->hdtl; s->htu += alpha * s->hdtu;
+      s->hql += alpha * s->hdql; s->hqu += alpha * s->hdqu;
+      if (P->soft) {
+        s->hs += alpha * s->hds;
+        s->hqs += alpha * s->hdqs;
+      }
     }
     for (int j = 0; j < ne; ++j) P->qnu[j] += alpha * (nu_new[j] - P->qnu[j]);
     P->rs *= (1.0 - alpha);
@@ -787,7 +926,7 @@ static int fqp(fprob_t* P, int* iters) {
     const fstage_t* sN = &P->st[N];
     for (int i = 0; i < nx; ++i) {
       lam[i] = (rho + fhq(P, N, i)) * sN->dz[i] + fgrad(P, N, i) - sN->ql[i] + sN->qu[i];
-      if (P->nn) lam[i] += P->hg[i] * (P->hqu - P->hql);
+      if (frow(P, N)) lam[i] += sN->hg[i] * (sN->hqu - sN->hql);
     }
     for (int j = 0; j < ne; ++j) lam[P->ei[j]] += P->qnu[j];
     for (int k = N - 1; k >= 0; --k) {
@@ -797,6 +936,7 @@ static int fqp(fprob_t* P, int* iters) {
       double ln[FX];
       for (int i = 0; i < nx; ++i) {
         double t = (rho + fhq(P, k, i)) * s->dz[i] + fgrad(P, k, i) - s->ql[i] + s->qu[i];
+        if (frow(P, k)) t += s->hg[i] * (s->hqu - s->hql);   /* a path row's term */
         for (int q = 0; q < nx; ++q) t += s->A[q * nx + i] * lam[q];
         ln[i] = t;
       }
@@ -855,9 +995,20 @@ static double fmerit(const fprob_t* P, double alpha) {
     memcpy(uk, un, sizeof(uk));
   }
   for (int j = 0; j < P->ne; ++j) val += P->wnu[j] * fabs(xk[P->ei[j]] - P->ev[j]);
-  if (P->nn) {   /* the terminal row's violation at the trial state, weighted like the boxes */
-    const double hv = nn_row(P->nn, P->nq, xk, NULL);
-    val += P->wbnd * (fmax(0.0, P->nn->lh - hv) + fmax(0.0, hv - P->nn->uh));
+  for (int k = 0; k <= N; ++k) {
+    /* the rows' violations at the trial states, weighted like the boxes; a soft row's trial slack, its cost and
+       its bound s >= 0 */
+    if (!frow(P, k)) continue;
+    const fstage_t* st = &P->st[k];
+    fstate_at(P, k, alpha, xn, un);
+    const double hv = nn_row(P->nn, P->nq, xn, NULL, P->soft, P->sm);
+    const double sa = P->soft ? st->sl + alpha * (st->hs - st->sl) : 0.0;
+    double v = fmax(0.0, P->nn->lh - hv - sa) + fmax(0.0, hv - P->nn->uh);
+    if (P->soft) {
+      v += fmax(0.0, -sa);
+      val += st->zl * sa + 0.5 * st->Zl * sa * sa;
+    }
+    val += P->wbnd * v;
   }
   return val;
 }
@@ -892,7 +1043,12 @@ static void fsqp(fprob_t* P, vboc_result_t* res) {
       if (k < N) for (int i = 0; i < nx; ++i) s->wpi[i] = fwupd(s->wpi[i], s->qpi[i]);
       for (int i = 0; i < fnz(P, k); ++i) lmax = fmax(lmax, fmax(s->ql[i], s->qu[i]));
     }
-    if (P->nn) lmax = fmax(lmax, fmax(P->hql, P->hqu));
+    for (int k = 0; k <= N; ++k) {
+      if (!frow(P, k)) continue;
+      const fstage_t* s = &P->st[k];
+      lmax = fmax(lmax, fmax(s->hql, s->hqu));
+      if (P->soft) lmax = fmax(lmax, s->hqs);
+    }
     for (int j = 0; j < P->ne; ++j) P->wnu[j] = fwupd(P->wnu[j], P->qnu[j]);
     P->wbnd = fwupd(P->wbnd, lmax);
     double alpha = 1.0;
@@ -918,9 +1074,15 @@ static void fsqp(fprob_t* P, vboc_result_t* res) {
       if (k < N) for (int i = 0; i < nx; ++i) s->pi[i] += alpha * (s->qpi[i] - s->pi[i]);
     }
     for (int j = 0; j < P->ne; ++j) P->tnu[j] += alpha * (P->qnu[j] - P->tnu[j]);
-    if (P->nn) {
-      P->hll += alpha * (P->hql - P->hll);
-      P->hlu += alpha * (P->hqu - P->hlu);
+    for (int k = 0; k <= N; ++k) {
+      if (!frow(P, k)) continue;
+      fstage_t* s = &P->st[k];
+      s->hll += alpha * (s->hql - s->hll);
+      s->hlu += alpha * (s->hqu - s->hlu);
+      if (P->soft) {
+        s->sl += alpha * (s->hs - s->sl);
+        s->lsl += alpha * (s->hqs - s->lsl);
+      }
     }
     if (!isfinite(P->st[0].x[nx - 1])) { status = 1; break; }
   }
@@ -999,12 +1161,15 @@ int vboc_oracle_ft_solve_batch(int nq, int B, int Nmax, const int* N, const doub
 }
 
 /* Safe-MPC OCP_solve (HardTerm, :163-181): x_0 fixed, boxes, tracking cost, terminal NN row, SQP or SQP_RTI.
-   x [N + 1][2 nq] and u [N][nq] without the dt column; hrow (may be NULL) gets h(x_N) of the result. */
-int vboc_oracle_mpc_solve(int nq, int N, double h, const double* x0, const double* x_guess, const double* u_guess,
-                          const double* xlb, const double* xub, const double* ulb, const double* uub,
-                          const double* xNlb, const double* xNub, const double* W, const double* We,
-                          const double* yref, const double* yref_e, double cs, const vboc_mpc_nn_t* nn, int rti,
-                          const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* hrow) {
+   x [N + 1][2 nq] and u [N][nq] without the dt column; hrow (may be NULL) gets h(x_N) of the result.
+   soft (SoftTraj, :242-304; NULL = HardTerm): the margin-scaled row on every stage, soft lower sides with the
+   per-stage weights zl / Zl [N + 1]. */
+int vboc_oracle_mpc_solve_soft(int nq, int N, double h, const double* x0, const double* x_guess,
+                               const double* u_guess, const double* xlb, const double* xub, const double* ulb,
+                               const double* uub, const double* xNlb, const double* xNub, const double* W,
+                               const double* We, const double* yref, const double* yref_e, double cs,
+                               const vboc_mpc_nn_t* nn, const vboc_mpc_soft_t* soft, int rti, const vboc_opts_t* opts,
+                               double* x_out, double* u_out, vboc_result_t* res, double* hrow) {
   if (nq < 1 || nq > FQ || N < 1) return -1;
   const int n2 = 2 * nq, nx = n2 + 1, nu = nq;
   for (int i = 0; i < n2; ++i) if (!(xlb[i] < xub[i]) || !(xNlb[i] < xNub[i])) return -2;
@@ -1021,6 +1186,8 @@ int vboc_oracle_mpc_solve(int nq, int N, double h, const double* x0, const doubl
   P.x0lb[n2] = P.x0ub[n2] = h;
   for (int a = 0; a < nu; ++a) { P.ulb[a] = ulb[a]; P.uub[a] = uub[a]; }
   P.track = 1; P.rti = rti; P.cs = cs; P.nn = nn;
+  if (soft && !nn) return -2;
+  if (soft) { P.soft = 1; P.sm = 100.0 - soft->margin; }
   for (int i = 0; i < n2; ++i) { P.wq[i] = W[i]; P.yr[i] = yref[i]; P.we[i] = We[i]; P.yre[i] = yref_e[i]; }
   for (int a = 0; a < nu; ++a) { P.wq[nx + a] = W[n2 + a]; P.yr[nx + a] = yref[n2 + a]; }
   P.st = (fstage_t*)calloc((size_t)N + 1, sizeof(fstage_t));
@@ -1031,14 +1198,64 @@ int vboc_oracle_mpc_solve(int nq, int N, double h, const double* x0, const doubl
     if (k < N) for (int a = 0; a < nu; ++a) P.st[k].u[a] = u_guess[k * nu + a];
   }
   for (int i = 0; i < n2; ++i) P.st[0].x[i] = x0[i];
+  if (soft)
+    for (int k = 0; k <= N; ++k) { P.st[k].zl = soft->zl ? soft->zl[k] : 0.0; P.st[k].Zl = soft->Zl ? soft->Zl[k] : 0.0; }
   fsqp(&P, res);
   for (int k = 0; k <= N; ++k) {
     for (int i = 0; i < n2; ++i) x_out[k * n2 + i] = P.st[k].x[i];
     if (k < N) for (int a = 0; a < nu; ++a) u_out[k * nu + a] = P.st[k].u[a];
   }
-  if (hrow) *hrow = nn ? nn_row(nn, nq, P.st[N].x, NULL) : 0.0;
+  if (hrow) *hrow = nn ? nn_row(nn, nq, P.st[N].x, NULL, P.soft, P.sm) : 0.0;
   free(P.st);
   return 0;
+}
+
+int vboc_oracle_mpc_solve(int nq, int N, double h, const double* x0, const double* x_guess, const double* u_guess,
+                          const double* xlb, const double* xub, const double* ulb, const double* uub,
+                          const double* xNlb, const double* xNub, const double* W, const double* We,
+                          const double* yref, const double* yref_e, double cs, const vboc_mpc_nn_t* nn, int rti,
+                          const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* hrow) {
+  return vboc_oracle_mpc_solve_soft(nq, N, h, x0, x_guess, u_guess, xlb, xub, ulb, uub, xNlb, xNub, W, We, yref,
+                                    yref_e, cs, nn, NULL, rti, opts, x_out, u_out, res, hrow);
+}
+
+/* SoftTraj batch: per problem its stage weights W [B][3 nq] / We [B][2 nq] (the receding driver's cost_set(i, "W")
+   per initial state) and its slack weights zl / Zl [B][N + 1] */
+int vboc_oracle_mpc_soft_solve_batch(int nq, int B, int N, double h, const double* x0, const double* x_guess,
+                                     const double* u_guess, const double* xlb, const double* xub, const double* ulb,
+                                     const double* uub, const double* xNlb, const double* xNub, const double* W,
+                                     const double* We, const double* yref, const double* yref_e, double cs,
+                                     const vboc_mpc_nn_t* nn, double margin, const double* zl, const double* Zl,
+                                     int rti, const vboc_opts_t* opts, int nthreads, double* x_out, double* u_out,
+                                     vboc_result_t* res, double* hrow) {
+  const int n2 = 2 * nq;
+  int err = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(| : err)
+  for (int b = 0; b < B; ++b) {
+    const size_t xo = (size_t)b * (N + 1) * n2, uo = (size_t)b * N * nq;
+    vboc_mpc_soft_t sf;
+    sf.margin = margin;
+    sf.zl = zl + (size_t)b * (N + 1);
+    sf.Zl = Zl + (size_t)b * (N + 1);
+    const int r = vboc_oracle_mpc_solve_soft(nq, N, h, x0 + (size_t)b * n2, x_guess + xo, u_guess + uo, xlb, xub,
+                                             ulb, uub, xNlb, xNub, W + (size_t)b * 3 * nq, We + (size_t)b * n2, yref,
+                                             yref_e, cs, nn, &sf, rti, opts, x_out + xo, u_out + uo, res + b,
+                                             hrow ? hrow + b : NULL);
+    if (r == -2) { res[b].status = 5; res[b].sqp_iter = 0; res[b].qp_iter = 0; res[b].cost = NAN; }
+    else if (r) err |= 1;
+  }
+  return err ? -1 : 0;
+}
+
+/* the SoftTraj row h(x) = NN(z(x)) (100 - margin) / 100 - vn(x) at B states x [B][2 nq] (nn_decisionfunction_
+   conservative, :284-304; the receding driver evaluates it on the previous solution, receiding_hard_constraints/
+   3dof_sym.py:32-35); margin < 0: the unscaled HardTerm row */
+void vboc_oracle_mpc_row(int nq, int B, const double* x, const vboc_mpc_nn_t* nn, double margin, double* out) {
+  for (int b = 0; b < B; ++b) {
+    double xx[FX] = {0};
+    for (int i = 0; i < 2 * nq; ++i) xx[i] = x[(size_t)b * 2 * nq + i];
+    out[b] = nn_row(nn, nq, xx, NULL, margin >= 0.0, 100.0 - margin);
+  }
 }
 
 int vboc_oracle_mpc_solve_batch(int nq, int B, int N, double h, const double* x0, const double* x_guess,

@@ -233,3 +233,92 @@ def slsqp_mpc(spec, x0, start, params=None, mean=0.0, std=1.0, maxiter=300):
                  options=dict(maxiter=maxiter, ftol=1e-14))
     U, X = unpack(r.x)
     return X, U, cost(r.x), r
+
+
+def slsqp_mpc_soft(spec, x0, start, params, mean, std, margin, Zl, zl=None, W=None, We=None, maxiter=500):
+    """OCPtriplependulumSoftTraj (VBOC/Safe MPC/triplependulum_class_vboc.py:242-304) as an independent NLP for scipy
+    SLSQP: decision vector (u_0..u_{N-1}, x_1..x_N, s_0..s_N) with the slacks explicit, RK4 defects, boxes, the
+    margin-scaled row h(x_k) = NN(x_k) (100 - margin) / 100 - vn(x_k) on every stage softened as h(x_k) + s_k >= 0,
+    s_k >= 0, and the slack cost sum_k zl_k s_k + Zl_k s_k^2 / 2 (zu = Zu = 0: the upper side h <= 1e6 is never active
+    and left out).  start = (x [N+1, 6], u [N, 3], s [N+1] or None).  Returns (x, u, s, cost, scipy result)."""
+    from vboc_amd.safempc import nn_row
+    N, h, nx, nu = spec.N, spec.time_step, 6, 3
+    x0 = np.asarray(x0, dtype=np.float64)
+    W = spec.W if W is None else np.asarray(W, float)
+    We = spec.W_e if We is None else np.asarray(We, float)
+    Zl = np.broadcast_to(np.asarray(Zl, float), (N + 1,))
+    zl = np.zeros(N + 1) if zl is None else np.broadcast_to(np.asarray(zl, float), (N + 1,))
+    yr, yre, cs = spec.yref, spec.yref_e, spec.cost_scale
+    nq = N * nu + N * nx
+    nv = nq + N + 1
+    row = lambda x: nn_row(params, mean, std, x, safety_margin=margin)
+
+    def unpack(z):
+        return z[:N * nu].reshape(N, nu), np.vstack([x0, z[N * nu:nq].reshape(N, nx)]), z[nq:]
+
+    def cost(z):
+        U, X, S = unpack(z)
+        c = 0.0
+        for k in range(N):
+            d = np.r_[X[k], U[k]] - yr
+            c += cs * 0.5 * float(d @ (W * d))
+        d = X[N] - yre
+        return c + 0.5 * float(d @ (We * d)) + float(zl @ S) + 0.5 * float(S @ (Zl * S))
+
+    def grad(z):
+        U, X, S = unpack(z)
+        g = np.zeros(nv)
+        for k in range(N):
+            d = np.r_[X[k], U[k]] - yr
+            g[k * nu:(k + 1) * nu] = cs * W[nx:] * d[nx:]
+            if k > 0:
+                g[N * nu + (k - 1) * nx:N * nu + k * nx] += cs * W[:nx] * d[:nx]
+        g[N * nu + (N - 1) * nx:nq] += We * (X[N] - yre)
+        g[nq:] = zl + Zl * S
+        return g
+
+    def eq(z):
+        U, X, _ = unpack(z)
+        return np.concatenate([X[k + 1] - oracle.rk4(3, h, X[k], U[k]) for k in range(N)])
+
+    def eqjac(z):
+        U, X, _ = unpack(z)
+        J = np.zeros((N * nx, nv))
+        for k in range(N):
+            _, A, B = oracle.rk4_sens(3, h, X[k], U[k])
+            r = slice(k * nx, (k + 1) * nx)
+            J[r, k * nu:(k + 1) * nu] = -B
+            if k > 0:
+                J[r, N * nu + (k - 1) * nx:N * nu + k * nx] = -A
+            J[r, N * nu + k * nx:N * nu + (k + 1) * nx] += np.eye(nx)
+        return J
+
+    def ineq(z):
+        _, X, S = unpack(z)
+        return np.array([row(X[k]) + S[k] for k in range(N + 1)])
+
+    def ineqjac(z):
+        _, X, _ = unpack(z)
+        J = np.zeros((N + 1, nv))
+        for k in range(N + 1):
+            J[k, nq + k] = 1.0
+            if k == 0:
+                continue                      # x_0 fixed
+            for j in range(nx):
+                e = np.zeros(nx)
+                e[j] = 1e-6
+                J[k, N * nu + (k - 1) * nx + j] = (row(X[k] + e) - row(X[k] - e)) / 2e-6
+        return J
+
+    bounds = [(spec.umin[a], spec.umax[a]) for _ in range(N) for a in range(nu)]
+    bounds += [(spec.xmin[j], spec.xmax[j]) for _ in range(N) for j in range(nx)]
+    bounds += [(0.0, None)] * (N + 1)
+    xs, us = start[0], start[1]
+    s0 = start[2] if len(start) > 2 and start[2] is not None else np.array(
+        [max(0.0, -row(np.asarray(xs, float)[k])) for k in range(N + 1)])
+    z0 = np.r_[np.asarray(us, float).ravel(), np.asarray(xs, float)[1:].ravel(), np.asarray(s0, float)]
+    r = minimize(cost, z0, jac=grad, bounds=bounds,
+                 constraints=[dict(type="eq", fun=eq, jac=eqjac), dict(type="ineq", fun=ineq, jac=ineqjac)],
+                 method="SLSQP", options=dict(maxiter=maxiter, ftol=1e-14))
+    U, X, S = unpack(r.x)
+    return X, U, S, cost(r.x), r

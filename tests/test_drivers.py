@@ -61,19 +61,16 @@ def test_driver_matches_reference_state_machine(nq):
 @pytest.mark.gpu
 @pytest.mark.parametrize("nq", [3, 2])
 def test_driver_on_gpu_matches_reference(nq):
-    from vboc_amd.drivers import GpuBackend, data_generation_batch
+    """The batched driver on the GPU against the reference's own data_generation on the oracle, both fixture sets:
+    every problem equal to 1e-5, or parting from the oracle-backed driver in lockstep for an allowed reason
+    (tests/parity.py: a flipped tolerance decision, a different status, two confirmed optima)."""
+    from parity import FailingGpu, explain
+    from vboc_amd.drivers import data_generation_batch
     g = _golden(nq)
-    res, _ = data_generation_batch(nq, np.array(g["ids"]), GpuBackend(nq), N_start=g["N_start"])
-    same = 0
-    for got, ref in zip(res, g["results"]):
-        a, b = _samples(nq, got), _samples(nq, ref)
-        if a is None or b is None:
-            same += (a is None) == (b is None)
-        elif a.shape == b.shape and np.abs(a - b).max() < 1e-5:
-            same += 1
-    # rounding-level solver differences may flip a tolerance decision on a problem (classified in
-    # test_gpu_driver_mismatches_are_rounding_level_flips; measured: none on these fixtures)
-    assert same >= 0.95 * len(g["ids"]), (same, len(g["ids"]))
+    for ids, results, fail_mod in _sets(g):
+        res, _ = data_generation_batch(nq, np.array(ids), FailingGpu(nq, fail_mod), N_start=g["N_start"])
+        n, kinds, _ = explain(nq, "dg", g, ids, res, results, fail_mod)
+        print(f"nq {nq} fail_mod {fail_mod}: {len(ids) - n}/{len(ids)} as the fixture, mismatches {kinds}")
 
 
 # ------------------------------------------------------------------------------------------------
@@ -147,18 +144,15 @@ class _FailingGpu:
 @pytest.mark.gpu
 @pytest.mark.parametrize("nq", [3, 2, 1])
 def test_testing_driver_on_gpu_matches_reference(nq):
+    """The batched `testing` driver on the GPU against the reference's function on the oracle: every problem equal
+    to 1e-5 or explained in lockstep (tests/parity.py) - e.g. the 3-decimal stop rule flipped on a rounding-level
+    cost difference."""
+    from parity import explain
     from vboc_amd.drivers import testing_batch
     g = _golden_test(nq)
     res, _ = testing_batch(nq, np.array(g["ids"]), _FailingGpu(nq, g["fail_mod"]), N_start=g["N_start"])
-    same = 0
-    for got, ref in zip(res, g["results"]):
-        if got is None or ref is None:
-            same += (got is None) == (ref is None)
-        elif np.abs(np.asarray(got) - np.asarray(ref)).max() < 1e-5:
-            same += 1
-    # a rounding-level cost difference can flip the 3-decimal stop rule on a problem (classified in
-    # test_gpu_driver_mismatches_are_rounding_level_flips; measured: none on these fixtures)
-    assert same >= 0.95 * len(g["ids"]), (same, len(g["ids"]))
+    n, kinds, _ = explain(nq, "test", g, g["ids"], res, g["results"], g["fail_mod"])
+    print(f"nq {nq}: {len(g['ids']) - n}/{len(g['ids'])} as the fixture, mismatches {kinds}")
 
 
 def _gens(nq, law, g):
@@ -236,11 +230,16 @@ def test_gpu_driver_mismatches_are_rounding_level_flips(nq, law):
     fm = g.get("fail_mod", 0)
     gpu = GpuBackend(nq) if law == "dg" else _FailingGpu(nq, fm)
     ora = OracleBackend(nq) if law == "dg" else OracleBackend(nq, fm)
+    from parity import dump
+    trace = {}
     kinds = lockstep(nq, _gens(nq, law, g), [int(p) for p in g["ids"]], gpu, ora, nmax=200,
-                     verify=_converges_back(nq, OracleBackend(nq)))
+                     verify=_converges_back(nq, OracleBackend(nq)), trace=trace)
     counts = {k: sum(v[0] == k for v in kinds.values()) for k in ("same", "decision", "status", "optimum", "value")}
     print(nq, law, counts, {p: v for p, v in kinds.items() if v[0] != "same"})
-    assert counts["value"] == 0, kinds
+    dump(f"lockstep_{law}_{nq}.json", dict(counts=counts, partings=trace))
+    assert counts["value"] == 0, trace
+    # two confirmed optima are reported and capped like the decision flips: at most 1 % of the problems (at least 1)
+    assert counts["optimum"] <= max(1, len(kinds) // 100), trace
     # measured on MI355X (profiles/r02s_pytest_gpu_lockstep_classification.log): every problem 'same'
     assert counts["same"] >= 0.95 * len(kinds), counts
 

@@ -260,10 +260,12 @@ __device__ __forceinline__ void tri(int u, int& i, int& j) {
 __device__ unsigned long long g_wave_prof[16];
 __device__ unsigned g_dbg_cnt;
 // measurement builds (-DVBOC_VEC_DUMP): workgroup 0's first VBOC_VEC_DUMP_CALLS vector-pass outputs (the staged rows
-// XS[0..N][NX] and the stage-0 value), read back with vboc_debug_dump()
+// XS[0..N][NX] and the stage-0 value), read back with vboc_debug_dump(); absent from product builds
+#ifdef VBOC_VEC_DUMP
 __device__ double g_vdump[8][1024];
 __device__ unsigned g_vdump_calls;
 __device__ double g_vdump2[8][256];   // [0, W) the landed first slot, [W, 2W) the record's window read directly, pcur
+#endif
 #ifdef VBOC_COOP_PROF
 #define CPROF_DECL unsigned long long cp0 = 0, cp1 = 0, cp2 = 0, cp3 = 0, cp4 = 0, cp5 = 0, cp6 = 0, cp7 = 0, cp8 = 0; \
   unsigned long long cp_t = __builtin_amdgcn_s_memtime();
@@ -302,6 +304,24 @@ __device__ double g_vdump2[8][256];   // [0, W) the landed first slot, [W, 2W) t
 
 #define VREP(id, stmt) do { stmt; if constexpr (VBOC_REPEAT == (id)) { stmt; } } while (0)
 
+// Pass fusions of the IPM iteration (round 5; pendulum chains with the MFMA factorisation, no path constraint - the
+// instantiations of the data-generation loop and the first solves).  Each removes stage-record traffic (a pass or
+// part of a window) with the same arithmetic in the same order, so results are bit-identical; -DVBOC_FUSE=<mask>
+// selects them for measurements (0: the round-4 passes).
+//   1 FAC1   the factorisation's window is its inputs [A, K) - one LDS-DMA per stage instead of two ([K, C) was
+//            loaded only to be overwritten by the stage's outputs before the write-back);
+//   2 PFUSE  the predictor preparation (D = H, DA = predictor gradient) is computed by the iterate update of the
+//            previous IPM iteration from the values it has just written (prep_pred runs for the first only) - OFF:
+//            not bit-identical on the box (another digest of the 100k-problem launch, gpurun_out/r05a; the compiler
+//            contracts the inlined copy differently), +0.4 % bulk rate alone;
+//   4 CCORR  the corrector gradient pass also forms the corrector vector pass's constant c' (vec's stage-parallel
+//            pre-pass re-read the gradient with K, A_cl, P e);
+//   8 KFM    the forward sweep's constant pass stores k_f - M nu over k_f, and the step-length pass reads it instead
+//            of re-reading M and chol(Ru) to recompute it.
+#ifndef VBOC_FUSE
+#define VBOC_FUSE 13
+#endif
+
 // HC: the Cartesian path-constraint rows (vboc_set_path_constraint; oracle/vboc_oracle.c hc_*, Lane::hc_*) on
 // stages 1..N-1, pendulum chains with the VALU factorisation only.  No change of the stage-record layout: the
 // rows' state lives in a per-workgroup region `gh` (Lane<NQ>::FHC fields per stage); the Hessian's position
@@ -315,6 +335,9 @@ struct Coop {
   static_assert(!HC || (!FM && NQ >= 2 && NQ <= 3), "path constraint: pendulum chains, VALU factorisation");
   using PF = Par<NQ>;
   static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1, REC = L::REC;
+  static constexpr bool FUSE_OK = FM && NQ <= 3 && !HC;
+  static constexpr bool FAC1 = FUSE_OK && (VBOC_FUSE & 1), PFUSE = FUSE_OK && (VBOC_FUSE & 2),
+                        CCORR = FUSE_OK && (VBOC_FUSE & 4), KFM = FUSE_OK && (VBOC_FUSE & 8);
   static constexpr int OA = L::OA, OB = L::OB, OZ = L::OZ, ODZ = L::ODZ, OQL = L::OQL, OQU = L::OQU,
                        OE = L::OE, OK = L::OK, OKF = L::OKF, OLR = L::OLR, OM = L::OM, OY = L::OY,
                        OPE = L::OPE, OD = L::OD, ODA = L::ODA, OC = L::OC, OACL = L::OACL, OX = L::OX, OU = L::OU,
@@ -1009,6 +1032,14 @@ struct Coop {
     return 1;
   }
 
+  // H -> D, predictor gradient -> DA of stage k from its iterate r (z, dz, lambda_l, lambda_u)
+  __device__ __forceinline__ void prep_from(const IP& r, int k, gdouble* rec) const {
+    UNR for (int i = 0; i < NZ; ++i) {
+      const CS c = comp_r(r, k, i);
+      rec[OD + i] = o.lm + (c.bx ? c.ql * c.itl + c.qu * c.itu : 0.0);
+      rec[ODA + i] = o.lm * c.dz + cgrad(k, i);
+    }
+  }
   // H -> D slot, predictor gradient -> DA slot
   __device__ __forceinline__ void prep_pred() {
     fresh();
@@ -1017,11 +1048,7 @@ struct Coop {
       ld_ip(k, r);
       __builtin_amdgcn_sched_barrier(0);
       gdouble* rec = &g[(long long)k * REC];
-      UNR for (int i = 0; i < NZ; ++i) {
-        const CS c = comp_r(r, k, i);
-        rec[OD + i] = o.lm + (c.bx ? c.ql * c.itl + c.qu * c.itu : 0.0);
-        rec[ODA + i] = o.lm * c.dz + cgrad(k, i);
-      }
+      prep_from(r, k, rec);
       if constexpr (HC) {
         if (hc_on(k)) {
           const double htl = hcr(k, HL::HTL), htu = hcr(k, HL::HTU), hql = hcr(k, HL::HQL), hqu = hcr(k, HL::HQU);
@@ -1049,6 +1076,7 @@ struct Coop {
       ldr<OD, (2 * NZ + 1) / 2>(k, da);
       __builtin_amdgcn_sched_barrier(0);
       gdouble* rec = &g[(long long)k * REC];
+      double gv[NZ];
       UNR for (int i = 0; i < NZ; ++i) {
         const CS c = comp_r(r, k, i);
         double gg = o.lm * c.dz + cgrad(k, i);
@@ -1058,6 +1086,11 @@ struct Coop {
           gg += -c.ql - rl * c.itl + c.qu + ru * c.itu;
         }
         rec[OD + i] = gg;
+        gv[i] = gg;
+      }
+      if constexpr (CCORR) {
+        // the corrector vector pass's constant c' = g_x + K' g_u + A_cl' P e (vec_const, the same arithmetic)
+        if (k >= 1 && k < N) vec_const(k, gv);
       }
       if constexpr (HC) {
         if (hc_on(k)) {
@@ -1216,10 +1249,14 @@ struct Coop {
       if (row < NX && c >= CP && c < CP + NQ && row == NQ + (c - CP)) v = 1.0;
       Dm[r] = v;
     }
-    constexpr int P = L::P_FAC;
+    // FAC1: the window is the stage's inputs [A, K) (A, B, z .. lambda_u, e, D, DA): the outputs [K, A_cl] are
+    // written into the slot by this sweep before the write-back; k_f and C keep stale slot words, which the record
+    // holds only until the vector passes rewrite them (neither is read before)
+    constexpr int WF = FAC1 ? OK : L::W_FAC, P = (WF + 127) / 128;
+    static_assert(!FAC1 || P == 1, "the factorisation's inputs fit one LDS-DMA");
     auto fdma = [&](int j) {
       const int kk = N - 1 - j >= 0 ? N - 1 - j : 0;
-      UNR for (int part = 0; part < P; ++part) dma<1>(kk, 0, L::W_FAC, fslot(j % L::NSF), part);
+      UNR for (int part = 0; part < P; ++part) dma<1>(kk, 0, WF, fslot(j % L::NSF), part);
     };
     // loop-invariant per-lane constants.  A lane without a G / H operand reads the zeroed LDS words (ZERO,
     // absolute: slot base multiplier 0), never the slot's tail: the tail holds whatever the record's next
@@ -1278,7 +1315,7 @@ struct Coop {
       }
       fdma(j + 2);
       vmwait<2 * P>();   // loads only, as in factor()
-      dbg_check(kb, k, 0, L::W_FAC, 1);
+      dbg_check(kb, k, 0, WF, 1);
       // the three operand reads issue back to back (one LDS latency, not three)
       const double r0 = s[kb * gb[0] + goff[0]], r1 = s[kb * gb[1] + goff[1]], hv = s[kb * hb + hoff];
       double g0 = r0 * gm[0], g1 = r1 * gm[1];
@@ -1436,12 +1473,36 @@ struct Coop {
 
   // vector pass with the gradient in slot OG; leaves the stage-0 open-loop step w0 and the
   // terminal multiplier nu (wave-uniform).  False if S = sum Y'M is not positive definite.
+  // c'_k = g_x + K'g_u + A_cl' PE_k of stage k from its gradient gv (the vector pass's constant) -> OC
+  __device__ __forceinline__ void vec_const(int k, const double* gv) const {
+    constexpr int NKK = (NU * NX) / 2;
+    double kk[2 * NKK], ac[NX * NX], pe[NX];
+    ldr<OK, NKK>(k, kk);
+    ldr<OACL, NX * NX / 2>(k, ac);
+    ldr<OPE, NX / 2>(k, pe);
+    gdbl2* dst = (gdbl2*)(g + (long long)k * REC + OC);
+    double cv[NX];
+    UNR for (int i = 0; i < NX; ++i) {
+      double c = gv[i];
+      UNR for (int q = 0; q < NU; ++q) c += kk[q * NX + i] * gv[NX + q];
+      UNR for (int q = 0; q < NX; ++q) c += ac[q * NX + i] * pe[q];
+      cv[i] = c;
+    }
+    UNR for (int i = 0; i < NX; i += 2) {
+      dbl2 vv;
+      vv.x = cv[i];
+      vv.y = cv[i + 1];
+      dst[i / 2] = vv;
+    }
+  }
+  // PRE == false: the constants c' are already in OC (CCORR: prep_corr formed them)
+  template <bool PRE = true>
   __device__ __forceinline__ bool vec(int OG, double (&w0)[M0], double (&nun)[NQ]) {
     fresh();
     // p_k = c'_k + A_cl,k' p_{k+1},  c'_k = g_x + K'g_u + A_cl' PE_k  (lane i: row i of p);
     // v_k = PE_k + p_{k+1} is kept for k_f.  c' is formed stage-parallel first (-> OC).
     SPROF_DECL(2)
-    {
+    if constexpr (PRE) {
       constexpr int NZH = (2 * NZ + 1) / 2, NKK = (NU * NX) / 2;
       for (int k = 1 + t; k < N; k += 64) {
         double gg[2 * NZH], kk[2 * NKK], ac[NX * NX], pe[NX];
@@ -1695,6 +1756,9 @@ struct Coop {
           UNR for (int j = 0; j < NQ; ++j) x -= fm[(OM - OKF) + a * NQ + j] * nun[j];
           kfm[a] = x;
         }
+        if constexpr (KFM) {
+          UNR for (int a = 0; a < NU; ++a) st(k, OKF + a) = kfm[a];   // read by the step-length pass below
+        }
         gdbl2* dst = (gdbl2*)(g + (long long)k * REC + OC);
         UNR for (int i = 0; i < NX; i += 2) {
           double v[2];
@@ -1800,7 +1864,8 @@ struct Coop {
     // controls of the middle stages, then the step-length tests (stage-parallel)
     typename Lane<NQ>::MinRatio mr{1.0, CORR ? o.tau : 1.0};
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-    constexpr int NKM = (OY - OK + 1) / 2;   // K, k_f, chol(Ru), M: the range [OK, OY)
+    // K, k_f, chol(Ru), M: the range [OK, OY); KFM: K and k_f - M nu, the range [OK, OLR)
+    constexpr int NKM = KFM ? (OLR - OK + 1) / 2 : (OY - OK + 1) / 2;
     for (int k = t; k <= N; k += 64) {
       IP r;
       double km[2 * NKM], da[2 * ((2 * NZ + 1) / 2)];
@@ -1819,7 +1884,9 @@ struct Coop {
           double x = 0.0;
           if (k < N) {
             x = km[OKF - OK + a];
-            UNR for (int j = 0; j < NQ; ++j) x -= km[OM - OK + a * NQ + j] * nun[j];
+            if constexpr (!KFM) {
+              UNR for (int j = 0; j < NQ; ++j) x -= km[OM - OK + a * NQ + j] * nun[j];
+            }
             UNR for (int i = 0; i < NX; ++i) x += km[a * NX + i] * d[i];
           }
           d[NX + a] = x;
@@ -1882,10 +1949,14 @@ struct Coop {
       ldr<OD, (2 * NZ + 1) / 2>(k, dd);
       __builtin_amdgcn_sched_barrier(0);
       gdouble* rec = &g[(long long)k * REC];
+      IP rn;   // PFUSE: the updated iterate, for the next IPM iteration's D / DA
+      if constexpr (PFUSE) rn = r;
       UNR for (int i = 0; i < NZ; ++i) {
         const CS c = comp_r(r, k, i);
         const double d = dd[i];
-        rec[ODZ + i] = c.dz + alpha * d;
+        const double dzn = c.dz + alpha * d;
+        rec[ODZ + i] = dzn;
+        if constexpr (PFUSE) rn.v[NZ + i] = dzn;
         if (!c.bx) continue;
         double rl, ru;
         corr_rhs(c, dd[NZ + i], smu, rl, ru);
@@ -1893,8 +1964,10 @@ struct Coop {
         const double qln = c.ql + alpha * dll, qun = c.qu + alpha * dlu;
         rec[OQL + i] = qln;
         rec[OQU + i] = qun;
+        if constexpr (PFUSE) { rn.v[2 * NZ + i] = qln; rn.v[3 * NZ + i] = qun; }
         musum += (c.tl + alpha * d) * qln + (c.tu - alpha * d) * qun;
       }
+      if constexpr (PFUSE) prep_from(rn, k, rec);
       if constexpr (HC) {
         if (hc_on(k)) {
           double dtl, dtu, dql, dqu;
@@ -2150,7 +2223,7 @@ struct Coop {
         int q = qp_check();
         if (q == 1 && qcur >= o.qp_max_iter) q = 2;
         if (q != 1) { qst = q; break; }
-        VREP(1, prep_pred());
+        if (!PFUSE || qcur == 0) VREP(1, prep_pred());   // PFUSE: update() prepared the later iterations
         CPROF(2)
         bool okf;
         if constexpr (FM) VREP(2, okf = factor_mfma());
@@ -2171,7 +2244,7 @@ struct Coop {
         VREP(6, prep_corr(smu));
         CPROF(2)
         bool okc;
-        VREP(7, okc = vec(OD, w0, nun));
+        VREP(7, okc = vec<!CCORR>(OD, w0, nun));
         if (!okc) { qst = -1; break; }
         CPROF(4)
         double amax;

@@ -1830,7 +1830,9 @@ int vboc_create(int nq, int nmax, int slots, int device, vboc_handle* out) {
 int vboc_destroy(vboc_handle h) {
   if (!h) return VBOC_OK;
   (void)hipSetDevice(h->device);
-  if (h->dg_busy) (void)hipDeviceSynchronize();   // an un-waited async launch still uses the buffers freed below
+  // an un-waited async launch still uses the buffers freed below: wait for it alone (ev1 is recorded behind it on its
+  // stream), not for every stream of the device
+  if (h->dg_busy && h->ev1) (void)hipEventSynchronize(h->ev1);
   if (h->pool) (void)hipFree(h->pool);
   if (h->head) (void)hipFree(h->head);
   if (h->ist) (void)hipFree(h->ist);
@@ -2105,12 +2107,16 @@ int vboc_debug_counters(unsigned long long* out16) {
 // landed slot / its record window / pcur, and the call count (reset)
 int vboc_debug_dump(double* out8k, unsigned* calls) {
   if (!out8k || !calls) return fail(VBOC_ERR_ARG, "vboc_debug_dump: NULL argument");
+#ifndef VBOC_VEC_DUMP
+  return fail(VBOC_ERR_UNSUPPORTED, "vboc_debug_dump: a measurement build (-DVBOC_VEC_DUMP) only");
+#else
   HIPCHK(hipMemcpyFromSymbol(out8k, HIP_SYMBOL(g_vdump), 8 * 1024 * sizeof(double)));
   HIPCHK(hipMemcpyFromSymbol(calls, HIP_SYMBOL(g_vdump_calls), sizeof(unsigned)));
   HIPCHK(hipMemcpyFromSymbol(out8k + 8 * 1024, HIP_SYMBOL(g_vdump2), 8 * 256 * sizeof(double)));
   const unsigned z = 0;
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_vdump_calls), &z, sizeof(z)));
   return VBOC_OK;
+#endif
 }
 
 int vboc_last_kernel_ms(vboc_handle h, double* ms, int* launches) {
@@ -2495,7 +2501,11 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
     J.park_q = (int*)h->dg_park_buf;
     J.park_res = (double*)((char*)h->dg_park_buf + qbytes);
     J.park_stride = stride;
-    J.park_window = h->dg_park_window > 0 ? h->dg_park_window : b->B;
+    // park window: by default parked problems wait until the new ones run out (one launch = one batch).  A streamed
+    // launch (done flags: pipeline.StreamedRounds, many VBOC iterations' ids in order) releases its iterations as they
+    // complete, so a parked problem must not wait for every later iteration's new problems: there the window
+    // defaults to the resident waves, i.e. a parked problem resumes about one wave-generation after it was parked
+    J.park_window = h->dg_park_window > 0 ? h->dg_park_window : (done_flag ? (int)(groups < b->B ? groups : b->B) : b->B);
     HIPCHK(hipMemsetAsync(h->dg_park_buf, 0, sizeof(int) * 2 * (size_t)b->B, st));
   }
   HIPCHK(hipMemsetAsync(h->head, 0, 256, st));
@@ -2604,10 +2614,13 @@ int vboc_testing_test(vboc_handle h, vboc_tt_batch_t* b, void* stream) {
 
 // the end of a data-generation launch: its counters, the pool and horizon checks
 static int dg_wait(vboc_handle h, vboc_dg_batch_t* b, hipStream_t st) {
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipMemcpyAsync(h->host_done, h->head, 14 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  // the handle is released on every path: a failed copy / sync leaves the launch's outcome unknown (reported), but
+  // must not lock the handle for good
+  hipError_t e = hipSetDevice(h->device);
+  if (e == hipSuccess) e = hipMemcpyAsync(h->host_done, h->head, 14 * sizeof(unsigned), hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
   h->dg_busy = false;   // the launch has ended: the handle's buffers are free again
+  if (e != hipSuccess) return fail(VBOC_ERR_HIP, std::string("vboc_data_generation: waiting for the launch: ") + hipGetErrorString(e));
   const unsigned* c = h->host_done;
   b->rows_used = (long long)(((unsigned long long)c[5] << 32) | c[4]);
   b->spec_solves = (long long)(((unsigned long long)c[11] << 32) | c[10]);

@@ -57,15 +57,20 @@ def nn_params(model):
     return [np.ascontiguousarray(p.detach().cpu().numpy().astype(np.float64)) for p in model.parameters()]
 
 
-def nn_row(params, mean, std, x):
-    """h(x) = nn_decisionfunction(params, mean, std, x) (:208-230) for one state x [6] (numpy, for tests)."""
+def nn_row(params, mean, std, x, safety_margin=None):
+    """h(x) = nn_decisionfunction(params, mean, std, x) (:208-230) for one state x [6] (numpy); with safety_margin
+    the SoftTraj class's nn_decisionfunction_conservative (:284-304): out * (100 - safety_margin) / 100 - vn.  The
+    receding driver evaluates it on the previous solution's states (receiding_hard_constraints/3dof_sym.py:32-35)."""
     x = np.asarray(x, dtype=np.float64)
     vn = max(float(np.linalg.norm(x[2:])), 1e-3)
     z = np.concatenate([(x[:3] - mean) / std, x[3:] / vn])
     W0, b0, W1, b1, W2, b2 = params
     a = np.maximum(W0 @ z + b0, 0.0)
     a = np.maximum(W1 @ a + b1, 0.0)
-    return float((W2 @ a + b2)[0]) - vn
+    out = float((W2 @ a + b2)[0])
+    if safety_margin is not None:
+        out = out * (100 - safety_margin) / 100
+    return out - vn
 
 
 # ------------------------------------------------------------------------------------------------
