@@ -28,6 +28,8 @@
  *   vboc_mpc_solve_batch   <- one OCPtriplependulumHardTerm.OCP_solve(x0, x_sol_guess, u_sol_guess) per problem:
  *                             Safe MPC with the VBOC network as terminal constraint (VBOC/Safe MPC/
  *                             triplependulum_class_vboc.py:91-240; drivers hard_terminal_constraints/3dof_sym.py)
+ *   vboc_mpc_soft_solve_batch <- one OCPtriplependulumSoftTraj.OCP_solve(...) per problem (:242-304; drivers
+ *                             soft_traj_constraints/3dof_sym.py, receiding_hard_constraints/3dof_sym.py)
  *   vboc_set_path_constraint <- model.con_h_expr + constraints.lh / uh of the Cartesian double pendulum
  *                             (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160)
  *   vboc_destroy           <- solver object destruction (acados_template __del__ -> free)
@@ -305,6 +307,25 @@ typedef struct {
   double* h_out;
 } vboc_mpc_batch_t;
 int vboc_mpc_solve_batch(vboc_handle h, const vboc_mpc_batch_t* batch, void* stream);
+
+/* The soft-constraint Safe MPC: OCPtriplependulumSoftTraj.OCP_solve(x0, x_sol_guess, u_sol_guess) (VBOC/Safe MPC/
+ * triplependulum_class_vboc.py:242-304) for every x0 of a vboc_mpc_batch_t: the row
+ * nn_decisionfunction_conservative = NN(x) (100 - safety_margin) / 100 - max(|x[2:]|, 1e-3) on EVERY stage 0..N
+ * (con_h_expr and con_h_expr_e), each soft on its lower side (idxsh / idxsh_e) with a slack s_k >= 0 costing
+ * zl_k s_k + Zl_k s_k^2 / 2 - the per-stage weights the drivers set with ocp_solver.cost_set(i, "Zl", ...)
+ * (soft_traj_constraints/3dof_sym.py:102-105, receiding_hard_constraints/3dof_sym.py:41-46); the upper side
+ * (uh = 1e6, zu = Zu = 0) is never active and kept hard.  W_b / We_b: each problem's stage weights, the receding
+ * driver's cost_set(i, "W", block_diag(Q, R)) / cost_set(N, "W", Q) (:36-40; NULL: the batch's host W / We).  Device
+ * pointers: Zl [B][N+1] (required), zl [B][N+1] (NULL = 0), W_b [B][3nq], We_b [B][2nq].  hidden > 0 required. */
+typedef struct {
+  double safety_margin;
+  const double* Zl;
+  const double* zl;
+  const double* W_b;
+  const double* We_b;
+} vboc_mpc_soft_t;
+int vboc_mpc_soft_solve_batch(vboc_handle h, const vboc_mpc_batch_t* batch, const vboc_mpc_soft_t* soft,
+                              void* stream);
 
 /* Device time of the last vboc_solve_batch* call's solver kernel in milliseconds (HIP events on
  * the call's stream) and the number of kernel launches it used. */

@@ -177,17 +177,19 @@ def test_gpu_sqp_matches_oracle(with_row):
     o = oracle.default_opts(lm=sp.lm, tol_stat=1e-6, qp_tol_stat=1e-8, max_iter=1000)
     x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, opts=o)
     assert (g["status"] == r["status"]).mean() >= 0.98, (g["status"], r["status"])
-    # The SQP-iteration bar, calibrated: on this OCP the converged iteration count moves with rounding - the oracle
-    # against ITSELF with the guess perturbed by 1e-15 (relative) agrees on 95 % (no row) / 74 % (row) of the
-    # problems, with equal status and final costs to 1e-16 (measured, round 4).  The GPU must be as close to the
-    # oracle as the oracle is to that perturbed copy of itself (5 points of slack).
-    xg2 = xg * (1 + 1e-15 * np.random.default_rng(0).standard_normal(xg.shape))
-    xg2[:, 0] = x0
-    _, _, r2, _ = oracle.mpc_solve_batch(sp, x0, xg2, ug, P, mean=MEAN, std=STD, opts=o)
-    self_agree = (r2["sqp_iter"] == r["sqp_iter"]).mean()
-    gpu_agree = (g["sqp_iter"] == r["sqp_iter"]).mean()
-    print(f"SQP-iteration agreement: GPU vs oracle {gpu_agree:.3f}, oracle vs 1e-15-perturbed oracle {self_agree:.3f}")
-    assert gpu_agree >= min(0.95, self_agree - 0.05), (gpu_agree, self_agree)
+    # SQP iterations per problem, classified instead of an agreement bar: on this OCP the converged iteration count
+    # moves with rounding (the oracle against itself with the guess perturbed by 1e-15 agrees on only 95 % / 74 % of
+    # the problems, round 4).  A problem whose iteration counts differ must have reached the same optimum: both
+    # converged (tol_stat 1e-6) with the cost to 1e-6 relative and x_N to 1e-3 - two KKT points to tol_stat 1e-6 of a
+    # problem whose QP Hessian is >= levenberg_marquardt 1e-2 differ by at most ~1e-4 - or both stopped at the cap.
+    moved = np.flatnonzero((g["sqp_iter"] != r["sqp_iter"]) & (g["status"] == r["status"]))
+    dcm = np.abs(g["cost"] - r["cost"])[moved] / np.abs(r["cost"][moved])
+    dxm = np.abs(g["x"][moved, -1] - x[moved, -1]).max(axis=1)
+    print(f"{moved.size} problems with moved SQP-iteration counts, statuses {np.unique(g['status'][moved])}, "
+          f"max rel dcost {dcm.max() if moved.size else 0:.2e}, max |dx_N| {dxm.max() if moved.size else 0:.2e}")
+    assert set(np.unique(g["status"][moved]).tolist()) <= {0, 2}
+    conv = g["status"][moved] == 0
+    assert (dcm[conv] <= 1e-6).all() and (dxm[conv] <= 1e-3).all(), (moved, dcm, dxm)
     for st_, least in ((0, 30), (2, 40)):
         both = (g["status"] == st_) & (r["status"] == st_)
         assert both.sum() >= least, (st_, both.sum())
@@ -197,10 +199,64 @@ def test_gpu_sqp_matches_oracle(with_row):
         assert np.median(dx) <= 1e-9 and dx.max() <= 2e-3, (st_, np.median(dx), dx.max())
 
 
+# Per-step lockstep of a closed loop (the drivers' simulate): the loop runs on the GPU, and every MPC step's OCP is
+# also solved by the oracle from the SAME inputs (state, shifted guesses, weights).  Each step pair is classified:
+#   same    - equal status; for status 0 the applied u_0 and the predicted states agree to STEP_TOL;
+#   cap     - a QP stopped at qp_solver_iter_max (100) - an unconverged interior-point iterate, which rounding moves
+#             freely - while the other solver's QP also needed >= 50 iterations (a QP hard for both);
+#   status  - the solvers returned different statuses for the same request;
+#   value   - anything else: a defect.
+# STEP_TOL: an RTI QP converged to qp_tol_stat 1e-8 on a Hessian >= levenberg_marquardt 1e-2 is within ~1e-6 of its
+# solution; two such solves agree to 2e-6.
+STEP_TOL = 2e-6
+
+
+def _lockstep_solve(gpu_solve, ora_solve, pairs):
+    def solve(x0, xg, ug, w=None):
+        a = gpu_solve(x0, xg, ug, w) if w is not None else gpu_solve(x0, xg, ug)
+        b = ora_solve(x0, xg, ug, w) if w is not None else ora_solve(x0, xg, ug)
+        for j in range(x0.shape[0]):
+            if a["status"][j] != b["status"][j]:
+                k = "status"
+            elif a["status"][j] != 0:
+                k = "same"
+            elif max(a["qp_iter"][j], b["qp_iter"][j]) >= 100:
+                k = "cap" if min(a["qp_iter"][j], b["qp_iter"][j]) >= 50 else "value"
+            else:
+                d = max(np.abs(a["u"][j] - b["u"][j]).max(), np.abs(a["x"][j] - b["x"][j]).max())
+                k = "same" if d <= STEP_TOL else "value"
+            pairs.append(k)
+        return a
+    return solve
+
+
+def _classify_closed_loop(pairs):
+    counts = {k: pairs.count(k) for k in ("same", "cap", "status", "value")}
+    print("closed-loop step pairs:", counts)
+    assert counts["value"] == 0, counts
+    assert counts["status"] <= max(2, len(pairs) // 100), counts   # reported and capped at 1 %
+    return counts
+
+
+def _gpu_hard_solve(ocp):
+    def solve(x0, xg, ug):
+        return ocp.solve_batch(x0, xg, ug)
+    return solve
+
+
+def _oracle_solve_q(sp, P, rti):
+    def solve(x0, xg, ug):
+        x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, rti=rti)
+        return dict(status=r["status"], x=x, u=u, qp_iter=r["qp_iter"])
+    return solve
+
+
 @pytest.mark.gpu
 def test_gpu_closed_loop_matches_oracle():
     """The Safe-MPC closed loop (simulate_batch, SQP_RTI, 60 steps) of 48 initial states at rest on the GPU drop-in
-    class against the same driver on the oracle: the same stopping step for >= 95 % of the states."""
+    class, every step's OCP also solved by the oracle from the same inputs: every step pair classified (above), no
+    'value'; QP-cap pairs reported (measured: 31 of 2 880), status pairs capped at 1 %.  (The trajectories themselves are not compared at a
+    fixed tolerance: a closed loop feeds each step's QP tolerance into the next state.)"""
     from vboc_amd.safempc import OCPtriplependulumHardTerm, simulate_batch
     from vboc_amd import lib
     P = _net()
@@ -209,17 +265,205 @@ def test_gpu_closed_loop_matches_oracle():
     xg = np.repeat(x0[:, None, :], sp.N + 1, 1)
     ocp = OCPtriplependulumHardTerm("SQP_RTI", sp.time_step, sp.tot_time, P, MEAN, STD)
     rk4 = lambda X, U: lib.rk4_host(3, sp.time_step, X, U)
-    rg, Xg, _ = simulate_batch(ocp.solve_batch, rk4, sp, x0, xg, ug, tot_steps=60)
-    ro, Xo, _ = simulate_batch(_oracle_solve(sp, P, True), _oracle_rk4(sp), sp, x0, xg, ug, tot_steps=60)
-    assert (rg == ro).mean() >= 0.95, (rg, ro)
-    same = rg == ro
-    # a closed loop feeds each step's rounding into the next OCP (and RTI QPs stopped at their iteration cap return
-    # unconverged iterates), so trajectories are compared by state: most agree to 1e-6 over all 60 steps
-    dev = np.abs(Xg[same] - Xo[same]).max(axis=(1, 2))
-    print("closed-loop max deviation per state: median %.2e, 90th pct %.2e, max %.2e" %
-          (np.median(dev), np.percentile(dev, 90), dev.max()))
-    assert np.median(dev) < 1e-6 and (dev < 1e-4).mean() >= 0.8
+    pairs = []
+    simulate_batch(_lockstep_solve(_gpu_hard_solve(ocp), _oracle_solve_q(sp, P, True), pairs), rk4, sp, x0, xg, ug,
+                   tot_steps=60)
+    _classify_closed_loop(pairs)
     # the drop-in batch-of-one call gives the batched call's result
     st = ocp.OCP_solve(x0[0], xg[0], ug[0])
     r = ocp.solve_batch(x0[:1], xg[:1], ug[:1])
     assert st == r["status"][0] and np.array_equal(ocp.ocp_solver.get(3, "x"), r["x"][0, 3])
+
+
+# ------------------------------------------------------------------------------------------------
+# OCPtriplependulumSoftTraj (:242-304): the margin-scaled row on every stage, soft lower sides
+# ------------------------------------------------------------------------------------------------
+MARGIN = 2.0
+
+
+def _soft_weights(N, kind):
+    if kind == "soft_traj":                       # soft_traj_constraints/3dof_sym.py:102-105
+        Zl = np.zeros(N + 1)
+        Zl[N] = 1e6
+        return Zl
+    return np.full(N + 1, 1e2)                    # every stage penalised (the receding driver's kind of weights)
+
+
+def test_soft_row_is_the_margin_scaled_network():
+    """The oracle's row (vboc_oracle_mpc_row) equals vboc_amd.safempc.nn_row with the safety margin:
+    nn_decisionfunction_conservative (:284-304), out * (100 - margin) / 100 - vn; margin < 0 the HardTerm row."""
+    from vboc_amd.safempc import nn_row
+    P = _net()
+    sp, x0, xg, ug = _states(16, seed=11)
+    h = oracle.mpc_row(x0, P, MEAN, STD, MARGIN)
+    h0 = oracle.mpc_row(x0, P, MEAN, STD, -1.0)
+    for i in range(16):
+        assert abs(h[i] - nn_row(P, MEAN, STD, x0[i], safety_margin=MARGIN)) < 1e-12
+        assert abs(h0[i] - nn_row(P, MEAN, STD, x0[i])) < 1e-12
+
+
+def test_soft_oracle_optimum_is_the_slsqp_optimum():
+    """The oracle's SoftTraj SQP optimum is the optimum of an independently written NLP with the slacks explicit
+    (tests/nlp_reference.py slsqp_mpc_soft): SLSQP started at the oracle's point (slacks at the rows' violations)
+    does not move and has the oracle's cost (slack penalties included), and started cold from the constant guess it
+    reaches the same cost.  The soft rows are violated at these optima (slacks > 0 on the path, where Zl = 0)."""
+    from nlp_reference import slsqp_mpc_soft
+    from vboc_amd.safempc import nn_row
+    P = _net()
+    sp, x0, xg, ug = _states(16)
+    Zl = _soft_weights(sp.N, "soft_traj")
+    x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, Zl, rti=False)
+    ok = np.flatnonzero(r["status"] == 0)
+    assert ok.size >= 6
+    for n, i in enumerate(ok[:2]):
+        X, U, S, c, _ = slsqp_mpc_soft(sp, x0[i], (x[i], u[i]), P, MEAN, STD, MARGIN, Zl)
+        assert np.abs(X - x[i]).max() < 1e-6 and abs(c - r["cost"][i]) < 1e-8 * abs(r["cost"][i]), (c, r["cost"][i])
+        hk = np.array([nn_row(P, MEAN, STD, x[i, k], safety_margin=MARGIN) for k in range(sp.N + 1)])
+        assert hk.min() < -1e-3 and S.max() > 1e-3 and -1e-2 < hk[-1] < 0.0   # path rows violated, the terminal one only
+        # slightly: Zl = 1e6 there trades the cost against an L2 penalty (a slack of ~1e-4 costs ~1e-2)
+        if n == 0:
+            X2, U2, S2, c2, _ = slsqp_mpc_soft(sp, x0[i], (xg[i], ug[i]), P, MEAN, STD, MARGIN, Zl, maxiter=1000)
+            assert abs(c2 - r["cost"][i]) < 1e-7 * abs(r["cost"][i]), (c2, r["cost"][i])
+            assert np.abs(X2 - x[i]).max() < 1e-4
+
+
+def test_soft_rows_with_zero_weights_are_free():
+    """With zl = Zl = 0 on every stage the soft rows cost nothing: the SoftTraj optimum is the unconstrained
+    (OCPtriplependulumSTD) optimum, up to the solvers' tolerances."""
+    P = _net()
+    sp, x0, xg, ug = _states(16)
+    x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, np.zeros(sp.N + 1), rti=False)
+    xs, us, rs, hs = oracle.mpc_solve_batch(sp, x0, xg, ug, None, rti=False)
+    both = (r["status"] == 0) & (rs["status"] == 0)
+    assert both.sum() >= 6
+    assert np.abs(x[both] - xs[both]).max() < 1e-4 and np.abs(r["cost"][both] - rs["cost"][both]).max() < 1e-6
+
+
+def test_soft_rti_is_one_qp():
+    P = _net()
+    sp, x0, xg, ug = _states(8)
+    for kind in ("soft_traj", "all"):
+        x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, _soft_weights(sp.N, kind))
+        assert (r["status"] == 0).all() and (r["sqp_iter"] == 1).all() and (r["qp_iter"] > 0).all()
+        assert (x[:, 0] == x0).all()
+
+
+def _fixture():
+    g = np.load(os.path.join(HERE, "golden", "mpc_drivers.npz"))
+    from vboc_amd.safempc import MpcSpec, halton_states
+    sp = MpcSpec(4e-3, 0.148)
+    x0 = halton_states(sp, int(g["test_num"]))
+    return g, sp, x0, np.repeat(x0[:, None, :], sp.N + 1, 1), np.zeros((x0.shape[0], sp.N, 3))
+
+
+def _oracle_soft_solve(sp, P, Zl_default):
+    def solve(x0, xg, ug, w=None):
+        w = w or {}
+        Zl = w.get("Zl", np.tile(Zl_default, (x0.shape[0], 1)))
+        x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, Zl, W=w.get("W"),
+                                                 We=w.get("We"), rti=True)
+        return dict(status=r["status"], x=x, u=u, qp_iter=r["qp_iter"])
+    return solve
+
+
+@pytest.mark.parametrize("kind", ["hard", "soft", "receding"])
+def test_mpc_drivers_reproduce_the_reference_simulate(kind):
+    """tests/golden/mpc_drivers.npz: the reference's own simulate(p) of hard_terminal_constraints/,
+    soft_traj_constraints/ and receiding_hard_constraints/3dof_sym.py (AST-extracted, run on the oracle,
+    tests/golden/make_mpc_golden.py).  vboc_amd.safempc.simulate_batch on the same oracle - all initial states at once
+    - reproduces every problem's stop step and every control applied to the plant, bit for bit."""
+    from vboc_amd.safempc import receding_weights, simulate_batch, soft_traj_weights
+    g, sp, x0, xg, ug = _fixture()
+    P = _net()
+    if kind == "hard":
+        solve, weights = _oracle_solve(sp, P, True), None
+    else:
+        solve = _oracle_soft_solve(sp, P, soft_traj_weights(sp.N) if kind == "soft" else np.zeros(sp.N + 1))
+        weights = receding_weights(P, MEAN, STD, MARGIN, sp.N) if kind == "receding" else None
+    log = {}
+    res, simX, _ = simulate_batch(solve, _oracle_rk4(sp), sp, x0, xg, ug, tot_steps=int(g["tot_steps"]),
+                                  weights=weights, log=log)
+    np.testing.assert_array_equal(res, g[f"{kind}_res"])
+    A = g[f"{kind}_applied"]
+    np.testing.assert_array_equal(simX[:, :A.shape[1]], np.where(np.isnan(A[..., :6]), simX[:, :A.shape[1]], A[..., :6]))
+    np.testing.assert_array_equal(log["u"], A[..., 6:])
+
+
+# ------------------------------------------------------------------------------------------------
+# GPU: vboc_mpc_soft_solve_batch (ft.h, SoftTraj) against the oracle
+# ------------------------------------------------------------------------------------------------
+def _gpu_soft(sp, P, x0, xg, ug, Zl, W=None, We=None, rti=True):
+    import torch
+    from vboc_amd import lib
+    s = lib.Solver(3, sp.N)
+    s.set_option("levenberg_marquardt", sp.lm)
+    s.set_option("nlp_solver_tol_stat", 1e-6)
+    s.set_option("qp_solver_tol_stat", 1e-8)
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device="cuda:0")
+    B = x0.shape[0]
+    soft = dict(margin=MARGIN, Zl=T(np.broadcast_to(Zl, (B, sp.N + 1))),
+                W=T(W) if W is not None else None, We=T(We) if We is not None else None)
+    out = s.mpc_solve_device(sp, T(x0), T(xg), T(ug), [T(p) for p in P], MEAN, STD, rti=rti, soft=soft)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["soft_traj", "weighted"])
+def test_gpu_soft_rti_matches_oracle(kind):
+    """OCPtriplependulumSoftTraj's SQP_RTI solve on 128 states: with the soft_traj driver's weights (Zl = 1e6 at N),
+    and with every stage penalised and per-problem stage weights (the receding driver's kind of call).  Every problem
+    classified as the closed-loop step pairs: equal status, u_0 / x to STEP_TOL when both QPs converged, QP-cap pairs
+    reported; the margin-scaled row at the results' x_N as the oracle's."""
+    P = _net()
+    sp, x0, xg, ug = _states(128, seed=5)
+    W = We = None
+    Zl = _soft_weights(sp.N, "soft_traj" if kind == "soft_traj" else "all")
+    if kind == "weighted":
+        rng = np.random.default_rng(3)
+        q0 = 1e-2 + 10 ** rng.uniform(0, 2, 128)
+        W = np.tile(np.r_[1e-4, 1e-4, 1e-4, 1e-4, 1e-4, 1e-4, 1e-4, 1e-4, 1e-4], (128, 1))
+        W[:, 0] = q0
+        We = W[:, :6].copy()
+    g = _gpu_soft(sp, P, x0, xg, ug, Zl, W, We)
+    x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, Zl, W=W, We=We, rti=True)
+    pairs = []
+    _lockstep_solve(lambda *a: dict(g), lambda *a: dict(status=r["status"], x=x, u=u, qp_iter=r["qp_iter"]),
+                    pairs)(x0, xg, ug)
+    _classify_closed_loop(pairs)
+    ok = (g["status"] == 0) & (r["status"] == 0) & (g["qp_iter"] < 100) & (r["qp_iter"] < 100)
+    assert ok.mean() >= 0.9 and np.abs(g["h"][ok] - h[ok]).max() < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["hard", "soft", "receding"])
+def test_gpu_mpc_drivers_lockstep(kind):
+    """The three Safe-MPC drivers' closed loops (tests/golden/mpc_drivers.npz initial states, 100 steps) on the GPU
+    drop-in classes, every step's OCP also solved by the oracle from the same inputs and classified (no 'value');
+    the problems whose every step pair is 'same' and whose GPU loop ended at the fixture's step are counted and
+    printed beside the fixture comparison of their applied controls."""
+    from vboc_amd import lib
+    from vboc_amd.safempc import (OCPtriplependulumHardTerm, OCPtriplependulumSoftTraj, receding_weights,
+                                  simulate_batch, soft_traj_weights)
+    g, sp, x0, xg, ug = _fixture()
+    P = _net()
+    rk4 = lambda X, U: lib.rk4_host(3, sp.time_step, X, U)
+    if kind == "hard":
+        ocp = OCPtriplependulumHardTerm("SQP_RTI", sp.time_step, sp.tot_time, P, MEAN, STD)
+        gs, os_, weights = _gpu_hard_solve(ocp), _oracle_solve_q(sp, P, True), None
+    else:
+        ocp = OCPtriplependulumSoftTraj("SQP_RTI", sp.time_step, sp.tot_time, P, MEAN, STD, MARGIN)
+        if kind == "soft":   # the soft_traj driver's main block (:102-105)
+            for i in range(1, sp.N):
+                ocp.ocp_solver.cost_set(i, "Zl", 0 * np.ones((1,)))
+            ocp.ocp_solver.cost_set(sp.N, "Zl", 1e6 * np.ones((1,)))
+        gs = lambda x0_, xg_, ug_, w=None: ocp.solve_batch(x0_, xg_, ug_, w)
+        os_ = _oracle_soft_solve(sp, P, soft_traj_weights(sp.N) if kind == "soft" else np.zeros(sp.N + 1))
+        weights = receding_weights(P, MEAN, STD, MARGIN, sp.N) if kind == "receding" else None
+    pairs, log = [], {}
+    res, _, _ = simulate_batch(_lockstep_solve(gs, os_, pairs), rk4, sp, x0, xg, ug, tot_steps=int(g["tot_steps"]),
+                               weights=weights, log=log)
+    _classify_closed_loop(pairs)
+    dev = np.nanmax(np.abs(log["u"] - g[f"{kind}_applied"][..., 6:]), axis=(1, 2))
+    print(f"{kind}: stop steps as the fixture {(res == g[kind + '_res']).sum()}/{res.size}; applied controls vs the "
+          f"fixture: median max |du| {np.median(dev):.2e}, {(dev < 1e-6).sum()} problems within 1e-6")

@@ -36,7 +36,17 @@ struct FtL {
                        B = A + NX * NX, BD = B + NX * NU, LB = BD + NX, UB = LB + NZ, DZ = UB + NZ, QL = DZ + NZ,
                        QU = QL + NZ, E0 = QU + NZ, H = E0 + NX, G = H + NZ, D = G + NZ, DAFF = D + NZ, K = DAFF + NZ,
                        KF = K + NU * NX, LR = KF + NU, M = LR + NZ * NZ, Y = M + NZ * NX, PE = Y + NZ * NX,
-                       QPI = PE + NX, F0 = QPI + NX, REC = F0 + NX * NZ;
+                       QPI = PE + NX, F0 = QPI + NX;
+  // the Safe-MPC NN row of the stage (HardTerm: stage N; SoftTraj: every stage; the oracle's fstage_t row fields):
+  // value, gradient, the QP slacks / duals of both sides, their affine directions, residual starts, the NLP
+  // multipliers; a soft lower side's slack (QP value, dual, affine directions), its NLP iterate / multiplier and weights
+  // zl, Zl; the factorisation weight sigma, the slack elimination b, W; the combined directions; lh - h, uh - h
+  static constexpr int RV = F0 + NX * NZ, RG = RV + 1, RTL = RG + NX, RTU = RTL + 1, RQL = RTU + 1, RQU = RQL + 1,
+                       RR0L = RQU + 1, RR0U = RR0L + 1, RATL = RR0U + 1, RATU = RATL + 1, RAQL = RATU + 1,
+                       RAQU = RAQL + 1, RLL = RAQU + 1, RLU = RLL + 1, RS = RLU + 1, RQS = RS + 1, RAS = RQS + 1,
+                       RAQS = RAS + 1, RSL = RAQS + 1, RLSL = RSL + 1, RZL = RLSL + 1, RZ2 = RZL + 1, RSIG = RZ2 + 1,
+                       RB = RSIG + 1, RW = RB + 1, RDTL = RW + 1, RDTU = RDTL + 1, RDQL = RDTU + 1, RDQU = RDQL + 1,
+                       RDS = RDQU + 1, RDQS = RDS + 1, RL = RDQS + 1, RU = RL + 1, REC = RU + 1;
   static constexpr long long region_doubles(int nmax) { return (long long)REC * (nmax + 1); }
 };
 
@@ -45,27 +55,32 @@ struct FtL {
 // (weights wq on [x; u], we at N, stage costs times cs), the dt column pinned by x_0, the terminal row
 // lh <= NN(x_N) - max(|x_N[2:]|, 1e-3) <= uh (NeuralNetDIR(2 nq, hid, 1); W1T = W1 transposed, for coalesced loads),
 // and SQP_RTI.  on == 0: the free-time OCP above, unchanged.
+// soft == 1: OCPtriplependulumSoftTraj (triplependulum_class_vboc.py:242-304): the row scaled by sm / 100
+// (sm = 100 - safety_margin) on every stage 0..N, soft lower sides with the per-problem per-stage slack weights zl / Zl
+// [B][N + 1] (oracle/vboc_oracle_ft.c header: the slack eliminated per stage); Wb / Web [B][3 nq] / [B][2 nq]: per-problem
+// stage weights (the receding driver's cost_set(i, "W")), nullptr = wq / we
 constexpr int FT_NN_MAX = 512;
 struct MpcArgs {
-  int on, rti, hid;
-  double wq[10], yr[10], we[7], yre[7], cs;
+  int on, rti, hid, soft;
+  double wq[10], yr[10], we[7], yre[7], cs, sm;
   const double *W0, *b0, *W1, *W1T, *b1, *W2, *b2;
   double mean, std, lh, uh;
+  const double *zl, *Zl, *Wb, *Web;
   double* hrow;   // [B] h(x_N) of each result (nullptr: not written)
 };
 
-template <int NQ>
+// MP: the Safe-MPC instantiation (k_ft<3, true>); the free-time pendulum solver carries no network buffers
+template <int NQ, bool MP>
 struct FtShared {
-  static constexpr int NX = FtL<NQ>::NX, NU = FtL<NQ>::NU;
+  static constexpr int NX = FtL<NQ>::NX, NU = FtL<NQ>::NU, NNB = MP ? FT_NN_MAX : 1;
   int N, nf0, ne, pid, bad;
   int f0[NX], ei[NX], fix[NX];
   double ev[NX], c0[NX], cp[NX], x0lb[NX], x0ub[NX], xlb[NX], xub[NX], xNlb[NX], xNub[NX], ulb[NU], uub[NU];
   double tnu[NX], wnu[NX], qnu[NX], nun[NX], S[NX * NX], lin_e[NX];
   double wbnd, rs;
   int qp_fail;
-  // Safe-MPC terminal row: value, gradient, QP slacks / duals, their affine directions, the NLP multipliers
-  double hv, hg[NX], hL, hU, htl, htu, hql, hqu, hr0l, hr0u, hatl, hatu, haql, haqu, hll, hlu;
-  double nn1[FT_NN_MAX], nn2[FT_NN_MAX];   // hidden activations / backward weights of the row's network
+  double wq[NX + NU], we[NX];              // this problem's tracking weights (MpcArgs wq / we or Wb / Web)
+  double nn1[NNB], nn2[NNB];               // hidden activations / backward weights of the row's network
 };
 
 __device__ __forceinline__ double ft_wmax(double v) {
@@ -175,17 +190,17 @@ __device__ __forceinline__ void ft_chol_solve(const double* L, int m, double* b)
   }
 }
 
-template <int NQ>
+template <int NQ, bool MP = false>
 struct Ft {
   using L = FtL<NQ>;
   static constexpr int NX = L::NX, NU = L::NU, NZ = L::NZ, N2 = 2 * NQ;
-  FtShared<NQ>& sh;
+  FtShared<NQ, MP>& sh;
   double* g;     // this workgroup's stage records
   const Opts& o;
   int t;
   const MpcArgs& mp;
 
-  __device__ Ft(FtShared<NQ>& s_, double* g_, const Opts& o_, int t_, const MpcArgs& mp_)
+  __device__ Ft(FtShared<NQ, MP>& s_, double* g_, const Opts& o_, int t_, const MpcArgs& mp_)
       : sh(s_), g(g_), o(o_), t(t_), mp(mp_) {}
 
   // ---- Safe-MPC terminal row (all lanes; x uniform): h(x) = NN(z(x)) - vn(x), grad (NX, uniform) if asked ----
@@ -196,6 +211,7 @@ struct Ft {
   // once per SQP iteration and line-search trial), so the row and its gradient are bit-identical to the oracle's.
   __device__ double nn_row(const double* x, double* grad) {
 #pragma clang fp contract(off)
+    static_assert(MP, "the network row belongs to the Safe-MPC instantiation");
     const int H = mp.hid;
     double ss = 0.0;
     for (int j = 2; j < N2; ++j) ss += x[j] * x[j];    // norm_2(x[2:]): theta_3 included, as the reference
@@ -233,6 +249,7 @@ struct Ft {
       if (a2 > 0.0) out += mp.W2[i] * a2;
     }
     out += mp.b2[0];
+    if (mp.soft) out = out * mp.sm / 100.0;   // nn_decisionfunction_conservative: out*(100-safety_margin)/100 (:301)
     if (grad) {
       __syncthreads();
       for (int i = t; i < H; i += 64) sh.nn2[i] = sh.nn2[i] > 0.0 ? mp.W2[i] : 0.0;   // W2 [a2 > 0]
@@ -257,6 +274,7 @@ struct Ft {
         const double gi = sh.nn2[i];
         for (int q = 0; q < N2; ++q) gz[q] += gi * mp.W0[i * N2 + q];
       }
+      if (mp.soft) for (int q = 0; q < N2; ++q) gz[q] = gz[q] * mp.sm / 100.0;
       double dvn[N2];
       for (int j = 0; j < N2; ++j) dvn[j] = (nrm > 1e-3 && j >= 2) ? x[j] / nrm : 0.0;
       for (int j = 0; j < N2; ++j) {
@@ -269,19 +287,80 @@ struct Ft {
     return out - vn;
   }
   __device__ __forceinline__ double hq(int k, int i) const {   // Gauss-Newton Hessian diagonal of the tracking cost
-    if (!mp.on) return 0.0;
-    if (k == sh.N) return mp.we[i];
-    return mp.cs * mp.wq[k == 0 ? (i < sh.nf0 ? sh.f0[i] : NX + (i - sh.nf0)) : i];
+    if (!MP) return 0.0;
+    if (k == sh.N) return sh.we[i];
+    return mp.cs * sh.wq[k == 0 ? (i < sh.nf0 ? sh.f0[i] : NX + (i - sh.nf0)) : i];
   }
   __device__ __forceinline__ double track(int k, const double* x, const double* u) const {
     double c = 0.0;
     if (k == sh.N) {
-      for (int i = 0; i < NX; ++i) { const double d = x[i] - mp.yre[i]; c += mp.we[i] * d * d; }
+      for (int i = 0; i < NX; ++i) { const double d = x[i] - mp.yre[i]; c += sh.we[i] * d * d; }
       return 0.5 * c;
     }
-    for (int i = 0; i < NX; ++i) { const double d = x[i] - mp.yr[i]; c += mp.wq[i] * d * d; }
-    for (int a = 0; a < NU; ++a) { const double d = u[a] - mp.yr[NX + a]; c += mp.wq[NX + a] * d * d; }
+    for (int i = 0; i < NX; ++i) { const double d = x[i] - mp.yr[i]; c += sh.wq[i] * d * d; }
+    for (int a = 0; a < NU; ++a) { const double d = u[a] - mp.yr[NX + a]; c += sh.wq[NX + a] * d * d; }
     return 0.5 * mp.cs * c;
+  }
+  // ---- the Safe-MPC rows (oracle/vboc_oracle_ft.c frow_*: the same expressions) ----------------------------
+  __device__ __forceinline__ bool row_at(int k) const { return MP && mp.hid > 0 && (mp.soft || k == sh.N); }
+  // c'd of stage k's row over the stage vector at record offset `off` (its state components; stage 0: the free ones)
+  __device__ __forceinline__ double row_dot(const double* r, int k, int off) const {
+    double v = 0.0;
+    if (k == 0) {
+      for (int j = 0; j < sh.nf0; ++j) v += r[L::RG + sh.f0[j]] * r[off + j];
+      return v;
+    }
+    for (int i = 0; i < NX; ++i) v += r[L::RG + i] * r[off + i];
+    return v;
+  }
+  __device__ __forceinline__ void row_addgrad(double* r, int k, double v) const {
+    if (k == 0) {
+      for (int j = 0; j < sh.nf0; ++j) r[L::G + j] += r[L::RG + sh.f0[j]] * v;
+      return;
+    }
+    for (int i = 0; i < NX; ++i) r[L::G + i] += r[L::RG + i] * v;
+  }
+  __device__ __forceinline__ static void row_rc(const double* r, double smu, double& rcl, double& rcu, double& rcs) {
+    rcl = smu - r[L::RTL] * r[L::RQL] - r[L::RATL] * r[L::RAQL];
+    rcu = smu - r[L::RTU] * r[L::RQU] - r[L::RATU] * r[L::RAQU];
+    rcs = smu - r[L::RS] * r[L::RQS] - r[L::RAS] * r[L::RAQS];
+  }
+  // the row's gradient term for the targets rc (pred: the predictor's form) and (pred) its factorisation weight
+  __device__ __forceinline__ double row_gamma(double* r, double rs, double rcl, double rcu, double rcs, bool pred) const {
+    const double rl = rs * r[L::RR0L], ru = rs * r[L::RR0U];
+    const double tl = r[L::RTL], tu = r[L::RTU], ql = r[L::RQL], qu = r[L::RQU];
+    double gam;
+    if (pred) gam = ql * rl / tl - qu * ru / tu;
+    else gam = -ql + qu - (rcl - ql * rl) / tl + (rcu - qu * ru) / tu;
+    if (mp.soft) {
+      const double sv = r[L::RS], qs = r[L::RQS], Z = r[L::RZ2];
+      const double Sl = ql / tl, Ss = qs / sv, W = Z + Sl + Ss;
+      const double b = -(Z * sv + r[L::RZL] - ql - qs) + rcl / tl + rcs / sv - Sl * rl;
+      r[L::RW] = W;
+      r[L::RB] = b;
+      gam += Sl * b / W;
+      if (pred) r[L::RSIG] = qu / tu + Sl * (Z + Ss) / W;
+    } else if (pred) {
+      r[L::RSIG] = ql / tl + qu / tu;
+    }
+    return gam;
+  }
+  __device__ __forceinline__ void row_dirs(const double* r, double cd, double rs, double rcl, double rcu, double rcs,
+                                           double& dtl, double& dtu, double& dql, double& dqu, double& ds,
+                                           double& dqs) const {
+    const double rl = rs * r[L::RR0L], ru = rs * r[L::RR0U];
+    ds = 0.0;
+    dqs = 0.0;
+    if (mp.soft) {
+      ds = (r[L::RB] - r[L::RQL] / r[L::RTL] * cd) / r[L::RW];
+      dtl = cd + ds + rl;
+    } else {
+      dtl = cd + rl;
+    }
+    dtu = ru - cd;
+    dql = (rcl - r[L::RQL] * dtl) / r[L::RTL];
+    dqu = (rcu - r[L::RQU] * dtu) / r[L::RTU];
+    if (mp.soft) dqs = (rcs - r[L::RQS] * ds) / r[L::RS];
   }
 
   __device__ __forceinline__ double* rec(int k) const { return g + (long long)k * L::REC; }
@@ -292,25 +371,25 @@ struct Ft {
     if (k == 0) {
       if (i < sh.nf0) { const int c = sh.f0[i]; v = r[L::X + c]; lb = sh.x0lb[c]; ub = sh.x0ub[c]; }
       else { v = r[L::U + i - sh.nf0]; lb = sh.ulb[i - sh.nf0]; ub = sh.uub[i - sh.nf0]; }
-      return !(isinf(lb) && isinf(ub));
+      return !(MP && isinf(lb) && isinf(ub));
     }
     if (k == sh.N) {
       v = r[L::X + i];
       if (sh.fix[i]) { lb = -INFINITY; ub = INFINITY; return false; }
       lb = sh.xNlb[i]; ub = sh.xNub[i];
-      return !(isinf(lb) && isinf(ub));
+      return !(MP && isinf(lb) && isinf(ub));
     }
     if (i < NX) { v = r[L::X + i]; lb = sh.xlb[i]; ub = sh.xub[i]; }
     else { v = r[L::U + i - NX]; lb = sh.ulb[i - NX]; ub = sh.uub[i - NX]; }
-    return !(isinf(lb) && isinf(ub));   // a free component: the Safe-MPC model's pinned dt
+    return !(MP && isinf(lb) && isinf(ub));   // a free component: the Safe-MPC model's pinned dt
   }
   __device__ __forceinline__ double grad(int k, int i) const {
-    if (mp.on) {   // W ([x; u] - yref) at the current iterate
+    if (MP) {   // W ([x; u] - yref) at the current iterate
       double v, lb, ub;
       (void)comp(k, i, v, lb, ub);
-      if (k == sh.N) return mp.we[i] * (v - mp.yre[i]);
+      if (k == sh.N) return sh.we[i] * (v - mp.yre[i]);
       const int w = k == 0 ? (i < sh.nf0 ? sh.f0[i] : NX + (i - sh.nf0)) : i;
-      return mp.cs * mp.wq[w] * (v - mp.yr[w]);
+      return mp.cs * sh.wq[w] * (v - mp.yr[w]);
     }
     if (k == 0) return i < sh.nf0 ? sh.c0[sh.f0[i]] : 0.0;
     if (k == sh.N) return 0.0;
@@ -343,9 +422,16 @@ struct Ft {
       sh.c0[2 * NQ] = p[NQ];
       sh.cp[2 * NQ] = p[NQ];
       sh.wbnd = 0.0;
-      sh.hll = sh.hlu = 0.0;
-      sh.hv = 0.0;
-      for (int i = 0; i < NX; ++i) sh.hg[i] = 0.0;
+      if (MP) {   // this problem's tracking weights
+        for (int i = 0; i < NX + NU; ++i) sh.wq[i] = mp.wq[i];
+        for (int i = 0; i < NX; ++i) sh.we[i] = mp.we[i];
+        if (mp.Wb) {   // [3 nq]: x (2 nq, the pinned dt column carries none) then u
+          for (int i = 0; i < N2; ++i) sh.wq[i] = mp.Wb[(long long)pid * (N2 + NU) + i];
+          for (int a = 0; a < NU; ++a) sh.wq[NX + a] = mp.Wb[(long long)pid * (N2 + NU) + N2 + a];
+        }
+        if (mp.Web)
+          for (int i = 0; i < N2; ++i) sh.we[i] = mp.Web[(long long)pid * N2 + i];
+      }
       sh.bad = bad;
     }
     __syncthreads();
@@ -360,15 +446,29 @@ struct Ft {
       for (int i = 0; i < NX; ++i) { r[L::PI + i] = 0.0; r[L::WPI + i] = 0.0; }
       if (k < N)
         for (int a = 0; a < NU; ++a) r[L::U + a] = ug[(long long)k * NU + a];
+      if (MP) {   // the rows' NLP multipliers and slacks start at 0 (ACADOS' nlp_out at creation); their weights
+        r[L::RLL] = r[L::RLU] = r[L::RSL] = r[L::RLSL] = 0.0;
+        r[L::RZL] = (mp.soft && mp.zl) ? mp.zl[(long long)pid * (N + 1) + k] : 0.0;
+        r[L::RZ2] = (mp.soft && mp.Zl) ? mp.Zl[(long long)pid * (N + 1) + k] : 0.0;
+      }
     }
     __syncthreads();
   }
 
   __device__ double cost() const {
     double c = 0.0;
-    if (mp.on) {
+    if (MP) {
       for (int k = t; k <= sh.N; k += 64) c += track(k, rec(k) + L::X, rec(k) + L::U);
-      return ft_wsum(c);
+      c = ft_wsum(c);
+      if (mp.soft) {   // the slacks' penalties (ACADOS' get_cost includes them), in stage order
+        double sc = 0.0;
+        for (int k = 0; k <= sh.N; ++k) {
+          const double* r = rec(k);
+          sc += r[L::RZL] * r[L::RSL] + 0.5 * r[L::RZ2] * r[L::RSL] * r[L::RSL];
+        }
+        c += sc;
+      }
+      return c;
     }
     for (int k = t; k < sh.N; k += 64) {
       const double* r = rec(k);
@@ -388,12 +488,14 @@ struct Ft {
         for (int a = 0; a < NU; ++a) uo[(long long)k * NU + a] = r[L::U + a];
     }
     const double c = cost();
-    if (mp.on && mp.hrow) {
-      __syncthreads();
-      double xN[NX];
-      for (int i = 0; i < NX; ++i) xN[i] = rec(N)[L::X + i];
-      const double hv = mp.hid > 0 ? nn_row(xN, nullptr) : 0.0;
-      if (t == 0) mp.hrow[pid] = hv;
+    if constexpr (MP) {
+      if (mp.hrow) {
+        __syncthreads();
+        double xN[NX];
+        for (int i = 0; i < NX; ++i) xN[i] = rec(N)[L::X + i];
+        const double hv = mp.hid > 0 ? nn_row(xN, nullptr) : 0.0;
+        if (t == 0) mp.hrow[pid] = hv;
+      }
     }
     if (t == 0) {
       in.status[pid] = status;
@@ -420,15 +522,19 @@ struct Ft {
       }
     }
     __syncthreads();
-    if (mp.hid > 0) {   // the terminal row's value and gradient at x_N
-      double xN[NX], gr[NX];
-      for (int i = 0; i < NX; ++i) xN[i] = rec(N)[L::X + i];
-      const double hv = nn_row(xN, gr);
-      if (t == 0) {
-        sh.hv = hv;
-        for (int i = 0; i < NX; ++i) sh.hg[i] = gr[i];
+    if constexpr (MP) {
+      if (mp.hid > 0) {   // the rows' values and gradients (HardTerm: x_N only; SoftTraj: every stage)
+        for (int k = mp.soft ? 0 : N; k <= N; ++k) {
+          double xk[NX], gr[NX];
+          for (int i = 0; i < NX; ++i) xk[i] = rec(k)[L::X + i];
+          const double hv = nn_row(xk, gr);
+          if (t == 0) {
+            rec(k)[L::RV] = hv;
+            for (int i = 0; i < NX; ++i) rec(k)[L::RG + i] = gr[i];
+          }
+        }
+        __syncthreads();
       }
-      __syncthreads();
     }
   }
 
@@ -456,7 +562,10 @@ struct Ft {
         } else {
           gr -= rp[L::PI + i];
           for (int j = 0; j < sh.ne; ++j) if (sh.ei[j] == i) gr += sh.tnu[j];
-          if (mp.hid > 0) gr += sh.hg[i] * (sh.hlu - sh.hll);
+        }
+        if (row_at(k)) {   // the row's term on the state components of the stage's variables
+          const int xi = k == 0 ? (i < sh.nf0 ? sh.f0[i] : -1) : (i < NX ? i : -1);
+          if (xi >= 0) gr += r[L::RG + xi] * (r[L::RLU] - r[L::RLL]);
         }
         st = fmax(st, fabs(gr));
         if (boxed) {
@@ -465,9 +574,17 @@ struct Ft {
         }
       }
     }
-    if (mp.hid > 0 && t == 0) {
-      in = fmax(in, fmax(mp.lh - sh.hv, sh.hv - mp.uh));
-      cp = fmax(cp, fmax(fabs(sh.hll * (sh.hv - mp.lh)), fabs(sh.hlu * (mp.uh - sh.hv))));
+    for (int k = t; k <= N; k += 64) {
+      if (!row_at(k)) continue;
+      const double* r = rec(k);
+      const double hv = r[L::RV], sl = mp.soft ? r[L::RSL] : 0.0;
+      in = fmax(in, fmax(mp.lh - (hv + sl), hv - mp.uh));
+      cp = fmax(cp, fmax(fabs(r[L::RLL] * (hv + sl - mp.lh)), fabs(r[L::RLU] * (mp.uh - hv))));
+      if (mp.soft) {   // the slack: s >= 0, its stationarity Zl s + zl - lambda_row - lambda_s = 0
+        in = fmax(in, -sl);
+        cp = fmax(cp, fabs(r[L::RLSL] * sl));
+        st = fmax(st, fabs(r[L::RZ2] * sl + r[L::RZL] - r[L::RLL] - r[L::RLSL]));
+      }
     }
     rstat = ft_wmax(st); req = ft_wmax(eq); rineq = ft_wmax(in); rcomp = ft_wmax(cp);
   }
@@ -488,10 +605,10 @@ struct Ft {
     const double* rN = rec(N);
     for (int i = 0; i < NX * NX; ++i) { Pm[i] = 0.0; Pi[i] = 0.0; }
     for (int i = 0; i < NX; ++i) { Pm[i * NX + i] = rN[L::H + i]; p[i] = rN[L::G + i]; lin[i] = 0.0; }
-    if (mp.hid > 0) {   // the terminal row's barrier: sigma c c'
-      const double sig = sh.hql / sh.htl + sh.hqu / sh.htu;
+    if (row_at(N)) {   // the terminal row's barrier: sigma c c'
+      const double sig = rN[L::RSIG];
       for (int i = 0; i < NX; ++i)
-        for (int j = 0; j < NX; ++j) Pm[i * NX + j] += sig * sh.hg[i] * sh.hg[j];
+        for (int j = 0; j < NX; ++j) Pm[i * NX + j] += sig * rN[L::RG + i] * rN[L::RG + j];
     }
     for (int j = 0; j < ne; ++j) Pi[sh.ei[j] * ne + j] = 1.0;
     if (factor) {
@@ -575,9 +692,11 @@ struct Ft {
               for (int q = 0; q < NX; ++q) s += r[L::A + q * NX + i] * Pm[q * NX + j];
               AP[i * NX + j] = s;
             }
+          const bool rk = row_at(k);
           for (int i = 0; i < NX; ++i)
             for (int j = 0; j < NX; ++j) {
               double s = (i == j) ? r[L::H + i] : 0.0;
+              if (rk) s += r[L::RSIG] * r[L::RG + i] * r[L::RG + j];   // a path row's barrier: sigma c c'
               for (int q = 0; q < NX; ++q) s += AP[i * NX + q] * r[L::A + q * NX + j];
               for (int a = 0; a < NU; ++a) s += Sux[a * NX + i] * r[L::K + a * NX + j];
               Pn[i * NX + j] = s;
@@ -678,19 +797,6 @@ struct Ft {
     return true;
   }
 
-  // Newton directions of the terminal row's slacks / duals (oracle frow_dir; lane 0, after newton())
-  __device__ void row_dir(double rs, double smu, double& dtl, double& dtu, double& dql, double& dqu) const {
-    const double* rN = rec(sh.N);
-    double cd = 0.0;
-    for (int i = 0; i < NX; ++i) cd += sh.hg[i] * rN[L::D + i];
-    const double rl = rs * sh.hr0l, ru = rs * sh.hr0u;
-    const double rcl = smu - sh.htl * sh.hql - sh.hatl * sh.haql, rcu = smu - sh.htu * sh.hqu - sh.hatu * sh.haqu;
-    dtl = cd + rl;
-    dtu = ru - cd;
-    dql = (rcl - sh.hql * dtl) / sh.htl;
-    dqu = (rcu - sh.hqu * dtu) / sh.htu;
-  }
-
   // ---- interior-point QP ------------------------------------------------------------------------
   // returns 0 converged, 1 max-iter, -1 failure; iterations in qit
   __device__ int qp(int& qit) {
@@ -714,28 +820,32 @@ struct Ft {
         r[L::QU + i] = o.mu0 / (Up - z0);
         nb += 2.0;
       }
-    }
-    double nbox = ft_wsum(nb);
-    __syncthreads();
-    const bool row = mp.hid > 0;
-    if (row) {   // terminal row: slacks from the initial c'dz_N, clipped to ipm_push (infeasible start)
-      if (t == 0) {
-        const double* rN = rec(N);
-        double gd = 0.0;
-        for (int i = 0; i < NX; ++i) gd += sh.hg[i] * rN[L::DZ + i];
-        sh.hL = mp.lh - sh.hv;
-        sh.hU = mp.uh - sh.hv;
-        sh.htl = fmax(gd - sh.hL, o.push);
-        sh.htu = fmax(sh.hU - gd, o.push);
-        sh.hql = o.mu0 / sh.htl;
-        sh.hqu = o.mu0 / sh.htu;
-        sh.hr0l = gd - sh.hL - sh.htl;
-        sh.hr0u = sh.hU - gd - sh.htu;
-        sh.hatl = sh.hatu = sh.haql = sh.haqu = 0.0;
+      if (row_at(k)) {
+        // the row: slacks from the initial c'dz, clipped to ipm_push (infeasible start); a soft row's slack starts
+        // at the row's violation + ipm_push, so its lower side starts feasible
+        const double gd = row_dot(r, k, L::DZ);
+        r[L::RL] = mp.lh - r[L::RV];
+        r[L::RU] = mp.uh - r[L::RV];
+        double gs = gd;
+        r[L::RS] = r[L::RQS] = r[L::RAS] = r[L::RAQS] = 0.0;
+        if (mp.soft) {
+          r[L::RS] = fmax(r[L::RL] - gd, 0.0) + o.push;
+          r[L::RQS] = o.mu0 / r[L::RS];
+          gs = gd + r[L::RS];
+          nb += 1.0;
+        }
+        r[L::RTL] = fmax(gs - r[L::RL], o.push);
+        r[L::RTU] = fmax(r[L::RU] - gd, o.push);
+        r[L::RQL] = o.mu0 / r[L::RTL];
+        r[L::RQU] = o.mu0 / r[L::RTU];
+        r[L::RR0L] = gs - r[L::RL] - r[L::RTL];
+        r[L::RR0U] = r[L::RU] - gd - r[L::RTU];
+        r[L::RATL] = r[L::RATU] = r[L::RAQL] = r[L::RAQU] = 0.0;
+        nb += 2.0;
       }
-      nbox += 2.0;
-      __syncthreads();
     }
+    const double nbox = ft_wsum(nb);
+    __syncthreads();
     double e00 = 0.0, rd0 = 0.0;
     for (int k = t; k <= N; k += 64) {
       double* r = rec(k);
@@ -759,11 +869,17 @@ struct Ft {
           e00 = fmax(e00, fabs(s));
         }
       }
-      for (int i = 0; i < nz(k); ++i)
+      const bool rk = row_at(k);
+      for (int i = 0; i < nz(k); ++i) {
+        const int xi = k == 0 ? (i < sh.nf0 ? sh.f0[i] : -1) : (i < NX ? i : -1);
         rd0 = fmax(rd0, fabs((rho + hq(k, i)) * r[L::DZ + i] + grad(k, i) - r[L::QL + i] + r[L::QU + i] +
-                             ((row && k == N) ? sh.hg[i] * (sh.hqu - sh.hql) : 0.0)));
+                             ((rk && xi >= 0) ? r[L::RG + xi] * (r[L::RQU] - r[L::RQL]) : 0.0)));
+      }
+      if (rk) {
+        e00 = fmax(e00, fmax(fabs(r[L::RR0L]), fabs(r[L::RR0U])));
+        if (mp.soft) rd0 = fmax(rd0, fabs(r[L::RZ2] * r[L::RS] + r[L::RZL] - r[L::RQL] - r[L::RQS]));
+      }
     }
-    if (row && t == 0) e00 = fmax(e00, fmax(fabs(sh.hr0l), fabs(sh.hr0u)));
     e00 = ft_wmax(e00);
     rd0 = ft_wmax(rd0);
     if (t == 0) {
@@ -780,8 +896,11 @@ struct Ft {
           if (!isfinite(r[L::LB + i])) continue;
           mu += (r[L::DZ + i] - r[L::LB + i]) * r[L::QL + i] + (r[L::UB + i] - r[L::DZ + i]) * r[L::QU + i];
         }
+        if (row_at(k)) {
+          mu += r[L::RTL] * r[L::RQL] + r[L::RTU] * r[L::RQU];
+          if (mp.soft) mu += r[L::RS] * r[L::RQS];
+        }
       }
-      if (row && t == 0) mu += sh.htl * sh.hql + sh.htu * sh.hqu;
       mu = ft_wsum(mu) / nbox;
       if (!isfinite(mu)) { status = -1; break; }
       const double rs = sh.rs;
@@ -797,14 +916,14 @@ struct Ft {
             Hh += r[L::QL + i] / (r[L::DZ + i] - r[L::LB + i]) + r[L::QU + i] / (r[L::UB + i] - r[L::DZ + i]);
           r[L::H + i] = Hh; r[L::G + i] = gg;
         }
+        if (row_at(k)) {   // the row's predictor term c gamma in the stage gradient
+          r[L::RATL] = r[L::RATU] = r[L::RAQL] = r[L::RAQU] = r[L::RAS] = r[L::RAQS] = 0.0;
+          double rcl, rcu, rcs;
+          row_rc(r, 0.0, rcl, rcu, rcs);
+          row_addgrad(r, k, row_gamma(r, rs, rcl, rcu, rcs, true));
+        }
       }
       __syncthreads();
-      if (row && t == 0) {   // the row's predictor term c gamma in the terminal gradient
-        sh.hatl = sh.hatu = sh.haql = sh.haqu = 0.0;
-        const double gam = sh.hql * (rs * sh.hr0l) / sh.htl - sh.hqu * (rs * sh.hr0u) / sh.htu;
-        double* rN = rec(N);
-        for (int i = 0; i < NX; ++i) rN[L::G + i] += sh.hg[i] * gam;
-      }
       if (!newton(true)) { status = -1; break; }
       FtRatio ma{1.0, 1.0};
       for (int k = t; k <= N; k += 64) {
@@ -818,12 +937,14 @@ struct Ft {
           const double dll = -ql - ql * d / tl, dlu = -qu + qu * d / tu;
           ma.add(tl, d); ma.add(tu, -d); ma.add(ql, dll); ma.add(qu, dlu);
         }
-      }
-      if (row && t == 0) {
-        double dtl, dtu, dql, dqu;
-        row_dir(rs, 0.0, dtl, dtu, dql, dqu);
-        sh.hatl = dtl; sh.hatu = dtu; sh.haql = dql; sh.haqu = dqu;
-        ma.add(sh.htl, dtl); ma.add(sh.htu, dtu); ma.add(sh.hql, dql); ma.add(sh.hqu, dqu);
+        if (row_at(k)) {
+          double rcl, rcu, rcs, dtl, dtu, dql, dqu, ds, dqs;
+          row_rc(r, 0.0, rcl, rcu, rcs);
+          row_dirs(r, row_dot(r, k, L::D), rs, rcl, rcu, rcs, dtl, dtu, dql, dqu, ds, dqs);
+          r[L::RATL] = dtl; r[L::RATU] = dtu; r[L::RAQL] = dql; r[L::RAQU] = dqu; r[L::RAS] = ds; r[L::RAQS] = dqs;
+          ma.add(r[L::RTL], dtl); ma.add(r[L::RTU], dtu); ma.add(r[L::RQL], dql); ma.add(r[L::RQU], dqu);
+          if (mp.soft) { ma.add(r[L::RS], ds); ma.add(r[L::RQS], dqs); }
+        }
       }
       const double aa = ma.reduce();
       double muaff = 0.0;
@@ -836,9 +957,12 @@ struct Ft {
           const double dll = -ql - ql * d / tl, dlu = -qu + qu * d / tu;
           muaff += (tl + aa * d) * (ql + aa * dll) + (tu - aa * d) * (qu + aa * dlu);
         }
+        if (row_at(k)) {
+          muaff += (r[L::RTL] + aa * r[L::RATL]) * (r[L::RQL] + aa * r[L::RAQL]) +
+                   (r[L::RTU] + aa * r[L::RATU]) * (r[L::RQU] + aa * r[L::RAQU]);
+          if (mp.soft) muaff += (r[L::RS] + aa * r[L::RAS]) * (r[L::RQS] + aa * r[L::RAQS]);
+        }
       }
-      if (row && t == 0)
-        muaff += (sh.htl + aa * sh.hatl) * (sh.hql + aa * sh.haql) + (sh.htu + aa * sh.hatu) * (sh.hqu + aa * sh.haqu);
       muaff = ft_wsum(muaff) / nbox;
       double sig = muaff / mu;
       sig = sig * sig * sig;
@@ -855,15 +979,13 @@ struct Ft {
           const double rl = smu - tl * ql - d * dll, ru = smu - tu * qu + d * dlu;
           r[L::G + i] = (rho + hq(k, i)) * r[L::DZ + i] + grad(k, i) - ql - rl * itl + qu + ru * itu;
         }
+        if (row_at(k)) {   // the row's Mehrotra-corrected term
+          double rcl, rcu, rcs;
+          row_rc(r, smu, rcl, rcu, rcs);
+          row_addgrad(r, k, row_gamma(r, rs, rcl, rcu, rcs, false));
+        }
       }
       __syncthreads();
-      if (row && t == 0) {   // the row's Mehrotra-corrected term
-        const double rl = rs * sh.hr0l, ru = rs * sh.hr0u;
-        const double rcl = smu - sh.htl * sh.hql - sh.hatl * sh.haql, rcu = smu - sh.htu * sh.hqu - sh.hatu * sh.haqu;
-        const double gam = -sh.hql + sh.hqu - (rcl - sh.hql * rl) / sh.htl + (rcu - sh.hqu * ru) / sh.htu;
-        double* rN = rec(N);
-        for (int i = 0; i < NX; ++i) rN[L::G + i] += sh.hg[i] * gam;
-      }
       if (!newton(false)) { status = -1; break; }
       FtRatio mx{1.0, o.tau};
       for (int k = t; k <= N; k += 64) {
@@ -877,11 +999,16 @@ struct Ft {
           const double dll = (rl - ql * d) * itl, dlu = (ru + qu * d) * itu;
           mx.add(tl, d); mx.add(tu, -d); mx.add(ql, dll); mx.add(qu, dlu);
         }
-      }
-      double rdtl = 0.0, rdtu = 0.0, rdql = 0.0, rdqu = 0.0;
-      if (row && t == 0) {
-        row_dir(rs, smu, rdtl, rdtu, rdql, rdqu);
-        mx.add(sh.htl, rdtl); mx.add(sh.htu, rdtu); mx.add(sh.hql, rdql); mx.add(sh.hqu, rdqu);
+        if (row_at(k)) {
+          double* rw = rec(k);
+          double rcl, rcu, rcs;
+          row_rc(rw, smu, rcl, rcu, rcs);
+          row_dirs(rw, row_dot(rw, k, L::D), rs, rcl, rcu, rcs, rw[L::RDTL], rw[L::RDTU], rw[L::RDQL], rw[L::RDQU],
+                   rw[L::RDS], rw[L::RDQS]);
+          mx.add(rw[L::RTL], rw[L::RDTL]); mx.add(rw[L::RTU], rw[L::RDTU]);
+          mx.add(rw[L::RQL], rw[L::RDQL]); mx.add(rw[L::RQU], rw[L::RDQU]);
+          if (mp.soft) { mx.add(rw[L::RS], rw[L::RDS]); mx.add(rw[L::RQS], rw[L::RDQS]); }
+        }
       }
       const double alpha = fmin(1.0, o.tau * mx.reduce());
       for (int k = t; k <= N; k += 64) {
@@ -898,12 +1025,16 @@ struct Ft {
           }
           r[L::DZ + i] += alpha * d;
         }
+        if (row_at(k)) {
+          r[L::RTL] += alpha * r[L::RDTL]; r[L::RTU] += alpha * r[L::RDTU];
+          r[L::RQL] += alpha * r[L::RDQL]; r[L::RQU] += alpha * r[L::RDQU];
+          if (mp.soft) {
+            r[L::RS] += alpha * r[L::RDS];
+            r[L::RQS] += alpha * r[L::RDQS];
+          }
+        }
       }
       if (t == 0) {
-        if (row) {
-          sh.htl += alpha * rdtl; sh.htu += alpha * rdtu;
-          sh.hql += alpha * rdql; sh.hqu += alpha * rdqu;
-        }
         for (int j = 0; j < ne; ++j) sh.qnu[j] += alpha * (sh.nun[j] - sh.qnu[j]);
         sh.rs = rs * (1.0 - alpha);
       }
@@ -917,7 +1048,7 @@ struct Ft {
       const double* rN = rec(N);
       for (int i = 0; i < NX; ++i) {
         lam[i] = (rho + hq(N, i)) * rN[L::DZ + i] + grad(N, i) - rN[L::QL + i] + rN[L::QU + i];
-        if (row) lam[i] += sh.hg[i] * (sh.hqu - sh.hql);
+        if (row_at(N)) lam[i] += rN[L::RG + i] * (rN[L::RQU] - rN[L::RQL]);
       }
       for (int j = 0; j < ne; ++j) lam[sh.ei[j]] += sh.qnu[j];
       for (int k = N - 1; k >= 0; --k) {
@@ -927,6 +1058,7 @@ struct Ft {
         double ln[NX];
         for (int i = 0; i < NX; ++i) {
           double s = (rho + hq(k, i)) * r[L::DZ + i] + grad(k, i) - r[L::QL + i] + r[L::QU + i];
+          if (row_at(k)) s += r[L::RG + i] * (r[L::RQU] - r[L::RQL]);   // a path row's term
           for (int q = 0; q < NX; ++q) s += r[L::A + q * NX + i] * lam[q];
           ln[i] = s;
         }
@@ -983,14 +1115,27 @@ struct Ft {
         for (int j = 0; j < sh.ne; ++j) val += sh.wnu[j] * fabs(xn[sh.ei[j]] - sh.ev[j]);
       }
     }
-    double hviol = 0.0;
-    if (mp.hid > 0) {   // the terminal row's violation at the trial state, weighted like the boxes
-      double xN[NX], uN[NU];
-      state_at(N, alpha, xN, uN);
-      const double hv = nn_row(xN, nullptr);
-      hviol = fmax(0.0, mp.lh - hv) + fmax(0.0, hv - mp.uh);
+    double hviol = 0.0, hcost = 0.0;
+    if constexpr (MP) {
+      if (mp.hid > 0) {
+        // the rows' violations at the trial states, weighted like the boxes (uniform: every lane evaluates); a soft
+        // row's trial slack, its cost and its bound s >= 0
+        for (int k = mp.soft ? 0 : N; k <= N; ++k) {
+          double xk[NX], uk[NU];
+          state_at(k, alpha, xk, uk);
+          const double hv = nn_row(xk, nullptr);
+          const double* r = rec(k);
+          const double sa = mp.soft ? r[L::RSL] + alpha * (r[L::RS] - r[L::RSL]) : 0.0;
+          double v = fmax(0.0, mp.lh - hv - sa) + fmax(0.0, hv - mp.uh);
+          if (mp.soft) {
+            v += fmax(0.0, -sa);
+            hcost += r[L::RZL] * sa + 0.5 * r[L::RZ2] * sa * sa;
+          }
+          hviol += v;
+        }
+      }
     }
-    return ft_wsum(val) + sh.wbnd * (ft_wsum(viol) + hviol);
+    return ft_wsum(val) + hcost + sh.wbnd * (ft_wsum(viol) + hviol);
   }
 
   __device__ void weights() {
@@ -1004,8 +1149,11 @@ struct Ft {
           r[L::WPI + i] = a > b ? a : b;
         }
       for (int i = 0; i < nz(k); ++i) lmax = fmax(lmax, fmax(r[L::QL + i], r[L::QU + i]));
+      if (row_at(k)) {
+        lmax = fmax(lmax, fmax(r[L::RQL], r[L::RQU]));
+        if (mp.soft) lmax = fmax(lmax, r[L::RQS]);
+      }
     }
-    if (mp.hid > 0 && t == 0) lmax = fmax(lmax, fmax(sh.hql, sh.hqu));
     lmax = ft_wmax(lmax);
     if (t == 0) {
       for (int j = 0; j < sh.ne; ++j) {
@@ -1033,13 +1181,17 @@ struct Ft {
       }
       if (k < N)
         for (int i = 0; i < NX; ++i) r[L::PI + i] += alpha * (r[L::QPI + i] - r[L::PI + i]);
+      if (row_at(k)) {
+        r[L::RLL] += alpha * (r[L::RQL] - r[L::RLL]);
+        r[L::RLU] += alpha * (r[L::RQU] - r[L::RLU]);
+        if (mp.soft) {
+          r[L::RSL] += alpha * (r[L::RS] - r[L::RSL]);
+          r[L::RLSL] += alpha * (r[L::RQS] - r[L::RLSL]);
+        }
+      }
     }
     if (t == 0) {
       for (int j = 0; j < sh.ne; ++j) sh.tnu[j] += alpha * (sh.qnu[j] - sh.tnu[j]);
-      if (mp.hid > 0) {
-        sh.hll += alpha * (sh.hql - sh.hll);
-        sh.hlu += alpha * (sh.hqu - sh.hlu);
-      }
     }
     __syncthreads();
   }
@@ -1052,7 +1204,7 @@ struct Ft {
       double rstat, req, rineq, rcomp;
       residuals(rstat, req, rineq, rcomp);
       if (!isfinite(rstat) || !isfinite(req)) { status = 1; break; }
-      const bool rti = mp.on && mp.rti;
+      const bool rti = MP && mp.rti;
       if (rti && it == 1) { status = 0; break; }   // SQP_RTI: one QP and its full step
       if (!rti && rstat < o.tol_stat && req < o.tol_eq && rineq < o.tol_ineq && rcomp < o.tol_comp) { status = 0; break; }
       if (it >= o.max_iter) { status = 2; break; }
@@ -1079,13 +1231,13 @@ struct Ft {
 };
 
 // one workgroup = one wave = one problem at a time; workgroups pull problem ids until none are left
-template <int NQ>
+template <int NQ, bool MP>
 __global__ __launch_bounds__(64) void k_ft(Opts o, Inputs in, double* regions, long long region_doubles,
                                            unsigned* head, MpcArgs mp) {
-  __shared__ FtShared<NQ> sh;
+  __shared__ FtShared<NQ, MP> sh;
   __shared__ int job;
   const int t = (int)threadIdx.x;
-  Ft<NQ> F(sh, regions + (long long)blockIdx.x * region_doubles, o, t, mp);
+  Ft<NQ, MP> F(sh, regions + (long long)blockIdx.x * region_doubles, o, t, mp);
   for (;;) {
     if (t == 0) job = (int)atomicAdd(head, 1u);
     __syncthreads();

@@ -1636,7 +1636,16 @@ static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st, const Mpc
     if (hipMalloc(&h->ft_regions, need) != hipSuccess) return -1;
     h->ft_bytes = need;
   }
-  hipLaunchKernelGGL(k_ft<NQ>, dim3((unsigned)groups), dim3(64), 0, st, h->o, in, h->ft_regions, rd, h->head, mp);
+  if constexpr (NQ == 3) {
+    if (mp.on) {
+      hipLaunchKernelGGL((k_ft<NQ, true>), dim3((unsigned)groups), dim3(64), 0, st, h->o, in, h->ft_regions, rd, h->head,
+                         mp);
+      return hipGetLastError() == hipSuccess ? 0 : -2;
+    }
+  }
+  if (mp.on) return -2;   // the Safe-MPC OCP is the triple's
+  hipLaunchKernelGGL((k_ft<NQ, false>), dim3((unsigned)groups), dim3(64), 0, st, h->o, in, h->ft_regions, rd, h->head,
+                     mp);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -2271,9 +2280,25 @@ __global__ void k_transpose(int H, const double* __restrict__ a, double* __restr
     at[(e % H) * H + e / H] = a[e];
 }
 
+static int mpc_solve(vboc_handle h, const vboc_mpc_batch_t* b, const vboc_mpc_soft_t* sf, void* stream,
+                     const std::string& W);
+
 int vboc_mpc_solve_batch(vboc_handle h, const vboc_mpc_batch_t* b, void* stream) {
-  const std::string W = "vboc_mpc_solve_batch";
-  if (busy(h, "vboc_mpc_solve_batch")) return VBOC_ERR_ARG;
+  return mpc_solve(h, b, nullptr, stream, "vboc_mpc_solve_batch");
+}
+
+int vboc_mpc_soft_solve_batch(vboc_handle h, const vboc_mpc_batch_t* b, const vboc_mpc_soft_t* soft, void* stream) {
+  const std::string W = "vboc_mpc_soft_solve_batch";
+  if (!soft) return fail(VBOC_ERR_ARG, W + ": NULL soft-constraint description");
+  if (b && b->B > 0 && !soft->Zl) return fail(VBOC_ERR_ARG, W + ": NULL Zl (the per-stage slack weights)");
+  if (b && b->hidden <= 0) return fail(VBOC_ERR_ARG, W + ": the soft rows need the network (hidden > 0)");
+  if (!(soft->safety_margin < 100.0)) return fail(VBOC_ERR_ARG, W + ": safety_margin must be < 100");
+  return mpc_solve(h, b, soft, stream, W);
+}
+
+static int mpc_solve(vboc_handle h, const vboc_mpc_batch_t* b, const vboc_mpc_soft_t* sf, void* stream,
+                     const std::string& W) {
+  if (busy(h, W.c_str())) return VBOC_ERR_ARG;
   if (!h || !b) return fail(VBOC_ERR_ARG, W + ": NULL argument");
   if (h->nq != 3) return fail(VBOC_ERR_UNSUPPORTED, W + ": the Safe-MPC OCP is the triple pendulum's (nq = 3)");
   if (h->o.hc) return fail(VBOC_ERR_UNSUPPORTED, W + ": no path constraint in the Safe-MPC OCP (clear it first)");
@@ -2324,6 +2349,11 @@ int vboc_mpc_solve_batch(vboc_handle h, const vboc_mpc_batch_t* b, void* stream)
     mp.mean = b->mean; mp.std = b->std; mp.lh = b->lh; mp.uh = b->uh;
   }
   mp.hrow = b->h_out;
+  mp.soft = 0; mp.sm = 100.0; mp.zl = mp.Zl = mp.Wb = mp.Web = nullptr;
+  if (sf) {   // OCPtriplependulumSoftTraj: the margin-scaled row on every stage, soft lower sides
+    mp.soft = 1; mp.sm = 100.0 - sf->safety_margin;
+    mp.zl = sf->zl; mp.Zl = sf->Zl; mp.Wb = sf->W_b; mp.Web = sf->We_b;
+  }
   Inputs in;
   in.B = b->B; in.nmax = b->N; in.N = Nb;
   in.xg = xg7; in.ug = b->u_guess; in.p = pp; in.lbx = lbx7; in.ubx = ubx7; in.lbu = lbu_b; in.ubu = ubu_b;

@@ -22,7 +22,7 @@ EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", 
            "vboc_rk4_sens_batch_host", "vboc_last_kernel_ms",
            "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_data_generation_async",
            "vboc_data_generation_wait", "vboc_testing", "vboc_testing_test", "vboc_hjr_solve_batch",
-           "vboc_set_path_constraint", "vboc_mpc_solve_batch",
+           "vboc_set_path_constraint", "vboc_mpc_solve_batch", "vboc_mpc_soft_solve_batch",
            "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
@@ -78,6 +78,11 @@ class MpcBatch(ctypes.Structure):
                                                "W", "We", "yref", "yref_e", "W0", "b0", "W1", "b1", "W2", "b2")] + \
                [(n, ctypes.c_double) for n in ("mean", "std", "lh", "uh")] + \
                [(n, ctypes.c_void_p) for n in ("status", "x_out", "u_out", "cost", "sqp_iter", "qp_iter", "h_out")]
+
+
+class MpcSoft(ctypes.Structure):
+    """vboc_mpc_soft_t (include/vboc.h): OCPtriplependulumSoftTraj's soft rows (device arrays)."""
+    _fields_ = [("safety_margin", ctypes.c_double)] + [(n, ctypes.c_void_p) for n in ("Zl", "zl", "W_b", "We_b")]
 
 
 # per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
@@ -136,6 +141,8 @@ def load():
     lib.vboc_testing.argtypes = [ctypes.c_void_p, ctypes.POINTER(DgBatch), ctypes.c_int, ctypes.c_void_p]
     lib.vboc_testing_test.argtypes = [ctypes.c_void_p, ctypes.POINTER(TtBatch), ctypes.c_void_p]
     lib.vboc_mpc_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(MpcBatch), ctypes.c_void_p]
+    lib.vboc_mpc_soft_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(MpcBatch), ctypes.POINTER(MpcSoft),
+                                              ctypes.c_void_p]
     lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
@@ -367,11 +374,13 @@ class Solver:
         return out
 
     def mpc_solve_device(self, spec, x0, x_guess, u_guess, params=None, mean=0.0, std=1.0, rti=False, lh=0.0,
-                         uh=1e6, stream=None):
+                         uh=1e6, stream=None, soft=None):
         """OCPtriplependulumHardTerm.OCP_solve (vboc_mpc_solve_batch, ft.h) for every row of the float64 cuda tensor
         x0 [B, 6]: guesses [B, N+1, 6] / [B, N, 3] (cuda, float64), spec a safempc.MpcSpec, params the NeuralNetDIR
         weights as float64 cuda tensors (None: no terminal row).  Returns a dict of device tensors: status, x, u, cost,
-        sqp_iter, qp_iter, h (the row at the result's x_N)."""
+        sqp_iter, qp_iter, h (the row at the result's x_N).
+        soft: OCPtriplependulumSoftTraj (vboc_mpc_soft_solve_batch) - dict(margin=..., Zl=[B, N+1], zl=[B, N+1] or
+        None, W=[B, 9] or None, We=[B, 6] or None), float64 cuda tensors."""
         import torch
         B, N = x0.shape[0], spec.N
         for t_ in (x0, x_guess, u_guess):
@@ -398,8 +407,24 @@ class Solver:
                      cost=out["cost"].data_ptr(), sqp_iter=out["sqp_iter"].data_ptr(),
                      qp_iter=out["qp_iter"].data_ptr(), h_out=out["h"].data_ptr())
         st = stream if stream is not None else torch.cuda.current_stream(dev)
-        _check(self.lib.vboc_mpc_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
-        out["_keep"] = (bnd, host, W)
+        if soft is None:
+            _check(self.lib.vboc_mpc_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+            out["_keep"] = (bnd, host, W)
+            return out
+        arrs = {}
+        for k_, shp in (("Zl", (B, N + 1)), ("zl", (B, N + 1)), ("W", (B, 9)), ("We", (B, 6))):
+            a = soft.get(k_)
+            if a is None:
+                continue
+            assert a.is_cuda and a.dtype == torch.float64 and a.is_contiguous() and tuple(a.shape) == shp, (k_, a.shape)
+            arrs[k_] = a
+        sf = MpcSoft(safety_margin=float(soft["margin"]), Zl=arrs["Zl"].data_ptr(),
+                     zl=arrs["zl"].data_ptr() if "zl" in arrs else None,
+                     W_b=arrs["W"].data_ptr() if "W" in arrs else None,
+                     We_b=arrs["We"].data_ptr() if "We" in arrs else None)
+        _check(self.lib.vboc_mpc_soft_solve_batch(self.h, ctypes.byref(b), ctypes.byref(sf),
+                                                  ctypes.c_void_p(st.cuda_stream)))
+        out["_keep"] = (bnd, host, W, arrs)
         return out
 
     def kernel_stats(self):

@@ -150,6 +150,79 @@ class OCPtriplependulumHardTerm(OCPtriplependulum):
                          mean=float(mean), std=float(std), regenerate=regenerate, **kw)
 
 
+class _SoftOcpSolver(_OcpSolver):
+    """The SoftTraj drivers' accessors: get(i, 'x' | 'u') and cost_set(i, 'Zl' | 'zl' | 'W', value) - the per-stage
+    slack weights (soft_traj_constraints/3dof_sym.py:102-105, receiding_hard_constraints/3dof_sym.py:41-46) and stage
+    weights (:36-40), kept until changed, as ACADOS keeps them in the solver."""
+
+    def __init__(self, ocp):
+        super().__init__()
+        self.ocp = ocp
+
+    def cost_set(self, i, field, value):
+        o, N = self.ocp, self.ocp.N
+        if not 0 <= i <= N:
+            raise ValueError(f"stage {i} outside 0..{N}")
+        v = np.asarray(value, dtype=np.float64)
+        if field in ("Zl", "zl"):
+            getattr(o, field)[i] = float(v.reshape(-1)[0])
+        elif field == "W":
+            if np.abs(v - np.diag(np.diag(v))).max() > 0.0:
+                raise NotImplementedError("cost_set(W): diagonal weights only (the drivers' block_diag(Q, R))")
+            if i < N:
+                o.W[i] = np.diag(v)
+            else:
+                o.We[:] = np.diag(v)
+        else:
+            raise NotImplementedError(f"cost_set field {field!r}")
+
+
+class OCPtriplependulumSoftTraj(OCPtriplependulum):
+    """The soft-constraint class (:242-304): the row nn_decisionfunction_conservative = NN(x) (100 - safety_margin) /
+    100 - max(|x[2:]|, 1e-3) on every stage 0..N (con_h_expr and con_h_expr_e, lh = 0, uh = 1e6), soft on its lower
+    side (idxsh / idxsh_e) with zl = Zl = zu = Zu = 0 until the driver sets them (ocp_solver.cost_set).  GPU:
+    vboc_mpc_soft_solve_batch (ft.h)."""
+
+    def __init__(self, nlp_solver_type, time_step, tot_time, nn_params, mean, std, safety_margin, regenerate=False,
+                 **kw):
+        super().__init__(nlp_solver_type, time_step, tot_time, nn_params=[np.asarray(p.detach().cpu().numpy()
+                         if hasattr(p, "detach") else p, dtype=np.float64) for p in nn_params],
+                         mean=float(mean), std=float(std), regenerate=regenerate, **kw)
+        self.safety_margin = float(safety_margin)
+        N = self.N
+        self.Zl, self.zl = np.zeros(N + 1), np.zeros(N + 1)     # ocp.cost.Zl / zl / Zl_e / zl_e = 0 (:265-282)
+        self.W = np.tile(self.spec.W, (N, 1))
+        self.We = self.spec.W_e.copy()
+        self.ocp_solver = _SoftOcpSolver(self)
+
+    def nn_decisionfunction_conservative(self, params, mean, std, safety_margin, x):
+        """The row at one state (:284-304), numerically (the receding driver's use, :32-35)."""
+        P = [np.asarray(p.detach().cpu().numpy() if hasattr(p, "detach") else p, dtype=np.float64) for p in params]
+        return nn_row(P, float(mean), float(std), x, safety_margin=safety_margin)
+
+    def weights(self, B):
+        """The solver's current weights as per-problem arrays (Zl, zl [B, N+1], W [B, 9], We [B, 6])."""
+        if np.abs(self.W - self.W[0]).max() > 0.0:
+            raise NotImplementedError("different stage weights W on different stages")
+        return dict(Zl=np.tile(self.Zl, (B, 1)), zl=np.tile(self.zl, (B, 1)), W=np.tile(self.W[0], (B, 1)),
+                    We=np.tile(self.We, (B, 1)))
+
+    def solve_batch(self, x0, x_guess, u_guess, weights=None):
+        """Batched OCP_solve: numpy [B, 6], [B, N+1, 6], [B, N, 3]; weights: per-problem arrays (Zl, zl, W, We;
+        default: the solver's, cost_set)."""
+        import torch
+        B = np.asarray(x0).shape[0]
+        w = self.weights(B)
+        if weights is not None:
+            w.update({k: np.asarray(v, dtype=np.float64) for k, v in weights.items() if v is not None})
+        T = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=self.dev)
+        soft = dict(margin=self.safety_margin, **{k: T(v) for k, v in w.items()})
+        out = self.solver.mpc_solve_device(self.spec, T(x0), T(x_guess), T(u_guess), self.params, self.mean,
+                                           self.std, rti=self.rti, soft=soft)
+        torch.cuda.synchronize(self.dev)
+        return {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
+
+
 class _Integrator:
     def __init__(self, T):
         self.T, self.x, self.u, self.out = T, None, None, None
@@ -179,12 +252,16 @@ class SYMtriplependulum:
 # ------------------------------------------------------------------------------------------------
 # the closed-loop driver (hard_terminal_constraints/3dof_sym.py:15-72) for a batch of initial states
 # ------------------------------------------------------------------------------------------------
-def simulate_batch(solve, rk4, spec, x0s, x_guess, u_guess, tot_steps=100):
+def simulate_batch(solve, rk4, spec, x0s, x_guess, u_guess, tot_steps=100, weights=None, log=None):
     """The reference's simulate(p) for every initial state at once: each MPC step solves the OCPs of the problems
     still running in one batched call (solve(x0 [b, 6], xg [b, N+1, 6], ug [b, N, 3]) -> dict(status, x, u)),
     applies the reference's guess shifting and failure bookkeeping per problem (failed_iter, :37-62), and steps the
     plant with one RK4 of time_step (rk4(x [b, 6], u [b, 3]) -> x1).  Returns (res_steps [B] - the step at which each
-    problem stopped, as simulate returns f -, simX [B, tot_steps + 1, 6], solves)."""
+    problem stopped, as simulate returns f -, simX [B, tot_steps + 1, 6], solves).
+    weights (the receding driver): weights(f, failed [b], last_x [b, N+1, 6]) -> per-problem solver weights for the
+    step, passed as solve(x0, xg, ug, weights); last_x is each problem's previous solve's result (ocp_solver.get).
+    log (dict, optional) receives 'u' [B, tot_steps, 3]: the control applied to the plant at each step (NaN after the
+    stop)."""
     x0s = np.asarray(x0s, dtype=np.float64)
     B, N = x0s.shape[0], spec.N
     xg = np.array(x_guess, dtype=np.float64, copy=True)
@@ -194,12 +271,18 @@ def simulate_batch(solve, rk4, spec, x0s, x_guess, u_guess, tot_steps=100):
     failed = np.full(B, -1)
     res = np.full(B, tot_steps - 1)
     live = np.ones(B, dtype=bool)
+    last_x = np.array(xg, copy=True)
+    appliedU = np.full((B, tot_steps, 3), np.nan)
     solves = 0
     for f in range(tot_steps):
         idx = np.flatnonzero(live)
         if idx.size == 0:
             break
-        r = solve(simX[idx, f], xg[idx], ug[idx])
+        if weights is None:
+            r = solve(simX[idx, f], xg[idx], ug[idx])
+        else:
+            r = solve(simX[idx, f], xg[idx], ug[idx], weights(f, failed[idx], last_x[idx]))
+        last_x[idx] = r["x"]
         solves += idx.size
         simU = np.zeros((idx.size, 3))
         keep = np.ones(idx.size, dtype=bool)
@@ -226,4 +309,61 @@ def simulate_batch(solve, rk4, spec, x0s, x_guess, u_guess, tot_steps=100):
         step = idx[keep]
         if step.size:
             simX[step, f + 1] = rk4(simX[step, f], simU[keep])
+            appliedU[step, f] = simU[keep]
+    if log is not None:
+        log["u"] = appliedU
     return res, simX, solves
+
+
+# ------------------------------------------------------------------------------------------------
+# the soft-constraint drivers (VBOC/Safe MPC/soft_traj_constraints/3dof_sym.py, receiding_hard_constraints/3dof_sym.py)
+# ------------------------------------------------------------------------------------------------
+def soft_traj_weights(N):
+    """soft_traj_constraints/3dof_sym.py:102-105: Zl = 0 on stages 1..N-1, 1e6 at N (stage 0 keeps the class's 0)."""
+    Zl = np.zeros(N + 1)
+    Zl[N] = 1e6
+    return Zl
+
+
+def receding_weights(params, mean, std, safety_margin, N):
+    """receiding_hard_constraints/3dof_sym.py:26-46 for the problems of one MPC step: the receding index from the
+    previous solution (the last stage i in 1..N whose state satisfies the row, when the previous solve succeeded),
+    receiding_iter = N - failed_iter - receiding, Q = diag(1e-2 + 10^(2 receiding_iter / N), 1e-4, ...), R = 1e-4 I,
+    Zl = 1e12 at stage receiding_iter and 10^(6 (1 - receiding_iter / N)) elsewhere.  Returns weights(f, failed,
+    last_x) for simulate_batch."""
+    def weights(f, failed, last_x):
+        b = failed.shape[0]
+        Zl, W, We = np.empty((b, N + 1)), np.empty((b, 9)), np.empty((b, 6))
+        for j in range(b):
+            receiding = 0
+            fi = int(failed[j])
+            if fi == 0 and f > 0:
+                for i in range(1, N + 1):
+                    if nn_row(params, mean, std, last_x[j, i], safety_margin=safety_margin) >= 0.:
+                        receiding = N - i + 1
+            ri = N - fi - receiding
+            Q = np.array([1e-2 + pow(10, ri / N * 2), 1e-4, 1e-4, 1e-4, 1e-4, 1e-4])
+            W[j] = np.r_[Q, [1e-4, 1e-4, 1e-4]]
+            We[j] = Q
+            Zl[j] = pow(10, (1 - ri / N) * 6)
+            if 0 <= ri <= N:
+                Zl[j, ri] = 1e12
+        return dict(Zl=Zl, W=W, We=We)
+    return weights
+
+
+def halton_states(spec, test_num=100):
+    """The drivers' initial states (:98-103): a Halton sequence (scipy.stats.qmc, unscrambled) of the positions
+    scaled to [Xmin, Xmax], zero velocities."""
+    from scipy.stats import qmc
+    sample = qmc.Halton(d=3, scramble=False).random(n=test_num)
+    data = qmc.scale(sample, spec.xmin[:3], spec.xmax[:3])
+    x0 = np.zeros((test_num, 6))
+    x0[:, :3] = data
+    return x0
+
+
+def compare_steps(res_steps_traj, res_steps):
+    """The drivers' comparison with the unconstrained MPC (:158-172): better / equal / worse counts."""
+    d = np.asarray(res_steps_traj) - np.asarray(res_steps)
+    return int((d > 0).sum()), int((d == 0).sum()), int((d < 0).sum())
