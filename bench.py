@@ -179,7 +179,7 @@ class GpuEngine:
         self.solver.set_option("factor_mfma", 1 if args.factor == "mfma" else 0)
         self.solver.set_option("profile_kernels", 1 if args.mode == "lane" else 0)
         self.solver.set_option("dg_spec_early", getattr(args, "spec_early", 0))
-        self.solver.set_option("dg_spec_first", getattr(args, "spec_first", 0))
+        self.solver.set_option("dg_spec_first", getattr(args, "spec_first", 2))
         self.solver.set_option("dg_spec_crit", getattr(args, "spec_crit", 0))
         if getattr(args, "wave_groups", 0):   # resident problems (default: sized to the 256 MiB MALL)
             self.solver.set_option("wave_groups", args.wave_groups)
@@ -278,9 +278,10 @@ def parse(argv=None):
     ap.add_argument("--spec-early", type=int, default=0,
                     help="dg-loop: queued speculative restarts go before new problems once this few problems are left "
                          "(0: only once the problem queue is drained)")
-    ap.add_argument("--spec-first", type=int, default=0,
-                    help="dg-loop: 1 = queued speculative restarts go before parked resumes once the new problems run "
-                         "out (measured: mixed, off by default; DESIGN.md section 14)")
+    ap.add_argument("--spec-first", type=int, default=2,
+                    help="dg-loop: queued speculative restarts go before parked resumes once the new problems run out: "
+                         "0 off, 1 on, 2 (default) on for launches of < 128 problems per resident wave (the warmup / "
+                         "configs[2] round; DESIGN.md section 14)")
     ap.add_argument("--spec-crit", type=int, default=0,
                     help="dg-loop: 1 = the critical-path rule for speculative restarts (DESIGN.md section 14)")
     ap.add_argument("--spec-min-ext", type=int, default=0,

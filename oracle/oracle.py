@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "libvboc_oracle.so")
+LIB = os.environ.get("VBOC_ORACLE_LIB") or os.path.join(HERE, "libvboc_oracle.so")   # tools/oracle_asan.sh: the ASan build
 
 
 class Opts(ctypes.Structure):

@@ -37,7 +37,7 @@ def main():
                     help="dg_park option values to run (1: parked first solves, the product default; 0: off)")
     ap.add_argument("--window", type=int, nargs="*", default=[0],
                     help="dg_spec_window option values to run (0: off, the product default)")
-    ap.add_argument("--spec-first", type=int, nargs="*", default=[0],
+    ap.add_argument("--spec-first", type=int, nargs="*", default=[2],
                     help="dg_spec_first option values to run (1: restart jobs before parked resumes)")
     ap.add_argument("--spec-crit", type=int, nargs="*", default=[0],
                     help="dg_spec_crit option values to run (1: the critical-path rule for restart jobs)")

@@ -9,6 +9,8 @@
 #   double                    configs[1]: the double pendulum's 10k dg-loop and first-solve lines
 #   probe=<B>[:<groups,...>]  tools/dg_probe.py over B problems with the product and every vboc_amd/ab/*.so
 #                             (same box A/B: kernel time, bulk rate, digest)
+#   ur5trunc                  tools/ur5_trunc.py (the UR5 parity problems' truncated-solve digests) per build: the
+#                             product and every vboc_amd/ab/*.so
 #   pmc=<pass,...>            rocprofv3 --pmc passes of bench (sqa sqb fetch write tcc mfma), one run per pass
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:?out-subdir}; shift; mkdir -p $O
@@ -41,6 +43,12 @@ for step in "$@"; do
                run "probe $(basename $L)" 400 env VBOC_LIB=$L python3 -u tools/dg_probe.py --B $B --groups ${G//,/ } \
                  >> $O/probe.jsonl 2>> $O/probe.err
              done; cat $O/probe.jsonl;;
+    ur5trunc) for L in $R/vboc_amd/libvboc_amd.so $R/vboc_amd/ab/*.so; do   # the UR5 truncated-solve digests per build
+                [ -f "$L" ] || continue
+                n=$(basename $L .so)
+                run "ur5trunc $n" 300 env VBOC_LIB=$L python3 -u tools/ur5_trunc.py $O/trunc_$n > $O/trunc_$n.jsonl \
+                  2> $O/trunc_$n.err
+              done;;
     pmc=*) for p in $(echo ${step#pmc=} | tr , ' '); do
              case $p in
                sqa) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES";;
@@ -51,8 +59,8 @@ for step in "$@"; do
                mfma) C="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE";;
                *) echo "unknown pmc pass $p"; exit 2;;
              esac
-             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 360 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$p -o run \
-                -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu --progress 30 > $O/bench_pmc_$p.json 2> $O/pmc_$p.err)
+             (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 360 rocprofv3 --pmc $C --output-format csv -d $O/$p -o run \
+                -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu --progress 30 > $O/bench_$p.json 2> $O/$p.err)
              rc=$?; echo "step pmc $p exit $rc"; [ $rc -eq 0 ] || exit $rc
            done;;
     *) echo "unknown step $step"; exit 2;;

@@ -1,4 +1,4 @@
-"""Summary of k_dg's counters at the driver's launch shape (tools/gpu_r04_pmc.sh: bench.py --steps 20 --warmup 5,
+"""Summary of k_dg's counters at the driver's launch shape (tools/gpu_run.sh pmc=...: bench.py --steps 20 --warmup 5,
 one rocprofv3 --pmc pass per counter group), for the TIMED launch (the largest k_dg dispatch; the warmup launch is
 a quarter of its size).  Verdict r03 item 4.
 
