@@ -7,6 +7,7 @@
 #   bench                     the driver's command (bench.py --steps 20 --warmup 5) -> <out>/bench.json
 #   prof                      the same command under rocprofv3 --kernel-trace --stats -> <out>/prof
 #   double                    configs[1]: the double pendulum's 10k dg-loop and first-solve lines
+#   doubleab                  the same per build (product and every vboc_amd/ab/*.so), same box, no CPU baseline
 #   probe=<B>[:<groups,...>]  tools/dg_probe.py over B problems with the product and every vboc_amd/ab/*.so
 #                             (same box A/B: kernel time, bulk rate, digest)
 #   ur5trunc                  tools/ur5_trunc.py (the UR5 parity problems' truncated-solve digests) per build: the
@@ -37,6 +38,14 @@ for step in "$@"; do
               2> $O/bench_double_dg.err &&
             run double_fs 200 python bench.py --workload first-solve --nq 2 --batch 10000 --steps 1 --warmup 1 \
               > $O/bench_double_fs.json 2> $O/bench_double_fs.err;;
+    doubleab) for L in $R/vboc_amd/libvboc_amd.so $R/vboc_amd/ab/*.so; do   # configs[1] lines per build, same box
+                [ -f "$L" ] || continue
+                n=$(basename $L .so)
+                run "double fs $n" 300 env VBOC_LIB=$L python bench.py --workload first-solve --nq 2 --batch 10000 --steps 3 \
+                  --warmup 1 --no-cpu > $O/double_fs_$n.json 2> $O/double_fs_$n.err &&
+                run "double dg $n" 300 env VBOC_LIB=$L python bench.py --nq 2 --batch 10000 --steps 1 --warmup 1 --no-cpu \
+                  > $O/double_dg_$n.json 2> $O/double_dg_$n.err
+              done;;
     probe=*) spec=${step#probe=}; B=${spec%%:*}; G=0; [ "$spec" != "$B" ] && G=${spec#*:}
              for L in $R/vboc_amd/libvboc_amd.so $R/vboc_amd/ab/*.so; do
                [ -f "$L" ] || continue
