@@ -3,7 +3,7 @@
 `s_waitcnt vmcnt(N)` - a store can complete before an older load and let the wait pass early.  (A spill
 LOAD there only over-waits: loads complete in order.)
 Compiles the device code to assembly (hipcc -S, gfx950, -O3) and scans every k_wave / k_dg / k_ts / k_tt instantiation.
-usage: python tools/check_ring_waits.py   (exit status 1 on a violation)"""
+usage: python tools/check_ring_waits.py [extra hipcc flags, e.g. -DVBOC_COMPACT=3]   (exit status 1 on a violation)"""
 import os
 import re
 import subprocess
@@ -18,7 +18,7 @@ def main():
     with tempfile.TemporaryDirectory() as d:
         asm = os.path.join(d, "dev.s")
         subprocess.check_call(["hipcc", "--offload-arch=gfx950", "-std=c++17", "-O3", "-S", "--cuda-device-only",
-                               SRC, "-o", asm])
+                               *sys.argv[1:], SRC, "-o", asm])
         lines = open(asm).read().split("\n")
     bad_total = 0
     starts = [k for k, l in enumerate(lines) if re.match(r"^_ZN4vboc(6k_wave|4k_dg|4k_ts|4k_tt)I.*:", l)]

@@ -12,7 +12,9 @@
 #                             (same box A/B: kernel time, bulk rate, digest)
 #   ur5trunc                  tools/ur5_trunc.py (the UR5 parity problems' truncated-solve digests) per build: the
 #                             product and every vboc_amd/ab/*.so
-#   pmc=<pass,...>            rocprofv3 --pmc passes of bench (sqa sqb fetch write tcc mfma), one run per pass
+#   phases                    every -DVBOC_COOP_PROF build in vboc_amd/prof/: cycles per IPM iteration by phase (and
+#                             the split of one pass with -DVBOC_PROF_SPLIT) of 16k triple first solves (tools/gpu_perf.py)
+#   pmc=<pass,...>            rocprofv3 --pmc passes of bench (sqa sqb fetch write tcc mfma icache), one run per pass
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:?out-subdir}; shift; mkdir -p $O
 cd $R
@@ -58,6 +60,11 @@ for step in "$@"; do
                 run "ur5trunc $n" 300 env VBOC_LIB=$L python3 -u tools/ur5_trunc.py $O/trunc_$n > $O/trunc_$n.jsonl \
                   2> $O/trunc_$n.err
               done;;
+    phases) for L in $R/vboc_amd/prof/*.so; do   # -DVBOC_COOP_PROF builds (+ -DVBOC_PROF_SPLIT=<pass>)
+              n=$(basename $L .so)
+              run "phases $n" 300 env VBOC_LIB=$L python3 -u tools/gpu_perf.py 3 16384 0 dg 0 wave > $O/phases_$n.log 2>&1
+              cat $O/phases_$n.log
+            done;;
     pmc=*) for p in $(echo ${step#pmc=} | tr , ' '); do
              case $p in
                sqa) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES";;
@@ -65,6 +72,7 @@ for step in "$@"; do
                fetch) C="FETCH_SIZE";;
                write) C="WRITE_SIZE";;
                tcc) C="TCC_HIT_sum TCC_MISS_sum";;
+               icache) C="SQC_ICACHE_HITS SQC_ICACHE_MISSES SQ_IFETCH SQ_WAVES";;
                mfma) C="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 GRBM_GUI_ACTIVE";;
                *) echo "unknown pmc pass $p"; exit 2;;
              esac

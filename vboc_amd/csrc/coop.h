@@ -1196,11 +1196,17 @@ struct Coop {
   static constexpr int CE = NX + NU, CP = CE + 1;   // H row / G column of rs e; first Pi column
   // A_cl = A + B K of stages N-1..1 is formed inside factor_mfma (acl_slot) and written back with the
   // stage's outputs (ring_wb<OK, OX>: K .. Pe, C (dead until vec rebuilds it), A_cl): no acl_pass re-reading A, B
-  // and K from the stage records.  -DVBOC_ACL_PASS keeps the separate pass (measurement builds).
+  // and K from the stage records.  Per chain (bit NQ of VBOC_ACL_FUSED_NQ): the triple only - the fusion makes the
+  // triple's data-generation launch 2.4 % faster (profiles/r04_bytes_ab.json) but the double's 10k launches 4.3 %
+  // (dg loop) / 10.2 % (first solves) slower (profiles/r05_double_acl_ab.json).  -DVBOC_ACL_PASS: the separate pass
+  // for every chain (measurement builds).
+#ifndef VBOC_ACL_FUSED_NQ
+#define VBOC_ACL_FUSED_NQ (1 << 3)
+#endif
 #ifdef VBOC_ACL_PASS
   static constexpr bool ACL_FUSED = false;
 #else
-  static constexpr bool ACL_FUSED = FM;
+  static constexpr bool ACL_FUSED = FM && ((VBOC_ACL_FUSED_NQ >> NQ) & 1);
 #endif
   // factor_mfma's junk target: lanes without an output write the slot's tail past the written-back fields
   static constexpr int FJUNK = L::OX;
@@ -1229,9 +1235,12 @@ struct Coop {
     const int kb = fslot(sl);
     if (t < NX * NX) {
       const int q = t / NX, i = t - q * NX;
-      double a = s[kb + OA + q * NX + i];
-      UNR for (int c = 0; c < NU; ++c) a += s[kb + OB + q * NU + c] * s[kb + OK + c * NX + i];
-      s[kb + OACL + t] = a;
+      // all operand reads first (one LDS latency; the compiler otherwise waits on each pair before its FMA)
+      double av = s[kb + OA + q * NX + i], bv[NU], kv[NU];
+      UNR for (int c = 0; c < NU; ++c) { bv[c] = s[kb + OB + q * NU + c]; kv[c] = s[kb + OK + c * NX + i]; }
+      __builtin_amdgcn_sched_barrier(0);
+      UNR for (int c = 0; c < NU; ++c) av += bv[c] * kv[c];
+      s[kb + OACL + t] = av;
     }
   }
 
@@ -1303,16 +1312,17 @@ struct Coop {
     fdma(0);
     fdma(1);
     bool ok = true;
+    auto wb_prev = [&](int j, int k) {
+      if constexpr (ACL_FUSED) {
+        acl_slot((j - 1) % L::NSF);                   // LDS ops of this wave run in order: the write-back's
+        ring_wb<OK, L::OX>((j - 1) % L::NSF, k + 1);  // reads of the slot see them
+      } else {
+        ring_wb<OK, OC>((j - 1) % L::NSF, k + 1);
+      }
+    };
     for (int j = 0; j < N - 1; ++j) {
       const int k = N - 1 - j, kb = fslot(j % L::NSF);
-      if (j >= 1) {
-        if constexpr (ACL_FUSED) {
-          acl_slot((j - 1) % L::NSF);                   // LDS ops of this wave run in order: the write-back's
-          ring_wb<OK, L::OX>((j - 1) % L::NSF, k + 1);  // reads of the slot see them
-        } else {
-          ring_wb<OK, OC>((j - 1) % L::NSF, k + 1);
-        }
-      }
+      if (j >= 1) wb_prev(j, k);
       fdma(j + 2);
       vmwait<2 * P>();   // loads only, as in factor()
       dbg_check(kb, k, 0, WF, 1);
@@ -1349,6 +1359,9 @@ struct Coop {
         }
         hu[a] = s[HS + ia * 16 + c];
       }
+      // Y's image word is read with the H_u image, not after the stage's output stores (the compiler cannot tell
+      // that those do not alias it, and waited on the read at the end of the stage: 2 % of k_dg, same results)
+      const double yv = s[ysrc];
       double w[NU];
       if constexpr (RINV) {
         // Ru^-1 in closed form (adjugate / determinant): a dependent chain of ~14 FP64 ops instead of the
@@ -1401,7 +1414,7 @@ struct Coop {
         s[kb + mofs + a * NQ] = w[a];
       }
       UNR for (int e = 0; e < NU * NU; ++e) s[kb + OLR + e] = Lm[e];
-      s[kb + yofs] = s[ysrc];
+      s[kb + yofs] = yv;
       s[kb + pofs] = pg[0];
       s[kb + pofs + 4] = pg[1];
       lsync();
@@ -2265,8 +2278,8 @@ struct Coop {
       if (qst < 0 || !costate()) { status = 4; break; }
       CPROF(7)
       update_weights();
-      const double phi0 = merit(0.0);
       double alpha = 1.0;
+      const double phi0 = merit(0.0);
       for (;;) {
         const double pa = merit(alpha);
         if (pa < phi0) break;
