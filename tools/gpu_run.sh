@@ -13,7 +13,8 @@
 #   ur5trunc                  tools/ur5_trunc.py (the UR5 parity problems' truncated-solve digests) per build: the
 #                             product and every vboc_amd/ab/*.so
 #   phases                    every -DVBOC_COOP_PROF build in vboc_amd/prof/: cycles per IPM iteration by phase (and
-#                             the split of one pass with -DVBOC_PROF_SPLIT) of 16k triple first solves (tools/gpu_perf.py)
+#                             the split of one pass with -DVBOC_PROF_SPLIT) of 16k triple first solves (tools/gpu_perf.py);
+#                             PHASE_COOP=wave1024 (env) runs them on 1 024 resident problems (one wave per SIMD)
 #   pmc=<pass,...>            rocprofv3 --pmc passes of bench (sqa sqb fetch write tcc mfma icache), one run per pass
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${1:?out-subdir}; shift; mkdir -p $O
@@ -62,8 +63,9 @@ for step in "$@"; do
               done;;
     phases) for L in $R/vboc_amd/prof/*.so; do   # -DVBOC_COOP_PROF builds (+ -DVBOC_PROF_SPLIT=<pass>)
               n=$(basename $L .so)
-              run "phases $n" 300 env VBOC_LIB=$L python3 -u tools/gpu_perf.py 3 16384 0 dg 0 wave > $O/phases_$n.log 2>&1
-              cat $O/phases_$n.log
+              run "phases $n" 300 env VBOC_LIB=$L python3 -u tools/gpu_perf.py 3 16384 0 dg 0 ${PHASE_COOP:-wave} \
+                > $O/phases_$n${PHASE_COOP:+_$PHASE_COOP}.log 2>&1
+              cat $O/phases_$n${PHASE_COOP:+_$PHASE_COOP}.log
             done;;
     pmc=*) for p in $(echo ${step#pmc=} | tr , ' '); do
              case $p in

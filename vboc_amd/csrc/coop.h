@@ -1247,6 +1247,16 @@ struct Coop {
   __device__ __forceinline__ bool factor_mfma() {
     static_assert(MFMA_OK, "stage blocks fit one 16x16 FP64 MFMA tile");
     fresh();
+    // -DVBOC_PROF_SPLIT=4: sections of the stage loop (top / products / Cholesky / outputs) + the tail; =5: the top
+    // split (write-back / DMA issue / ring wait / the rest of the stage) + the tail
+#if defined(VBOC_PROF_SPLIT) && VBOC_PROF_SPLIT == 5
+    constexpr int FSPL = 5;
+#else
+    constexpr int FSPL = 4;
+#endif
+#define FS4(i) if constexpr (FSPL == 4) { SPROF(i) }
+#define FS5(i) if constexpr (FSPL == 5) { SPROF(i) }
+    SPROF_DECL(FSPL)
     const int c = t & 15, g = t >> 4;
     constexpr int HS = L::XS;   // H_u image [8][16] (rows g and 4 + g of every lane group); XS is free here
     // initial state: P_N = diag(D_N), Pi = E' (velocity selection), Sc = 0, LINE = 0
@@ -1323,9 +1333,13 @@ struct Coop {
     for (int j = 0; j < N - 1; ++j) {
       const int k = N - 1 - j, kb = fslot(j % L::NSF);
       if (j >= 1) wb_prev(j, k);
+      FS5(0)
       fdma(j + 2);
+      FS5(1)
       vmwait<2 * P>();   // loads only, as in factor()
       dbg_check(kb, k, 0, WF, 1);
+      FS4(0)
+      FS5(2)
       // the three operand reads issue back to back (one LDS latency, not three)
       const double r0 = s[kb * gb[0] + goff[0]], r1 = s[kb * gb[1] + goff[1]], hv = s[kb * hb + hoff];
       double g0 = r0 * gm[0], g1 = r1 * gm[1];
@@ -1346,6 +1360,7 @@ struct Coop {
       vreg(b1);
       h = __builtin_amdgcn_mfma_f64_16x16x4f64(g0, b0, h, 0, 0, 0);
       h = __builtin_amdgcn_mfma_f64_16x16x4f64(g1, b1, h, 0, 0, 0);
+      FS4(1)
       // H rows 4..11 -> LDS image; Ru (uniform) and this lane's column of H_u back
       s[HS + g * 16 + c] = h[HR0];
       if (HR0 + 1 < 4) s[HS + (4 + g) * 16 + c] = h[HR0 + 1 < 4 ? HR0 + 1 : 3];
@@ -1408,6 +1423,7 @@ struct Coop {
       // the empty asm keeps the MFMA from being sunk to the loop latch
       asm volatile("" : "+v"(Dm));
 #endif
+      FS4(2)
       // outputs of stage k into its ring slot: K = -Ru^-1 S, M = Ru^-1 Y, chol(Ru) (RINV: Ru^-1), Y, P e
       UNR for (int a = 0; a < NU; ++a) {
         s[kb + kofs + a * NX] = -w[a];
@@ -1418,6 +1434,8 @@ struct Coop {
       s[kb + pofs] = pg[0];
       s[kb + pofs + 4] = pg[1];
       lsync();
+      FS4(3)
+      FS5(3)
     }
     // flush P, Pi, Sc, LINE for stage 0 (factor()'s dot-product steps)
     UNR for (int r = 0; r < 4; ++r) {
@@ -1452,6 +1470,10 @@ struct Coop {
       lsync();
     }
     __syncthreads();   // write-back visible to the next sweep's ring loads
+    SPROF(4)
+    SPROF_FLUSH
+#undef FS4
+#undef FS5
     return ok;
   }
 
@@ -1744,6 +1766,7 @@ struct Coop {
       }
       if (t == 0) {
         UNR for (int i = 0; i < NZ; ++i) st(0, OT + i) = i < M0 ? w0[i < M0 ? i : 0] : 0.0;
+
       }
       if (t < NX) {
         double x = rs * st(0, OE + t);
