@@ -183,7 +183,7 @@ class GpuEngine:
         self.solver.set_option("dg_spec_crit", getattr(args, "spec_crit", 0))
         if getattr(args, "wave_groups", 0):   # resident problems (default: sized to the 256 MiB MALL)
             self.solver.set_option("wave_groups", args.wave_groups)
-        if getattr(args, "spec_min_ext", 0):   # measurement builds only (tools/spec_early_ab.sh, VBOC_LIB variant)
+        if getattr(args, "spec_min_ext", 0):   # measurement builds only (a VBOC_LIB variant; profiles/r03z_spec_early_ab.json)
             self.solver.set_option("dg_spec_min_ext", args.spec_min_ext)
         self.stream = torch.cuda.current_stream(self.device)
         self.kernel = {("dg-loop", "wave"): f"k_dg<{nq}>", ("first-solve", "wave"): f"k_wave<{nq}>",

@@ -9,7 +9,7 @@
 #   double                    configs[1]: the double pendulum's 10k dg-loop and first-solve lines
 #   doubleab                  the same per build (product and every vboc_amd/ab/*.so), same box, no CPU baseline
 #   probe=<B>[:<groups,...>]  tools/dg_probe.py over B problems with the product and every vboc_amd/ab/*.so
-#                             (same box A/B: kernel time, bulk rate, digest)
+#                             (same box A/B: kernel time, bulk rate, digest); PROBE_ARGS (env) adds dg_probe options
 #   ur5trunc                  tools/ur5_trunc.py (the UR5 parity problems' truncated-solve digests) per build: the
 #                             product and every vboc_amd/ab/*.so
 #   phases                    every -DVBOC_COOP_PROF build in vboc_amd/prof/: cycles per IPM iteration by phase (and
@@ -52,7 +52,7 @@ for step in "$@"; do
     probe=*) spec=${step#probe=}; B=${spec%%:*}; G=0; [ "$spec" != "$B" ] && G=${spec#*:}
              for L in $R/vboc_amd/libvboc_amd.so $R/vboc_amd/ab/*.so; do
                [ -f "$L" ] || continue
-               run "probe $(basename $L)" 400 env VBOC_LIB=$L python3 -u tools/dg_probe.py --B $B --groups ${G//,/ } \
+               run "probe $(basename $L)" 600 env VBOC_LIB=$L python3 -u tools/dg_probe.py --B $B --groups ${G//,/ } $PROBE_ARGS \
                  >> $O/probe.jsonl 2>> $O/probe.err
              done; cat $O/probe.jsonl;;
     ur5trunc) for L in $R/vboc_amd/libvboc_amd.so $R/vboc_amd/ab/*.so; do   # the UR5 truncated-solve digests per build

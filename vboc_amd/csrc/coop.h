@@ -1353,7 +1353,7 @@ struct Coop {
       pg = __builtin_amdgcn_mfma_f64_16x16x4f64(p0, g0, pg, 0, 0, 0);
       pg = __builtin_amdgcn_mfma_f64_16x16x4f64(p1, g1, pg, 0, 0, 0);
       // H = G' [PG | Pi] + diag(Hx, Hu) + carried LINE / -Sc
-      dbl4 h;
+      dbl4 h = {0.0, 0.0, 0.0, 0.0};   // (every entry set below; the initialiser only quiets -Wuninitialized)
       UNR for (int r = 0; r < 4; ++r) h[r] = fma(Dm[r], cm[r], hv * hm[r]);
       double b0 = fma(Dm[0], pim, pg[0]), b1 = fma(Dm[1], pim, pg[1]);
       vreg(b0);
