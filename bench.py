@@ -115,7 +115,7 @@ def pmc_traffic(kernel, problems=None):
 
 def dg_counters():
     """The newest committed driver-shape counter summary of k_dg (profiles/*_k_dg_counters.json, tools/pmc_r04.py over
-    the rocprofv3 --pmc passes of tools/gpu_r04_pmc.sh): (summary dict, path) or (None, None)."""
+    the rocprofv3 --pmc passes of tools/gpu_run.sh pmc=...): (summary dict, path) or (None, None)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_k_dg_counters.json")))
     if not files:

@@ -8,7 +8,7 @@ N x QP iterations, from the bench line), memory-side bytes (FETCH_SIZE x 2 + WRI
 in round 4 on the product's own window shapes, profiles/r04_fetch_size_calibration.json) per launch, per
 stage-IPM-iteration and per second, the L2 hit rate, FP64 MFMA busy share and the effective clock.
 
-usage: python tools/pmc_r04.py <dir with sqa/ sqb/ fetch/ write/ tcc/ mfma/ and bench_*.json> > profiles/r04_k_dg_counters.json
+usage: python tools/pmc_r04.py <dir with sqa/ sqb/ fetch/ write/ tcc/ mfma/ and bench_*.json> > profiles/r05_k_dg_counters.json
 """
 import csv
 import glob
