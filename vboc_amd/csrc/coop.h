@@ -1756,7 +1756,16 @@ struct Coop {
                       double& c1, double& c2) {
     fresh();
     constexpr int OT = CORR ? OD : ODA;
-    SPROF_DECL(3)
+    // -DVBOC_PROF_SPLIT=3: [stage 0, constant pass, recursion, step-length pass]; =6: the step-length pass's trips
+    // [load issue, controls + stores, component tests, reductions, everything before the pass]
+#if defined(VBOC_PROF_SPLIT) && VBOC_PROF_SPLIT == 6
+    constexpr int WSPL = 6;
+#else
+    constexpr int WSPL = 3;
+#endif
+#define W3(i) if constexpr (WSPL == 3) { SPROF(i) }
+#define W6(i) if constexpr (WSPL == 6) { SPROF(i) }
+    SPROF_DECL(WSPL)
     {
       double w0[M0];
       UNR for (int a = 0; a < M0; ++a) {
@@ -1775,7 +1784,7 @@ struct Coop {
         s[L::DXV + t] = x;
       }
     }
-    SPROF(0)
+    W3(0)
     // dx_{k+1} = c_k + A_cl,k dx_k,  c_k = rs e_k + B_k (k_f - M_k nu)  (lane i: row i); c is formed
     // stage-parallel first (-> OC)
     {
@@ -1811,7 +1820,7 @@ struct Coop {
       }
       __syncthreads();
     }
-    SPROF(1)
+    W3(1)
     const int cnt = N - 1;   // stages 1 .. N-1
     __syncthreads();
     if constexpr (L::S_FWD > 1) {
@@ -1896,7 +1905,8 @@ struct Coop {
     }
     }
     __syncthreads();   // dx rows (global) visible to the stage-parallel pass
-    SPROF(2)
+    W3(2)
+    W6(4)
     // controls of the middle stages, then the step-length tests (stage-parallel)
     typename Lane<NQ>::MinRatio mr{1.0, CORR ? o.tau : 1.0};
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
@@ -1910,6 +1920,7 @@ struct Coop {
       ldr<OK, NKM>(kk, km);
       if (CORR) ldr<OD, (2 * NZ + 1) / 2>(k, da);
       __builtin_amdgcn_sched_barrier(0);
+      W6(0)
       gdouble* rec = &g[(long long)k * REC];
       double d[NZ];
       if (k == 0) {
@@ -1929,6 +1940,7 @@ struct Coop {
         }
         UNR for (int i = 0; i < NZ; ++i) rec[OT + i] = d[i];
       }
+      W6(1)
       UNR for (int i = 0; i < NZ; ++i) {
         const CS c = comp_r(r, k, i);
         if (!c.bx) continue;
@@ -1967,12 +1979,16 @@ struct Coop {
           mr.add(hqu, dqu);
         }
       }
+      W6(2)
     }
     amax = wmind(mr.value());
     c0 = wsum(a0); c1 = wsum(a1); c2 = wsum(a2);
     __syncthreads();
-    SPROF(3)
+    W3(3)
+    W6(3)
     SPROF_FLUSH
+#undef W3
+#undef W6
   }
 
   __device__ __forceinline__ void update(double alpha, double smu) {
