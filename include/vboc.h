@@ -116,7 +116,9 @@ int vboc_destroy(vboc_handle h);
  * "alpha_min", "alpha_reduction"; interior-point internals "ipm_mu0", "ipm_push", "ipm_tau";
  * scheduling: "wave_groups" (resident problems of the wave solver, 0 = automatic) and "mall_mib"
  * (automatic sizing: the resident problems' hot stage records fit this much Infinity Cache, default
- * 256).  Test-only: "dg_fail_mod" (> 0: vboc_data_generation reports status 4 for every solve whose
+ * 256); data-generation scheduling, none of which changes a result: "dg_park", "dg_park_window",
+ * "dg_speculate", "dg_spec_window", "dg_spec_first" (default 2 = automatic: on for launches of fewer than 128
+ * problems per resident wave), "dg_spec_crit" (INTEGRATION.md section 2).  Test-only: "dg_fail_mod" (> 0: vboc_data_generation reports status 4 for every solve whose
  * initial position q_0 has int(|q_0| 1e6) % dg_fail_mod == 0, exercising the restart branches). */
 int vboc_set_option(vboc_handle h, const char* field, double value);
 int vboc_get_option(vboc_handle h, const char* field, double* value);
