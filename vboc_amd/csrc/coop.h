@@ -1591,9 +1591,9 @@ struct Coop {
       for (int j = 0; j < ng; ++j) {
         const int G = ng - 1 - j;
         gdma(j + L::DV);
+        double acl[S][NX], cc[S], pe[S];
         vmwait<L::DV>();   // group j has landed (the DV younger DMAs stay in flight)
         const int kb = vslot(j & (L::NSV - 1));
-        double acl[S][NX], cc[S], pe[S];
         UNR for (int u = 0; u < S; ++u) {
           UNR for (int q = 0; q < NX; ++q) acl[u][q] = s[kb + u * W + (OACL - OPE) + q * NX + i];
           cc[u] = s[kb + u * W + (OC - OPE) + i];
@@ -1842,9 +1842,9 @@ struct Coop {
       }
       for (int j = 0; j < ng; ++j) {
         gdma(j + L::DV);
+        double acl[S][NX], cc[S];
         vmwait<L::DV>();   // group j has landed
         const int kb = vslot(j & (L::NSV - 1));
-        double acl[S][NX], cc[S];
         UNR for (int u = 0; u < S; ++u) {
           UNR for (int q = 0; q < NX; ++q) acl[u][q] = s[kb + u * W + (OACL - OC) + i * NX + q];
           cc[u] = s[kb + u * W + i];
