@@ -13,8 +13,11 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 # VBOC_LIB selects another in-tree build of the same sources (e.g. the phase-profiling build
-# libvboc_amd_prof.so made with -DVBOC_COOP_PROF); default: the product library.
+# libvboc_amd_prof.so made with -DVBOC_COOP_PROF); default: the product library.  Only builds inside this repository
+# are accepted (bench.py records `library.variant` when one is used).
 LIB_PATH = os.environ.get("VBOC_LIB") or os.path.join(HERE, "libvboc_amd.so")
+if os.environ.get("VBOC_LIB") and not os.path.realpath(LIB_PATH).startswith(os.path.realpath(ROOT) + os.sep):
+    raise RuntimeError(f"VBOC_LIB={LIB_PATH}: only solver builds inside {ROOT} may replace the product library")
 SRC = os.path.join(HERE, "csrc", "vboc_solver.hip")
 
 EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", "vboc_solve_batch",
