@@ -1233,15 +1233,16 @@ struct Coop {
   // A_cl field: one entry per lane, acl_pass's arithmetic and order (same bits)
   __device__ __forceinline__ void acl_slot(int sl) {
     const int kb = fslot(sl);
-    if (t < NX * NX) {
-      const int q = t / NX, i = t - q * NX;
-      // all operand reads first (one LDS latency; the compiler otherwise waits on each pair before its FMA)
-      double av = s[kb + OA + q * NX + i], bv[NU], kv[NU];
-      UNR for (int c = 0; c < NU; ++c) { bv[c] = s[kb + OB + q * NU + c]; kv[c] = s[kb + OK + c * NX + i]; }
-      __builtin_amdgcn_sched_barrier(0);
-      UNR for (int c = 0; c < NU; ++c) av += bv[c] * kv[c];
-      s[kb + OACL + t] = av;
-    }
+    // branch-free (lanes past NX * NX repeat the last entry: the same value to the same word; the exec-masked
+    // block cost 5 % of the factorisation, profiles/r05_factor_loop_experiments.json), all operand reads before
+    // the FMAs (one LDS latency)
+    const int tt = t < NX * NX ? t : NX * NX - 1;
+    const int q = tt / NX, i = tt - q * NX;
+    double av = s[kb + OA + q * NX + i], bv[NU], kv[NU];
+    UNR for (int c = 0; c < NU; ++c) { bv[c] = s[kb + OB + q * NU + c]; kv[c] = s[kb + OK + c * NX + i]; }
+    __builtin_amdgcn_sched_barrier(0);
+    UNR for (int c = 0; c < NU; ++c) av += bv[c] * kv[c];
+    s[kb + OACL + tt] = av;
   }
 
   __device__ __forceinline__ bool factor_mfma() {
