@@ -30,6 +30,9 @@
  *                             triplependulum_class_vboc.py:91-240; drivers hard_terminal_constraints/3dof_sym.py)
  *   vboc_mpc_soft_solve_batch <- one OCPtriplependulumSoftTraj.OCP_solve(...) per problem (:242-304; drivers
  *                             soft_traj_constraints/3dof_sym.py, receiding_hard_constraints/3dof_sym.py)
+ *   vboc_al_solve_batch    <- one OCPtriplependulumINIT.compute_problem(q0, v0) per problem: the active-learning
+ *                             labelling OCP (AL/triplependulum_class_al.py:148-169, fanned out by testing(s0) of
+ *                             AL/triplependulum_al.py:24-42 at :133, :284)
  *   vboc_set_path_constraint <- model.con_h_expr + constraints.lh / uh of the Cartesian double pendulum
  *                             (VBOC/Cartesian constraints/doublependulum_class_fixedveldir.py:154-160)
  *   vboc_destroy           <- solver object destruction (acados_template __del__ -> free)
@@ -314,7 +317,9 @@ int vboc_mpc_solve_batch(vboc_handle h, const vboc_mpc_batch_t* batch, void* str
  * triplependulum_class_vboc.py:242-304) for every x0 of a vboc_mpc_batch_t: the row
  * nn_decisionfunction_conservative = NN(x) (100 - safety_margin) / 100 - max(|x[2:]|, 1e-3) on EVERY stage 0..N
  * (con_h_expr and con_h_expr_e), each soft on its lower side (idxsh / idxsh_e) with a slack s_k >= 0 costing
- * zl_k s_k + Zl_k s_k^2 / 2 - the per-stage weights the drivers set with ocp_solver.cost_set(i, "Zl", ...)
+ * c_k (zl_k s_k + Zl_k s_k^2 / 2), c_k = cost_scale on stages 0..N-1 and 1 at N (ACADOS' cost_scaling scales a
+ * stage's slack weights with its least-squares weights) - zl / Zl the per-stage weights the drivers set with
+ * ocp_solver.cost_set(i, "Zl", ...)
  * (soft_traj_constraints/3dof_sym.py:102-105, receiding_hard_constraints/3dof_sym.py:41-46); the upper side
  * (uh = 1e6, zu = Zu = 0) is never active and kept hard.  W_b / We_b: each problem's stage weights, the receding
  * driver's cost_set(i, "W", block_diag(Q, R)) / cost_set(N, "W", Q) (:36-40; NULL: the batch's host W / We).  Device
@@ -328,6 +333,31 @@ typedef struct {
 } vboc_mpc_soft_t;
 int vboc_mpc_soft_solve_batch(vboc_handle h, const vboc_mpc_batch_t* batch, const vboc_mpc_soft_t* soft,
                               void* stream);
+
+/* Active learning's labelling OCP: OCPtriplependulumINIT.compute_problem(q0, v0) (AL/triplependulum_class_al.py:
+ * 148-169; the OCP :82-144 with the terminal rest of :204-222) for every x0 = (q0, v0) of a batch, on the Safe-MPC
+ * solver (ft.h) with ACADOS' default options (SQP_RTI, Gauss-Newton, levenberg_marquardt 0, qp_solver_iter_max 50
+ * - the handle's options): reset (u = 0, multipliers 0), x_0 fixed, every stage's x guess (q0, 0), one QP and its
+ * full step.  The QP is the feasibility question the label answers: a QP the interior-point solver does not finish
+ * within qp_solver_iter_max (or a factorisation / NaN failure) is status 4.  label[b] = 1 (status 0), 0 (status 4)
+ * or 2 (any other status), as compute_problem returns.  LINEAR_LS cost 1/2 |[x; u]|^2_W on stages 0..N-1 (times
+ * cost_scale) + 1/2 |x_N|^2_We, yref = 0; path boxes lbx/ubx, lbu/ubu; terminal lbx_e/ubx_e (lb == ub: fixed, the
+ * class's zero final velocity).  Device pointers except W [3nq] / We [2nq] (host); asynchronous on `stream`.
+ * The handle: nq = 3, nmax >= N.  x0[B][2nq]; outputs label[B], status[B], x_out[B][N+1][2nq] (get(i, "x")),
+ * u_out[B][N][nq], qp_iter[B]. */
+typedef struct {
+  int B, N;
+  double h, cost_scale;
+  const double* x0;
+  const double *lbx, *ubx, *lbu, *ubu, *lbx_e, *ubx_e;
+  const double *W, *We;   /* host */
+  int* label;
+  int* status;
+  double* x_out;
+  double* u_out;
+  int* qp_iter;
+} vboc_al_batch_t;
+int vboc_al_solve_batch(vboc_handle h, const vboc_al_batch_t* batch, void* stream);
 
 /* Device time of the last vboc_solve_batch* call's solver kernel in milliseconds (HIP events on
  * the call's stream) and the number of kernel launches it used. */

@@ -325,3 +325,23 @@ def mpc_row(x, params, mean, std, margin=-1.0):
     lib().vboc_oracle_mpc_row(3, x.shape[0], _p(x), ctypes.byref(nnp), ctypes.c_double(float(margin)), _p(out))
     del keep
     return out
+
+
+def al_solve_batch(spec, x0, opts=None, nthreads=None):
+    """AL's compute_problem (vboc_oracle_ft.c vboc_oracle_al_solve_batch) for every row of x0 [B, 6]: spec a
+    vboc_amd.al.AlSpec.  Returns dict(label, status, qp_iter, x [B, N+1, 6], u [B, N, 3])."""
+    x0 = np.ascontiguousarray(x0, dtype=np.float64)
+    B, N = x0.shape[0], spec.N
+    x_out, u_out = np.zeros((B, N + 1, 6)), np.zeros((B, N, 3))
+    res = np.zeros(B, dtype=RESULT_DTYPE)
+    label = np.zeros(B, np.int32)
+    if opts is None:
+        opts = default_opts(lm=spec.lm, tol_stat=1e-6, qp_tol_stat=1e-8, qp_max_iter=spec.qp_iter_max)
+    vec = [np.ascontiguousarray(a, dtype=np.float64) for a in
+           (spec.xmin, spec.xmax, spec.umin, spec.umax, spec.xmin_e, spec.xmax_e, spec.W, spec.W_e)]
+    rc = lib().vboc_oracle_al_solve_batch(3, B, N, ctypes.c_double(spec.time_step), _p(x0), *[_p(a) for a in vec],
+                                          ctypes.c_double(spec.cost_scale), ctypes.byref(opts),
+                                          int(nthreads or os.cpu_count()), _p(x_out), _p(u_out), _p(res), _p(label))
+    if rc != 0:
+        raise RuntimeError(f"oracle al_solve_batch failed rc={rc}")
+    return dict(label=label, status=np.array(res["status"]), qp_iter=np.array(res["qp_iter"]), x=x_out, u=u_out)

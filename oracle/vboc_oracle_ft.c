@@ -38,7 +38,8 @@
  *    the full step; status 0, or 4 if the QP fails.
  * and `OCPtriplependulumSoftTraj` (triplependulum_class_vboc.py:242-304; vboc_mpc_soft_t): the row scaled by the
  * safety margin, h(x) = NN(z(x)) (100 - m) / 100 - vn(x), on EVERY stage 0..N (con_h_expr and con_h_expr_e), each row
- * soft on its lower side (idxsh / idxsh_e) with a slack s_k >= 0 costing zl_k s_k + Zl_k s_k^2 / 2 (the drivers'
+ * soft on its lower side (idxsh / idxsh_e) with a slack s_k >= 0 costing cs_k (zl_k s_k + Zl_k s_k^2 / 2), cs_k = cs
+ * on stages 0..N-1 and 1 at N like the stage's least-squares cost (ACADOS' cost_scaling scales z / Z too; the drivers'
  * cost_set(k, "Zl", ...) per stage, soft_traj_constraints/3dof_sym.py:102-105, receiding_hard_constraints/
  * 3dof_sym.py:41-46); the upper side (uh = 1e6, zu = Zu = 0) is kept hard - it is never active.  In the QP the slack
  * is a variable of its own (absolute value, so an RTI QP does not depend on the previous slack iterate) with a
@@ -93,6 +94,7 @@ typedef struct {
   double wq[FZ], yr[FZ], we[FX], yre[FX], cs;
   const vboc_mpc_nn_t* nn;
   int soft;        /* SoftTraj: rows on every stage, soft lower sides, the row scaled by sm / 100 */
+  int qcf;         /* a QP stopped by qp_max_iter is a QP failure (status 4): the AL labelling OCP */
   double sm;       /* 100 - safety_margin */
 } fprob_t;
 
@@ -1036,7 +1038,7 @@ static void fsqp(fprob_t* P, vboc_result_t* res) {
     int qit = 0;
     const int qs = fqp(P, &qit);
     qp_total += qit;
-    if (qs < 0) { status = 4; break; }
+    if (qs < 0 || (P->qcf && qs == 1)) { status = 4; break; }
     double lmax = 0.0;
     for (int k = 0; k <= N; ++k) {
       fstage_t* s = &P->st[k];
@@ -1164,15 +1166,15 @@ int vboc_oracle_ft_solve_batch(int nq, int B, int Nmax, const int* N, const doub
    x [N + 1][2 nq] and u [N][nq] without the dt column; hrow (may be NULL) gets h(x_N) of the result.
    soft (SoftTraj, :242-304; NULL = HardTerm): the margin-scaled row on every stage, soft lower sides with the
    per-stage weights zl / Zl [N + 1]. */
-int vboc_oracle_mpc_solve_soft(int nq, int N, double h, const double* x0, const double* x_guess,
-                               const double* u_guess, const double* xlb, const double* xub, const double* ulb,
-                               const double* uub, const double* xNlb, const double* xNub, const double* W,
-                               const double* We, const double* yref, const double* yref_e, double cs,
-                               const vboc_mpc_nn_t* nn, const vboc_mpc_soft_t* soft, int rti, const vboc_opts_t* opts,
-                               double* x_out, double* u_out, vboc_result_t* res, double* hrow) {
+static int mpc_impl(int nq, int N, double h, const double* x0, const double* x_guess, const double* u_guess,
+                    const double* xlb, const double* xub, const double* ulb, const double* uub, const double* xNlb,
+                    const double* xNub, const double* W, const double* We, const double* yref, const double* yref_e,
+                    double cs, const vboc_mpc_nn_t* nn, const vboc_mpc_soft_t* soft, int rti, int qcf,
+                    const vboc_opts_t* opts, double* x_out, double* u_out, vboc_result_t* res, double* hrow) {
   if (nq < 1 || nq > FQ || N < 1) return -1;
   const int n2 = 2 * nq, nx = n2 + 1, nu = nq;
-  for (int i = 0; i < n2; ++i) if (!(xlb[i] < xub[i]) || !(xNlb[i] < xNub[i])) return -2;
+  /* path boxes proper; a terminal component with lb == ub is a terminal equality (AL's zero final velocity) */
+  for (int i = 0; i < n2; ++i) if (!(xlb[i] < xub[i]) || !(xNlb[i] <= xNub[i])) return -2;
   for (int a = 0; a < nu; ++a) if (!(ulb[a] < uub[a])) return -2;
   if (nn && !(nn->lh <= nn->uh)) return -2;
   fprob_t P;
@@ -1185,7 +1187,9 @@ int vboc_oracle_mpc_solve_soft(int nq, int N, double h, const double* x0, const 
   P.xlb[n2] = P.xNlb[n2] = -INFINITY; P.xub[n2] = P.xNub[n2] = INFINITY;   /* dt: pinned by x_0 and the dynamics */
   P.x0lb[n2] = P.x0ub[n2] = h;
   for (int a = 0; a < nu; ++a) { P.ulb[a] = ulb[a]; P.uub[a] = uub[a]; }
-  P.track = 1; P.rti = rti; P.cs = cs; P.nn = nn;
+  for (int i = 0; i < n2; ++i)
+    if (xNlb[i] == xNub[i]) { P.xNfix[i] = 1; P.ei[P.ne] = i; P.ev[P.ne] = xNlb[i]; P.ne++; }
+  P.track = 1; P.rti = rti; P.cs = cs; P.nn = nn; P.qcf = qcf;
   if (soft && !nn) return -2;
   if (soft) { P.soft = 1; P.sm = 100.0 - soft->margin; }
   for (int i = 0; i < n2; ++i) { P.wq[i] = W[i]; P.yr[i] = yref[i]; P.we[i] = We[i]; P.yre[i] = yref_e[i]; }
@@ -1198,8 +1202,12 @@ int vboc_oracle_mpc_solve_soft(int nq, int N, double h, const double* x0, const 
     if (k < N) for (int a = 0; a < nu; ++a) P.st[k].u[a] = u_guess[k * nu + a];
   }
   for (int i = 0; i < n2; ++i) P.st[0].x[i] = x0[i];
-  if (soft)
-    for (int k = 0; k <= N; ++k) { P.st[k].zl = soft->zl ? soft->zl[k] : 0.0; P.st[k].Zl = soft->Zl ? soft->Zl[k] : 0.0; }
+  if (soft)   /* the slack weights scaled like their stage's cost (ACADOS cost_scaling: cs on 0..N-1, 1 at N) */
+    for (int k = 0; k <= N; ++k) {
+      const double sc = k < N ? cs : 1.0;
+      P.st[k].zl = soft->zl ? sc * soft->zl[k] : 0.0;
+      P.st[k].Zl = soft->Zl ? sc * soft->Zl[k] : 0.0;
+    }
   fsqp(&P, res);
   for (int k = 0; k <= N; ++k) {
     for (int i = 0; i < n2; ++i) x_out[k * n2 + i] = P.st[k].x[i];
@@ -1208,6 +1216,16 @@ int vboc_oracle_mpc_solve_soft(int nq, int N, double h, const double* x0, const 
   if (hrow) *hrow = nn ? nn_row(nn, nq, P.st[N].x, NULL, P.soft, P.sm) : 0.0;
   free(P.st);
   return 0;
+}
+
+int vboc_oracle_mpc_solve_soft(int nq, int N, double h, const double* x0, const double* x_guess,
+                               const double* u_guess, const double* xlb, const double* xub, const double* ulb,
+                               const double* uub, const double* xNlb, const double* xNub, const double* W,
+                               const double* We, const double* yref, const double* yref_e, double cs,
+                               const vboc_mpc_nn_t* nn, const vboc_mpc_soft_t* soft, int rti, const vboc_opts_t* opts,
+                               double* x_out, double* u_out, vboc_result_t* res, double* hrow) {
+  return mpc_impl(nq, N, h, x0, x_guess, u_guess, xlb, xub, ulb, uub, xNlb, xNub, W, We, yref, yref_e, cs, nn, soft,
+                  rti, 0, opts, x_out, u_out, res, hrow);
 }
 
 int vboc_oracle_mpc_solve(int nq, int N, double h, const double* x0, const double* x_guess, const double* u_guess,
@@ -1274,6 +1292,38 @@ int vboc_oracle_mpc_solve_batch(int nq, int B, int N, double h, const double* x0
                                         u_out + uo, res + b, hrow ? hrow + b : NULL);
     if (r == -2) { res[b].status = 5; res[b].sqp_iter = 0; res[b].qp_iter = 0; res[b].cost = NAN; }
     else if (r) err |= 1;
+  }
+  return err ? -1 : 0;
+}
+
+/* Active learning's labelling OCP, OCPtriplependulumINIT.compute_problem(q0, v0) (AL/triplependulum_class_al.py:
+   148-169; the OCP :82-144, terminal rest :204-222): the tracking OCP above with yref = 0, no row, ACADOS' default
+   SQP_RTI (one QP at the reset point, its full step), x_0 = (q0, v0) fixed, every stage's guess (q0, 0) (:157-160),
+   u = 0 and zero multipliers (reset, :150); a QP stopped by qp_max_iter is a QP failure (qcf: the label is the QP's
+   feasibility answer).  label[b] = 1 / 0 / 2 for status 0 / 4 / other (:164-169). */
+int vboc_oracle_al_solve_batch(int nq, int B, int N, double h, const double* x0, const double* xlb, const double* xub,
+                               const double* ulb, const double* uub, const double* xNlb, const double* xNub,
+                               const double* W, const double* We, double cs, const vboc_opts_t* opts, int nthreads,
+                               double* x_out, double* u_out, vboc_result_t* res, int* label) {
+  if (nq < 1 || nq > FQ || N < 1) return -1;
+  const int n2 = 2 * nq;
+  const double zero[3 * FQ] = {0};
+  int err = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(| : err)
+  for (int b = 0; b < B; ++b) {
+    double* xg = (double*)malloc(sizeof(double) * ((size_t)(N + 1) * n2 + (size_t)N * nq));
+    if (!xg) { err |= 1; continue; }
+    double* ug = xg + (size_t)(N + 1) * n2;
+    for (int k = 0; k <= N; ++k)
+      for (int i = 0; i < n2; ++i) xg[k * n2 + i] = i < nq ? x0[(size_t)b * n2 + i] : 0.0;
+    for (int e = 0; e < N * nq; ++e) ug[e] = 0.0;
+    const size_t xo = (size_t)b * (N + 1) * n2, uo = (size_t)b * N * nq;
+    const int r = mpc_impl(nq, N, h, x0 + (size_t)b * n2, xg, ug, xlb, xub, ulb, uub, xNlb, xNub, W, We, zero, zero, cs,
+                           NULL, NULL, 1, 1, opts, x_out + xo, u_out + uo, res + b, NULL);
+    free(xg);
+    if (r == -2) { res[b].status = 5; res[b].sqp_iter = 0; res[b].qp_iter = 0; res[b].cost = NAN; }
+    else if (r) err |= 1;
+    label[b] = res[b].status == 0 ? 1 : (res[b].status == 4 ? 0 : 2);
   }
   return err ? -1 : 0;
 }

@@ -35,9 +35,13 @@ run the same way on the drop-in vboc_amd.cartesian.OCPdoublependulumINIT (keep-o
 The HJR labelling function data_generation(v) (HJR/triplependulum_hjr.py:21-40) is run the same way on a fake
 `ocp` whose compute_problem solves the HJR one-step OCP on the oracle (vboc_oracle_hjr.c).
 
-Usage: python tests/golden/make_driver_golden.py [dg|test|pend|ur5|cart|hjr]
+The active-learning driver testing(s0) (AL/triplependulum_al.py:24-42) is run the same way on a fake `ocp` whose
+compute_problem solves AL's labelling OCP on the oracle (vboc_oracle_al_solve_batch).
+
+Usage: python tests/golden/make_driver_golden.py [dg|test|pend|ur5|cart|hjr|al]
   ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json, tests/golden/driver_1.json,
-      tests/golden/testing_ur5.json, tests/golden/testing_cartesian.json, tests/golden/hjr_3.json (+ hjr_net_3.npz)
+      tests/golden/testing_ur5.json, tests/golden/testing_cartesian.json, tests/golden/hjr_3.json (+ hjr_net_3.npz),
+      tests/golden/al_testing_3.json
 """
 import ast
 import json
@@ -366,8 +370,47 @@ def main_hjr():
     print("hjr_3.json", sum(o is not None and o[0] == 0 for _, o in out), "labelled viable of", len(out))
 
 
+def main_al():
+    """The active-learning labelling driver testing(s0) of AL/triplependulum_al.py:24-42 (fanned out at :133 / :284),
+    AST-extracted and run over 96 states of the driver's unlabeled box (:115-123, seeded numpy draws; the widened
+    velocity range puts some states out of bounds) with injected globals: the state box (:77-80), ocp_dim, and
+    `ocp` = an object with the AL OCPtriplependulumINIT surface (compute_problem(q0, v0) -> 1 / 0 / 2, N,
+    ocp_solver.get(i, "x")) solving the labelling OCP on the oracle (vboc_oracle_ft.c vboc_oracle_al_solve_batch)."""
+    import oracle
+    from vboc_amd.al import AlSpec, unlabeled_states
+    spec = AlSpec()
+    X = unlabeled_states(spec, 96, np.random.default_rng(4))
+
+    class Solver:
+        x = None
+
+        def get(self, i, field):
+            assert field == "x"
+            return np.copy(self.x[i])
+
+    class AlOcp:
+        N, nx = spec.N, spec.nx
+        ocp_solver = Solver()
+
+        def compute_problem(self, q0, v0):
+            r = oracle.al_solve_batch(spec, np.r_[q0, v0][None], nthreads=1)
+            self.ocp_solver.x = r["x"][0]
+            return int(r["label"][0])
+
+    code = extract(os.path.join(os.path.dirname(REF), "AL", "triplependulum_al.py"), "testing")
+    g = dict(np=np, ocp=AlOcp(), ocp_dim=6, q_max=spec.thetamax, q_min=spec.thetamin, v_max=spec.dthetamax,
+             v_min=-spec.dthetamax)
+    exec(code, g)
+    out = [g["testing"](list(map(float, s))) for s in X]
+    json.dump({"nq": 3, "X": X.tolist(), "results": [None if o is None else [o[0], o[1]] for o in out]},
+              open(os.path.join(HERE, "al_testing_3.json"), "w"))
+    print("al_testing_3.json", sum(o is not None and o[0][-1] == 1 for o in out), "feasible of", len(out))
+
+
 if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what in ("al", "all"):
+        main_al()
     if what in ("hjr", "all"):
         main_hjr()
     if what in ("dg", "all"):

@@ -12,9 +12,11 @@ pair says why:
   'status'   - the two solvers returned different statuses for the same request (a rounding-level difference
                that changed the SQP path enough to hit max_iter or a QP failure on one side only);
   'optimum'  - same status 0, results differ beyond the comparison tolerance, and each side's result is confirmed as
-               a solution of the request by an independent check (`verify`: the oracle warm-started from it converges
-               back to it): two points that both satisfy the solver's stopping tolerances (tol_stat 1e-3) - after a
-               long SQP path (hundreds of iterations) the two solvers stop at different such points;
+               a valid stop of the request by an independent check (`verify`, tests/kkt_check.py: the point passes
+               the solver's own stopping test - tol_stat 1e-3, eq / ineq / comp 1e-6 - with the best multipliers for
+               it): two points that both satisfy the stopping tolerances - after a long SQP path (hundreds of
+               iterations), or on a build whose arithmetic is re-associated, the two solvers stop at different such
+               points;
   'value'    - same status, results differ beyond rounding and not both confirmed (a genuine solver disagreement).
 Problems that end on the same path with the same result are 'same'."""
 import numpy as np

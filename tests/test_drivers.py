@@ -175,40 +175,42 @@ def test_lockstep_classifier_on_identical_backends():
     assert all(k == "same" for k, _ in kinds.values()), kinds
 
 
-def _converges_back(nq, oracle):
-    """verify(request, solution): the oracle, warm-started from the solution (primal guess, zero multipliers),
-    converges (status 0) within 5 SQP iterations to the same point (cost and x_0 to the lockstep tolerances): the
-    solution is a local optimum of the request's NLP."""
+def test_stopping_test_confirms_valid_stops_and_rejects_others():
+    """The optimum check of the lockstep classifier (tests/kkt_check.py): oracle solutions of fixture requests pass the
+    solver's stopping test - at the default options and with levenberg_marquardt 1e-4 (another SQP path, another stop
+    of the same request: x_0 apart by more than the lockstep tolerance, the 'optimum' case); the same point with its x_0 velocities moved (primal infeasible) or judged against the opposite cost
+    direction (feasible, not stationary) does not."""
     import dataclasses
-    from vboc_amd.drivers import _pack
-
-    def verify(req, sol):
-        if sol.status != 0:
-            return False
-        warm = dataclasses.replace(req, x_guess=np.asarray(sol.x), u_guess=np.asarray(sol.u))
-        r = oracle.solve(_pack(nq, [warm], 200))
-        return (int(r["status"][0]) == 0 and int(r["sqp_iter"][0]) <= 5
-                and abs(float(r["cost"][0]) - sol.cost) <= 1e-6 * (1 + abs(sol.cost))
-                and np.abs(r["x"][0, 0] - sol.x[0]).max() <= 1e-6)
-    return verify
-
-
-def test_converges_back_confirms_an_oracle_solution_and_rejects_a_moved_one():
-    """The optimum check of the lockstep classifier: an oracle solution of a fixture request is confirmed; the same
-    solution with its x_0 moved is not."""
+    import oracle
+    from kkt_check import kkt_verify, stopping_test
     from vboc_amd.drivers import Solution, _pack
     g = _golden(3)
-    gen = _gens(3, "dg", g)(int(g["ids"][0]))
-    req = next(gen)
-    ora = OracleBackend(3)
-    r = ora.solve(_pack(3, [req], 200))
-    n = req.N
-    sol = Solution(int(r["status"][0]), r["x"][0, :n + 1], r["u"][0, :n], float(r["cost"][0]))
-    assert sol.status == 0
-    verify = _converges_back(3, ora)
-    assert verify(req, sol)
-    bad = Solution(0, sol.x.copy(), sol.u, sol.cost + 0.1)
-    assert not verify(req, bad)
+    verify = kkt_verify(3)
+    for pid in g["ids"][:3]:
+        req = next(_gens(3, "dg", g)(int(pid)))
+        n = req.N
+        b = _pack(3, [req], 200)
+        stops = []
+        for lm in (1e-5, 1e-4):
+            xo, uo, r = oracle.solve_batch(3, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                                           b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"],
+                                           opts=oracle.default_opts(lm=lm))
+            sol = Solution(int(r["status"][0]), xo[0, :n + 1], uo[0, :n], float(r["cost"][0]))
+            assert sol.status == 0 and verify(req, sol), (pid, lm)
+            stops.append(sol.x[0])
+        assert np.abs(stops[0] - stops[1]).max() > 1e-5, pid
+        moved = sol.x.copy()
+        moved[0, 3:6] *= 1.001
+        assert not verify(req, Solution(0, moved, sol.u, sol.cost))
+        flip = dataclasses.replace(req, p=np.r_[-req.p[:3], req.p[3:]])
+        ok, res = stopping_test(3, flip, sol.x, sol.u)
+        assert not ok and res["eq"] <= 1e-6 and res["stat"] > 1e-3, res
+        assert not verify(req, Solution(4, sol.x, sol.u, sol.cost))     # a failed solve is never a valid stop
+
+
+def test_decision_and_optimum_caps():
+    from parity import caps
+    assert caps(261) == (7, 2) and caps(64) == (2, 1) and caps(320) == (9, 3)
 
 
 @pytest.mark.gpu
@@ -232,14 +234,19 @@ def test_gpu_driver_mismatches_are_rounding_level_flips(nq, law):
     ora = OracleBackend(nq) if law == "dg" else OracleBackend(nq, fm)
     from parity import dump
     trace = {}
+    from kkt_check import kkt_verify
     kinds = lockstep(nq, _gens(nq, law, g), [int(p) for p in g["ids"]], gpu, ora, nmax=200,
-                     verify=_converges_back(nq, OracleBackend(nq)), trace=trace)
+                     verify=kkt_verify(nq), trace=trace)
     counts = {k: sum(v[0] == k for v in kinds.values()) for k in ("same", "decision", "status", "optimum", "value")}
     print(nq, law, counts, {p: v for p, v in kinds.items() if v[0] != "same"})
     dump(f"lockstep_{law}_{nq}.json", dict(counts=counts, partings=trace))
     assert counts["value"] == 0, trace
-    # two confirmed optima are reported and capped like the decision flips: at most 1 % of the problems (at least 1)
-    assert counts["optimum"] <= max(1, len(kinds) // 100), trace
+    # two confirmed stops ('optimum') at most 1 % of the problems (at least 1), tolerance flips ('decision') at most 3 %
+    # (at least 2): tests/parity.py caps
+    from parity import caps
+    cap_dec, cap_opt = caps(len(kinds))
+    assert counts["optimum"] <= cap_opt, trace
+    assert counts["decision"] <= cap_dec, (counts, trace)
     # measured on MI355X (profiles/r02s_pytest_gpu_lockstep_classification.log): every problem 'same'
     assert counts["same"] >= 0.95 * len(kinds), counts
 

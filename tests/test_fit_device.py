@@ -32,6 +32,7 @@ def test_make_trainer_picks_torch_on_cpu_and_for_unsupported_shapes():
     from vboc_amd import fitlib
     from vboc_amd.learn import DirTrainer, make_trainer
     assert type(make_trainer(3, "cpu")) is DirTrainer
+    assert type(make_trainer(3, "cpu", native=True)) is DirTrainer
     assert fitlib.supported(6, 500, 4096) and fitlib.supported(4, 300, 4096) and fitlib.supported(2, 100, 64)
     assert not fitlib.supported(8, 1000, 32768) and not fitlib.supported(6, 500, 8192)
 
@@ -151,3 +152,12 @@ def test_device_fit_learns_like_the_torch_trainer():
     d.fit(F, it_max=2001)
     rh, rd = h.rmse(Ft), d.rmse(Ft)
     assert abs(rh - rd) <= 0.15 * rd, (rh, rd)
+
+
+@pytest.mark.gpu
+def test_make_trainer_defaults_to_pytorch_on_gpu():
+    """north_star keeps the NN fit on PyTorch-ROCm: the loop's trainer is DirTrainer unless the native one is asked
+    for (native=True, the device trainer of csrc/fit.hip)."""
+    from vboc_amd.learn import DirTrainer, HipTrainer, make_trainer
+    assert type(make_trainer(3, "cuda")) is DirTrainer
+    assert type(make_trainer(3, "cuda", native=True)) is HipTrainer

@@ -233,6 +233,26 @@ def test_free_time_parity_with_oracle():
         assert abs(g["x"][i, N, 0] - b["lbxe"][i, 0]) < 1e-6 and abs(g["x"][i, N, 1]) < 1e-6
 
 
+def test_free_time_infinite_bounds_are_a_free_component():
+    """A path component with both bounds infinite is free (no barrier terms, not counted in the centring target) on
+    the GPU as in the oracle's fcomp (the non-MP instantiation once treated it as boxed)."""
+    import oracle
+    from vboc_amd import lib
+    b = _ft_batch(64)
+    b["lbx"][:, 1], b["ubx"][:, 1] = -np.inf, np.inf       # the velocity unbounded on the path
+    s = lib.Solver(1, int(b["N"].max()))
+    g = s.solve_host(b, free_time=True)
+    s.close()
+    xo, uo, r = oracle.solve_batch(1, b["N"], b["x_guess"], b["u_guess"], b["p"], b["lbx"], b["ubx"], b["lbu"],
+                                   b["ubu"], b["lbx0"], b["ubx0"], b["lbxe"], b["ubxe"], free_time=True)
+    assert np.mean(g["status"] == r["status"]) >= 0.98
+    assert np.mean(g["sqp_iter"] == r["sqp_iter"]) >= 0.95
+    both = (g["status"] == 0) & (r["status"] == 0)
+    assert both.mean() >= 0.8
+    dc = np.abs(g["cost"] - r["cost"])[both]
+    assert np.median(dc) <= 1e-9 and dc.max() <= 2e-3, (np.median(dc), dc.max())
+
+
 def test_free_time_device_path_and_unsupported():
     import torch
     from vboc_amd import lib

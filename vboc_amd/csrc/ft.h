@@ -28,7 +28,7 @@
 
 namespace vboc {
 
-template <int NQ>
+template <int NQ, bool MP = false>
 struct FtL {
   static constexpr int NX = 2 * NQ + 1, NU = NQ, NZ = NX + NU, N2 = 2 * NQ;
   // stage record (doubles)
@@ -46,7 +46,9 @@ struct FtL {
                        RAQU = RAQL + 1, RLL = RAQU + 1, RLU = RLL + 1, RS = RLU + 1, RQS = RS + 1, RAS = RQS + 1,
                        RAQS = RAS + 1, RSL = RAQS + 1, RLSL = RSL + 1, RZL = RLSL + 1, RZ2 = RZL + 1, RSIG = RZ2 + 1,
                        RB = RSIG + 1, RW = RB + 1, RDTL = RW + 1, RDTU = RDTL + 1, RDQL = RDTU + 1, RDQU = RDQL + 1,
-                       RDS = RDQU + 1, RDQS = RDS + 1, RL = RDQS + 1, RU = RL + 1, REC = RU + 1;
+                       RDS = RDQU + 1, RDQS = RDS + 1, RL = RDQS + 1, RU = RL + 1;
+  // the free-time solver (MP false) never touches the row fields: its records end at F0's block
+  static constexpr int REC = MP ? RU + 1 : F0 + NX * NZ;
   static constexpr long long region_doubles(int nmax) { return (long long)REC * (nmax + 1); }
 };
 
@@ -62,6 +64,7 @@ struct FtL {
 constexpr int FT_NN_MAX = 512;
 struct MpcArgs {
   int on, rti, hid, soft;
+  int qcf;   // a QP stopped by qp_max_iter is a QP failure (status 4): the AL labelling OCP (vboc_al_solve_batch)
   double wq[10], yr[10], we[7], yre[7], cs, sm;
   const double *W0, *b0, *W1, *W1T, *b1, *W2, *b2;
   double mean, std, lh, uh;
@@ -72,7 +75,7 @@ struct MpcArgs {
 // MP: the Safe-MPC instantiation (k_ft<3, true>); the free-time pendulum solver carries no network buffers
 template <int NQ, bool MP>
 struct FtShared {
-  static constexpr int NX = FtL<NQ>::NX, NU = FtL<NQ>::NU, NNB = MP ? FT_NN_MAX : 1;
+  static constexpr int NX = FtL<NQ, MP>::NX, NU = FtL<NQ, MP>::NU, NNB = MP ? FT_NN_MAX : 1;
   int N, nf0, ne, pid, bad;
   int f0[NX], ei[NX], fix[NX];
   double ev[NX], c0[NX], cp[NX], x0lb[NX], x0ub[NX], xlb[NX], xub[NX], xNlb[NX], xNub[NX], ulb[NU], uub[NU];
@@ -192,7 +195,7 @@ __device__ __forceinline__ void ft_chol_solve(const double* L, int m, double* b)
 
 template <int NQ, bool MP = false>
 struct Ft {
-  using L = FtL<NQ>;
+  using L = FtL<NQ, MP>;
   static constexpr int NX = L::NX, NU = L::NU, NZ = L::NZ, N2 = 2 * NQ;
   FtShared<NQ, MP>& sh;
   double* g;     // this workgroup's stage records
@@ -371,17 +374,19 @@ struct Ft {
     if (k == 0) {
       if (i < sh.nf0) { const int c = sh.f0[i]; v = r[L::X + c]; lb = sh.x0lb[c]; ub = sh.x0ub[c]; }
       else { v = r[L::U + i - sh.nf0]; lb = sh.ulb[i - sh.nf0]; ub = sh.uub[i - sh.nf0]; }
-      return !(MP && isinf(lb) && isinf(ub));
+      return !(isinf(lb) && isinf(ub));
     }
     if (k == sh.N) {
       v = r[L::X + i];
       if (sh.fix[i]) { lb = -INFINITY; ub = INFINITY; return false; }
       lb = sh.xNlb[i]; ub = sh.xNub[i];
-      return !(MP && isinf(lb) && isinf(ub));
+      return !(isinf(lb) && isinf(ub));
     }
     if (i < NX) { v = r[L::X + i]; lb = sh.xlb[i]; ub = sh.xub[i]; }
     else { v = r[L::U + i - NX]; lb = sh.ulb[i - NX]; ub = sh.uub[i - NX]; }
-    return !(MP && isinf(lb) && isinf(ub));   // a free component: the Safe-MPC model's pinned dt
+    // both sides infinite: a free component (the Safe-MPC model's pinned dt; any such input of the free-time OCP),
+    // as the oracle's fcomp
+    return !(isinf(lb) && isinf(ub));
   }
   __device__ __forceinline__ double grad(int k, int i) const {
     if (MP) {   // W ([x; u] - yref) at the current iterate
@@ -418,6 +423,9 @@ struct Ft {
         sh.ulb[a] = in.lbu[(long long)pid * NU + a]; sh.uub[a] = in.ubu[(long long)pid * NU + a];
         if (!(sh.ulb[a] < sh.uub[a])) bad = 1;
       }
+      // a stage-0 row acts on the free components of x_0, and the stage-0 Riccati block carries no sigma c c' term
+      // for them: the soft rows are implemented for a fully pinned x_0 only (every Safe-MPC OCP_solve pins it)
+      if (MP && mp.soft && sh.nf0 > 0) bad = 1;
       for (int j = 0; j < NQ; ++j) sh.c0[NQ + j] = p[j];
       sh.c0[2 * NQ] = p[NQ];
       sh.cp[2 * NQ] = p[NQ];
@@ -446,10 +454,13 @@ struct Ft {
       for (int i = 0; i < NX; ++i) { r[L::PI + i] = 0.0; r[L::WPI + i] = 0.0; }
       if (k < N)
         for (int a = 0; a < NU; ++a) r[L::U + a] = ug[(long long)k * NU + a];
-      if (MP) {   // the rows' NLP multipliers and slacks start at 0 (ACADOS' nlp_out at creation); their weights
+      if (MP) {   // the rows' NLP multipliers and slacks start at 0 (ACADOS' nlp_out at creation); their weights,
+        // scaled like the stage cost they belong to (ACADOS' cost_scaling multiplies a stage's z / Z with its
+        // least-squares weights: cs on stages 0..N-1, 1 at N)
+        const double sc = k < N ? mp.cs : 1.0;
         r[L::RLL] = r[L::RLU] = r[L::RSL] = r[L::RLSL] = 0.0;
-        r[L::RZL] = (mp.soft && mp.zl) ? mp.zl[(long long)pid * (N + 1) + k] : 0.0;
-        r[L::RZ2] = (mp.soft && mp.Zl) ? mp.Zl[(long long)pid * (N + 1) + k] : 0.0;
+        r[L::RZL] = (mp.soft && mp.zl) ? sc * mp.zl[(long long)pid * (N + 1) + k] : 0.0;
+        r[L::RZ2] = (mp.soft && mp.Zl) ? sc * mp.Zl[(long long)pid * (N + 1) + k] : 0.0;
       }
     }
     __syncthreads();
@@ -1211,7 +1222,7 @@ struct Ft {
       int qit = 0;
       const int qs = qp(qit);
       qtot += qit;
-      if (qs < 0) { status = 4; break; }
+      if (qs < 0 || (MP && mp.qcf && qs == 1)) { status = 4; break; }
       weights();
       double alpha = 1.0;
       if (!rti) {

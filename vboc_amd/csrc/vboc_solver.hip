@@ -1527,6 +1527,8 @@ struct vboc_solver {
   // Safe-MPC batches (vboc_mpc_solve_batch): the free-time solver's inputs with the dt column, W1 transposed
   void* mpc_buf = nullptr;
   size_t mpc_bytes = 0;
+  void* al_buf = nullptr;           // the AL labelling batches' guesses (vboc_al_solve_batch)
+  size_t al_bytes = 0;
   // parked first solves of the data-generation loop (dg.h): their results and the two resume queues
   bool dg_park = true;
   int dg_park_window = 0;           // 0: parked problems wait until the new ones run out
@@ -1629,7 +1631,7 @@ static hipError_t launch_round(vboc_solver* h, dim3 grid, dim3 block, hipStream_
 // free-time solver: a persistent grid of one-wave workgroups, each with its own stage-record region
 template <int NQ>
 static int launch_ft(vboc_solver* h, const Inputs& in, hipStream_t st, const MpcArgs& mp = MpcArgs{}) {
-  const long long rd = FtL<NQ>::region_doubles(in.nmax);
+  const long long rd = mp.on ? FtL<NQ, true>::region_doubles(in.nmax) : FtL<NQ, false>::region_doubles(in.nmax);
   long long groups = in.B < 1024 ? in.B : 1024;
   const size_t need = (size_t)groups * (size_t)rd * sizeof(double);
   if (need > h->ft_bytes) {
@@ -1862,6 +1864,7 @@ int vboc_destroy(vboc_handle h) {
   if (h->dg_spec) (void)hipFree(h->dg_spec);
   if (h->dg_park_buf) (void)hipFree(h->dg_park_buf);
   if (h->mpc_buf) (void)hipFree(h->mpc_buf);
+  if (h->al_buf) (void)hipFree(h->al_buf);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   for (auto ev : h->pev) (void)hipEventDestroy(ev);
@@ -2284,10 +2287,74 @@ __global__ void k_transpose(int H, const double* __restrict__ a, double* __restr
 }
 
 static int mpc_solve(vboc_handle h, const vboc_mpc_batch_t* b, const vboc_mpc_soft_t* sf, void* stream,
-                     const std::string& W);
+                     const std::string& W, int qcf = 0);
 
 int vboc_mpc_solve_batch(vboc_handle h, const vboc_mpc_batch_t* b, void* stream) {
   return mpc_solve(h, b, nullptr, stream, "vboc_mpc_solve_batch");
+}
+
+// AL compute_problem (AL/triplependulum_class_al.py:148-169): every stage's x guess (q0, 0) (:157-160), u = 0 (reset)
+__global__ void k_al_guess(int B, int N, int nq, const double* __restrict__ x0, double* __restrict__ xg,
+                           double* __restrict__ ug) {
+  const int n2 = 2 * nq;
+  const long long tot = (long long)B * (N + 1);
+  for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < tot; e += (long long)gridDim.x * blockDim.x) {
+    const long long b = e / (N + 1), k = e % (N + 1);
+    for (int i = 0; i < n2; ++i) xg[e * n2 + i] = i < nq ? x0[b * n2 + i] : 0.0;
+    if (k < N)
+      for (int a = 0; a < nq; ++a) ug[(b * N + k) * nq + a] = 0.0;
+  }
+}
+// compute_problem's return value: 1 (status 0), 0 (status 4), 2 (any other status) (:164-169)
+__global__ void k_al_label(int B, const int* __restrict__ status, int* __restrict__ label) {
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
+    label[b] = status[b] == 0 ? 1 : (status[b] == 4 ? 0 : 2);
+}
+
+int vboc_al_solve_batch(vboc_handle h, const vboc_al_batch_t* b, void* stream) {
+  const std::string W = "vboc_al_solve_batch";
+  if (!h || !b) return fail(VBOC_ERR_ARG, W + ": NULL argument");
+  if (busy(h, W.c_str())) return VBOC_ERR_ARG;
+  if (b->B < 0 || b->N < 1 || b->N > h->nmax) return fail(VBOC_ERR_ARG, W + ": needs B >= 0 and 1 <= N <= nmax");
+  if (b->B == 0) { h->launches = 0; return VBOC_OK; }
+  const void* ptrs[] = {b->x0, b->lbx, b->ubx, b->lbu, b->ubu, b->lbx_e, b->ubx_e, b->W, b->We, b->label,
+                        b->status, b->x_out, b->u_out, b->qp_iter};
+  for (const void* q : ptrs)
+    if (!q) return fail(VBOC_ERR_ARG, W + ": NULL array in batch");
+  if (h->nq != 3) return fail(VBOC_ERR_UNSUPPORTED, W + ": the AL labelling OCP is the triple pendulum's (nq = 3)");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = (hipStream_t)stream;
+  constexpr int NQ = 3;
+  const size_t B = (size_t)b->B, N = (size_t)b->N;
+  // the guesses, the cost and the sqp counter the Safe-MPC call writes, in a buffer of their own (mpc_solve owns
+  // mpc_buf)
+  const size_t need = (B * (N + 1) * 2 * NQ + B * N * NQ + B) * sizeof(double) + B * sizeof(int) + 256;
+  if (need > h->al_bytes) {
+    if (h->al_buf) (void)hipFree(h->al_buf);
+    h->al_buf = nullptr;
+    h->al_bytes = 0;
+    if (hipMalloc(&h->al_buf, need) != hipSuccess) return fail(VBOC_ERR_NOMEM, W + ": hipMalloc of the guesses");
+    h->al_bytes = need;
+  }
+  double* xg = (double*)h->al_buf;
+  double* ug = xg + B * (N + 1) * 2 * NQ;
+  double* cost = ug + B * N * NQ;
+  int* sqp = (int*)(cost + B);
+  hipLaunchKernelGGL(k_al_guess, dim3(256), dim3(256), 0, st, b->B, b->N, NQ, b->x0, xg, ug);
+  HIPCHK(hipGetLastError());
+  static const double zero[3 * NQ] = {0.0};   // yref = yref_e = 0 (:114-115)
+  vboc_mpc_batch_t m{};
+  m.B = b->B; m.N = b->N; m.rti = 1; m.hidden = 0; m.h = b->h; m.cost_scale = b->cost_scale;
+  m.x0 = b->x0; m.x_guess = xg; m.u_guess = ug;
+  m.lbx = b->lbx; m.ubx = b->ubx; m.lbu = b->lbu; m.ubu = b->ubu; m.lbx_e = b->lbx_e; m.ubx_e = b->ubx_e;
+  m.W = b->W; m.We = b->We; m.yref = zero; m.yref_e = zero;
+  m.status = b->status; m.x_out = b->x_out; m.u_out = b->u_out; m.cost = cost; m.sqp_iter = sqp;
+  m.qp_iter = b->qp_iter; m.h_out = nullptr;
+  const int rc = mpc_solve(h, &m, nullptr, stream, W, 1);
+  if (rc != VBOC_OK) return rc;
+  hipLaunchKernelGGL(k_al_label, dim3(64), dim3(256), 0, st, b->B, b->status, b->label);
+  HIPCHK(hipGetLastError());
+  return VBOC_OK;
 }
 
 int vboc_mpc_soft_solve_batch(vboc_handle h, const vboc_mpc_batch_t* b, const vboc_mpc_soft_t* soft, void* stream) {
@@ -2300,7 +2367,7 @@ int vboc_mpc_soft_solve_batch(vboc_handle h, const vboc_mpc_batch_t* b, const vb
 }
 
 static int mpc_solve(vboc_handle h, const vboc_mpc_batch_t* b, const vboc_mpc_soft_t* sf, void* stream,
-                     const std::string& W) {
+                     const std::string& W, int qcf) {
   if (busy(h, W.c_str())) return VBOC_ERR_ARG;
   if (!h || !b) return fail(VBOC_ERR_ARG, W + ": NULL argument");
   if (h->nq != 3) return fail(VBOC_ERR_UNSUPPORTED, W + ": the Safe-MPC OCP is the triple pendulum's (nq = 3)");
@@ -2341,7 +2408,7 @@ static int mpc_solve(vboc_handle h, const vboc_mpc_batch_t* b, const vboc_mpc_so
                      b->lbu, b->ubu, b->lbx_e, b->ubx_e, xg7, lbx7, ubx7, lbu_b, ubu_b, lbx0, ubx0, lbxe7, ubxe7, pp,
                      Nb);
   MpcArgs mp{};
-  mp.on = 1; mp.rti = b->rti ? 1 : 0; mp.hid = b->hidden; mp.cs = b->cost_scale;
+  mp.on = 1; mp.rti = b->rti ? 1 : 0; mp.hid = b->hidden; mp.cs = b->cost_scale; mp.qcf = qcf;
   const double *Wh = b->W, *Weh = b->We, *yr = b->yref, *yre = b->yref_e;   // host constants
   for (int i = 0; i < 2 * NQ; ++i) { mp.wq[i] = Wh[i]; mp.yr[i] = yr[i]; mp.we[i] = Weh[i]; mp.yre[i] = yre[i]; }
   mp.wq[2 * NQ] = mp.yr[2 * NQ] = mp.we[2 * NQ] = mp.yre[2 * NQ] = 0.0;   // the pinned dt column carries no cost

@@ -353,15 +353,16 @@ class HipTrainer(DirTrainer):
         return out
 
 
-def make_trainer(nq, device="cpu", **kw):
-    """The fit of the VBOC loop: the native device trainer (HipTrainer) on a GPU for the shapes it implements
-    (triple 6-500, double / Cartesian 4-300, pendulum 2-100, minibatch <= 4096), else DirTrainer (PyTorch; the CPU
-    tests and the UR5's 8-1000 / 32768 fit)."""
+def make_trainer(nq, device="cpu", native=False, **kw):
+    """The fit of the VBOC loop: DirTrainer - PyTorch-ROCm, the reference's my_nn.py loop
+    (VBOC/triplependulum_vboc.py:409-468) as north_star asks - by default.  native=True selects the native device
+    trainer (HipTrainer, csrc/fit.hip) on a GPU for the shapes it implements (triple 6-500, double / Cartesian 4-300,
+    pendulum 2-100, minibatch <= 4096; tests/test_fit_device.py pins it to torch Adam); other shapes and the CPU keep
+    DirTrainer."""
     from . import fitlib
     dev = torch.device(device)
     hidden = kw.get("hidden") or HIDDEN.get(nq, 0)
     k = kw.get("minibatch") or MINIBATCH.get(nq, 0)
-    if dev.type == "cuda" and fitlib.supported(2 * nq, hidden, k):
+    if native and dev.type == "cuda" and fitlib.supported(2 * nq, hidden, k):
         return HipTrainer(nq, device, **kw)
     return DirTrainer(nq, device, **kw)
-

@@ -26,7 +26,7 @@ EXPORTS = ("vboc_create", "vboc_destroy", "vboc_set_option", "vboc_get_option", 
            "vboc_kernel_stats", "vboc_debug_counters", "vboc_data_generation", "vboc_data_generation_async",
            "vboc_data_generation_wait", "vboc_testing", "vboc_testing_test", "vboc_hjr_solve_batch",
            "vboc_set_path_constraint", "vboc_mpc_solve_batch", "vboc_mpc_soft_solve_batch",
-           "vboc_last_error")
+           "vboc_al_solve_batch", "vboc_last_error")
 
 STATUS = {0: "success", 1: "nan", 2: "max_iter", 3: "min_step", 4: "qp_failure", 5: "unsupported"}
 
@@ -88,6 +88,13 @@ class MpcSoft(ctypes.Structure):
     _fields_ = [("safety_margin", ctypes.c_double)] + [(n, ctypes.c_void_p) for n in ("Zl", "zl", "W_b", "We_b")]
 
 
+class AlBatch(ctypes.Structure):
+    """vboc_al_batch_t (include/vboc.h): AL compute_problem batch (W, We are host arrays)."""
+    _fields_ = [("B", ctypes.c_int), ("N", ctypes.c_int), ("h", ctypes.c_double), ("cost_scale", ctypes.c_double)] + \
+               [(n, ctypes.c_void_p) for n in ("x0", "lbx", "ubx", "lbu", "ubu", "lbx_e", "ubx_e", "W", "We", "label",
+                                               "status", "x_out", "u_out", "qp_iter")]
+
+
 # per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
 DG_STATS = ("solves", "rk4", "sqp_iter", "n_sqp_iter", "n_qp_iter", "t0", "t1", "first_status", "first_sqp_iter",
             "t_last_job", "spec_taken", "spec_wait", "spec_lag")
@@ -146,6 +153,7 @@ def load():
     lib.vboc_mpc_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(MpcBatch), ctypes.c_void_p]
     lib.vboc_mpc_soft_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(MpcBatch), ctypes.POINTER(MpcSoft),
                                               ctypes.c_void_p]
+    lib.vboc_al_solve_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(AlBatch), ctypes.c_void_p]
     lib.vboc_kernel_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                       ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]
     _lib = lib
@@ -428,6 +436,30 @@ class Solver:
         _check(self.lib.vboc_mpc_soft_solve_batch(self.h, ctypes.byref(b), ctypes.byref(sf),
                                                   ctypes.c_void_p(st.cuda_stream)))
         out["_keep"] = (bnd, host, W, arrs)
+        return out
+
+    def al_solve_device(self, spec, x0, stream=None):
+        """AL's OCPtriplependulumINIT.compute_problem (vboc_al_solve_batch, ft.h) for every row of the float64 cuda
+        tensor x0 [B, 6]; spec a vboc_amd.al.AlSpec.  Returns a dict of device tensors: label (1 / 0 / 2), status,
+        x [B, N+1, 6], u [B, N, 3], qp_iter."""
+        import torch
+        assert x0.is_cuda and x0.dtype == torch.float64 and x0.is_contiguous() and x0.shape[1] == 6
+        B, N, dev = x0.shape[0], spec.N, x0.device
+        f64 = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)
+        bnd = [f64(a) for a in (spec.xmin, spec.xmax, spec.umin, spec.umax, spec.xmin_e, spec.xmax_e)]
+        host = [np.ascontiguousarray(a, dtype=np.float64) for a in (spec.W, spec.W_e)]
+        out = dict(label=torch.empty(B, dtype=torch.int32, device=dev), status=torch.empty(B, dtype=torch.int32, device=dev),
+                   x=torch.empty((B, N + 1, 6), dtype=torch.float64, device=dev),
+                   u=torch.empty((B, N, 3), dtype=torch.float64, device=dev),
+                   qp_iter=torch.empty(B, dtype=torch.int32, device=dev))
+        b = AlBatch(B=B, N=N, h=spec.time_step, cost_scale=spec.cost_scale, x0=x0.data_ptr(),
+                    **{n: t_.data_ptr() for n, t_ in zip(("lbx", "ubx", "lbu", "ubu", "lbx_e", "ubx_e"), bnd)},
+                    W=host[0].ctypes.data, We=host[1].ctypes.data, label=out["label"].data_ptr(),
+                    status=out["status"].data_ptr(), x_out=out["x"].data_ptr(), u_out=out["u"].data_ptr(),
+                    qp_iter=out["qp_iter"].data_ptr())
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        _check(self.lib.vboc_al_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
+        out["_keep"] = (bnd, host, x0)
         return out
 
     def kernel_stats(self):
