@@ -177,14 +177,6 @@ __device__ __forceinline__ double wred(double v, OP op) {
   v = op(v, dppd<0xB1>(v));    // quad_perm [1,0,3,2]
   return uni(v);
 }
-#ifdef VBOC_SHFL_RED   // measurement builds: the ds_bpermute butterfly
-template <class OP>
-__device__ __forceinline__ double wred_shfl(double v, OP op) {
-  UNR for (int off = 32; off >= 1; off >>= 1) v = op(v, __shfl_xor(v, off));
-  return uni(v);
-}
-#define wred wred_shfl
-#endif
 __device__ __forceinline__ double wsum(double v) {
   return wred(v, [](double x, double y) { return x + y; });
 }
@@ -258,14 +250,6 @@ __device__ __forceinline__ void tri(int u, int& i, int& j) {
 // vboc_debug_counters().  Scalar counters (no arrays, no printf) keep the instrumented build's
 // register allocation and schedule close to the product build.
 __device__ unsigned long long g_wave_prof[16];
-__device__ unsigned g_dbg_cnt;
-// measurement builds (-DVBOC_VEC_DUMP): workgroup 0's first VBOC_VEC_DUMP_CALLS vector-pass outputs (the staged rows
-// XS[0..N][NX] and the stage-0 value), read back with vboc_debug_dump(); absent from product builds
-#ifdef VBOC_VEC_DUMP
-__device__ double g_vdump[8][1024];
-__device__ unsigned g_vdump_calls;
-__device__ double g_vdump2[8][256];   // [0, W) the landed first slot, [W, 2W) the record's window read directly, pcur
-#endif
 #ifdef VBOC_COOP_PROF
 #define CPROF_DECL unsigned long long cp0 = 0, cp1 = 0, cp2 = 0, cp3 = 0, cp4 = 0, cp5 = 0, cp6 = 0, cp7 = 0, cp8 = 0; \
   unsigned long long cp_t = __builtin_amdgcn_s_memtime();
@@ -403,30 +387,15 @@ struct Coop {
   // Issued as inline asm: with the builtin, the compiler cannot tell the ring slots apart inside the one
   // dynamic LDS array and drains every in-flight DMA (vmcnt(0)) before each ds_read of the ring.  The asm
   // op is invisible to the compiler's own VMEM count, which can then only over-wait, never under-wait.
-  // TAG: 1 factor, 2 vector pass, 4 forward sweep, 8 costate (measurement builds: -DVBOC_SBASE_DMA converts every
-  // ring to the SGPR-base form, -DVBOC_SBASE_MASK=<mask> only the rings in the mask)
+  // TAG: 1 factor, 2 vector pass, 4 forward sweep, 8 costate
   template <int TAG>
   __device__ __forceinline__ void dma(int k, int lo, int W, int dst, int part) const {
     const int nc = W / 2;
     const int c = part * 64 + t < nc ? part * 64 + t : nc - 1;
-#ifndef VBOC_SBASE_MASK
-#ifdef VBOC_SBASE_DMA
-#define VBOC_SBASE_MASK 15
-#else
-#define VBOC_SBASE_MASK 0
-#endif
-#endif
-    if constexpr ((VBOC_SBASE_MASK & TAG) != 0) {
-#ifdef VBOC_SBASE_NOHOIST
-      asm volatile("" : "+s"(k));   // measurement builds: the stage base is computed here, not hoisted / spilled
-#endif
-      dma_s(g + (long long)k * REC, 8u * (unsigned)(lo + 2 * c), dst + part * 128);
-      return;
-    }
-    // per-lane 64-bit addresses.  The SGPR-base form (dma_s, -DVBOC_SBASE_DMA) gives the pendulum chains the same
-    // bits, but deterministically broke the UR5 instantiation (k_wave<4>: 24 % status agreement with the oracle,
-    // tools/ur5_bisect.sh, profiles/r03z_ur5_sgpr_base_dma_bisect.log) for a reason not found; the grouped
-    // recursions (nq <= 3) keep dma_s
+    // per-lane 64-bit addresses.  The SGPR-base form (dma_s) gives the pendulum chains the same bits, but
+    // deterministically broke the UR5 instantiation (k_wave<4>: 24 % status agreement with the oracle,
+    // profiles/r03z_ur5_sgpr_base_dma_bisect.log, r04_ur5_bisect.json) for a reason not found;
+    // the grouped recursions (nq <= 3) keep dma_s
     const gdouble* src = g + (long long)k * REC + lo + 2 * c;
     const unsigned lds = lds0 + 8u * (unsigned)(dst + part * 128);
     unsigned keep;
@@ -446,19 +415,8 @@ struct Coop {
     // s_nop 4: an "s" operand fresh from readfirstlane / v_readlane, read by a VMEM instruction as its base, needs
     // 5 wait states that hipcc does not insert in front of inline asm (cdna_hip_programming.md, inline asm rules)
     unsigned keep;
-    // (measurement builds: -DVBOC_DMAS_PRE / -DVBOC_DMAS_POST = 16 extra wait states before the block / after the load)
-#ifdef VBOC_DMAS_PRE
-#define VBOC_DMAS_PRE_S "s_nop 7\n\ts_nop 7\n\t"
-#else
-#define VBOC_DMAS_PRE_S ""
-#endif
-#ifdef VBOC_DMAS_POST
-#define VBOC_DMAS_POST_S "s_nop 7\n\ts_nop 7\n\t"
-#else
-#define VBOC_DMAS_POST_S ""
-#endif
-    asm volatile(VBOC_DMAS_PRE_S "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
-                 VBOC_DMAS_POST_S "s_mov_b32 m0, %0"
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 4\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+                 "s_mov_b32 m0, %0"
                  : "=&s"(keep)
                  : "v"(voff), "s"(bs), "s"(lds)
                  : "memory");
@@ -476,21 +434,13 @@ struct Coop {
   // wave's own ds_reads by this wait alone)
   template <int N>
   __device__ __forceinline__ static void vmwait() {
-#ifdef VBOC_VMWAIT_DRAIN
-    // measurement builds: every counted ring wait drains (an under-counted wait can then not read a stale slot)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-#endif
   }
   // retire every ordinary VMEM op in a way the compiler's waitcnt pass sees (the builtin, vmcnt(0)):
   // called before a ring's first DMA, so no loop-carried register is still "pending" in the pass's
   // bookkeeping - otherwise it re-waits vmcnt(0) inside the loop and drains the ring every stage
   __device__ __forceinline__ static void settle() {
     __builtin_amdgcn_s_waitcnt(0x0F70);
-#ifdef VBOC_RING_ACQ
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // measurement builds: invalidate the vector L1 first
-#endif
   }
   // write fields [LO, HI) of a factor slot back to stage k's record: exactly one VMEM op
   template <int LO, int HI>
@@ -498,13 +448,7 @@ struct Coop {
     static_assert((HI - LO) / 2 <= 64 && LO % 2 == 0, "one 16-B chunk per lane");
     const dbl2* src = (const dbl2*)(s + fslot(slot));
     gdbl2* dst = (gdbl2*)(g + (long long)k * REC);
-#ifndef VBOC_WB_MASKED
-#ifdef VBOC_WB_UNMASKED_ALL
-    constexpr bool UNMASKED = true;    // measurement builds: the arm with the chains' unmasked store
-#else
-    constexpr bool UNMASKED = NQ <= 3;
-#endif
-    if constexpr (UNMASKED) {
+    if constexpr (NQ <= 3) {
       // every lane stores (lanes past the field range repeat the last chunk: same bytes, same address), no exec
       // mask: 16k first solves 4 082 -> 3 949 ms on one box, same results (profiles/r03z_wb_ab.json).  The arm
       // keeps the masked store: its k_wave<4> lost parity with the unmasked one
@@ -513,31 +457,9 @@ struct Coop {
       dst[LO / 2 + c] = src[LO / 2 + c];
       return;
     }
-#endif
     if (t < (HI - LO) / 2) dst[LO / 2 + t] = src[LO / 2 + t];
   }
 
-  // debug (-DVBOC_DBG_CHECK): compare a landed ring window with a direct global read of the same fields
-  // (-DVBOC_DBG_TAGS=mask limits it to the rings whose tag bit is set: 1 factor, 2 vec, 3 fwd, 4 costate)
-  __device__ __forceinline__ void dbg_check(int kb, int k, int lo, int W, int tag) const {
-#if defined(VBOC_DBG_CHECK) && defined(VBOC_DBG_TAGS)
-    if (!((VBOC_DBG_TAGS >> tag) & 1)) return;
-#endif
-#ifdef VBOC_DBG_CHECK
-    int bad = -1;
-    double a0 = 0.0, b0 = 0.0;
-    for (int e = t; e < W; e += 64) {
-      const double a = s[kb + e], b = st(k, lo + e);
-      if (__double_as_longlong(a) != __double_as_longlong(b) && bad < 0) { bad = e; a0 = a; b0 = b; }
-    }
-    if (bad >= 0) {
-      const unsigned c = atomicAdd(&g_dbg_cnt, 1u);
-      if (c < 40) printf("tag %d lane %d k %d N %d off %d lds %.17g glob %.17g\n", tag, t, k, N, bad, a0, b0);
-    }
-#else
-    (void)kb; (void)k; (void)lo; (void)W; (void)tag;
-#endif
-  }
 
   // box of component i of stage k (the Lane::stage_box pattern)
   __device__ __forceinline__ bool box(int k, int i, double& lb, double& ub) const {
@@ -1145,7 +1067,6 @@ struct Coop {
       // counting them (2P + 1 / 2P + 2, as before) let the wait pass with the last part of stage k's window
       // still in flight whenever they completed first
       vmwait<2 * P>();
-      dbg_check(kb, k, 0, L::W_FAC, 1);
       SPROF(3)
       if (k >= 1) {
         dstep<NX, 0>(d1, kb);
@@ -1198,16 +1119,11 @@ struct Coop {
   // stage's outputs (ring_wb<OK, OX>: K .. Pe, C (dead until vec rebuilds it), A_cl): no acl_pass re-reading A, B
   // and K from the stage records.  Per chain (bit NQ of VBOC_ACL_FUSED_NQ): the triple only - the fusion makes the
   // triple's data-generation launch 2.4 % faster (profiles/r04_bytes_ab.json) but the double's 10k launches 4.3 %
-  // (dg loop) / 10.2 % (first solves) slower (profiles/r05_double_acl_ab.json).  -DVBOC_ACL_PASS: the separate pass
-  // for every chain (measurement builds).
+  // (dg loop) / 10.2 % (first solves) slower (profiles/r05_double_acl_ab.json).
 #ifndef VBOC_ACL_FUSED_NQ
 #define VBOC_ACL_FUSED_NQ (1 << 3)
 #endif
-#ifdef VBOC_ACL_PASS
-  static constexpr bool ACL_FUSED = false;
-#else
   static constexpr bool ACL_FUSED = FM && ((VBOC_ACL_FUSED_NQ >> NQ) & 1);
-#endif
   // factor_mfma's junk target: lanes without an output write the slot's tail past the written-back fields
   static constexpr int FJUNK = L::OX;
   static constexpr bool MFMA_OK = (NX <= 8) && (CP + NQ <= 16) && (FJUNK + 2 * NX + 2 <= L::RSF);
@@ -1338,7 +1254,6 @@ struct Coop {
       fdma(j + 2);
       FS5(1)
       vmwait<2 * P>();   // loads only, as in factor()
-      dbg_check(kb, k, 0, WF, 1);
       FS4(0)
       FS5(2)
       // the three operand reads issue back to back (one LDS latency, not three)
@@ -1419,11 +1334,9 @@ struct Coop {
         w[a] = tt * id[a];
       }
       }
-#ifndef VBOC_FAC_NOSB
       // the recursion's state update issues before the stage's outputs (they are off the critical path):
       // the empty asm keeps the MFMA from being sunk to the loop latch
       asm volatile("" : "+v"(Dm));
-#endif
       FS4(2)
       // outputs of stage k into its ring slot: K = -Ru^-1 S, M = Ru^-1 Y, chol(Ru) (RINV: Ru^-1), Y, P e
       UNR for (int a = 0; a < NU; ++a) {
@@ -1632,21 +1545,6 @@ struct Coop {
       UNR for (int d = 0; d < L::DV; ++d) vdma(d);
       vmwait<(L::DV - 1) * PV>();
       vld(vslot(0), acl, cc, pe);
-#ifdef VBOC_VEC_DUMP
-      if (blockIdx.x == 0) {
-        unsigned call = 0;
-        if (t == 0) call = __hip_atomic_load(&g_vdump_calls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        call = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl((int)call, 0));
-        if (call < 8) {
-          const int k0 = N - 1 >= 1 ? N - 1 : 1;
-          for (int e = t; e < L::W_VEC; e += 64) {
-            g_vdump2[call][e] = s[vslot(0) + e];
-            g_vdump2[call][L::W_VEC + e] = st(k0, L::LO_VEC + e);
-          }
-          if (t < NX) g_vdump2[call][2 * L::W_VEC + t] = pcur;
-        }
-      }
-#endif
     }
     // p_{k+1} reaches every lane by readlane (lane q holds component q): the recursion's dependent chain
     // carries no LDS round trip
@@ -1656,7 +1554,6 @@ struct Coop {
       const int k = N - 1 - j;
       vdma(j + L::DV);
       vmwait<(L::DV - 1) * PV>();   // stage of sweep index j + 1 has landed
-      dbg_check(vslot((j + 1) % L::NSV), N - 2 - j >= 1 ? N - 2 - j : 1, L::LO_VEC, L::W_VEC, 2);
       double an[NX], cn, pn;
       vld(vslot((j + 1) % L::NSV), an, cn, pn);
       __builtin_amdgcn_sched_barrier(0);
@@ -1673,18 +1570,6 @@ struct Coop {
     }
     if (t < NX) s[L::PV + t] = pcur;
     __syncthreads();
-#ifdef VBOC_VEC_DUMP
-    if (blockIdx.x == 0) {
-      unsigned call = 0;
-      if (t == 0) call = atomicAdd(&g_vdump_calls, 1u);
-      call = (unsigned)__builtin_amdgcn_readfirstlane((int)__shfl((int)call, 0));
-      if (call < 8) {
-        for (int e = t; e < (N + 1) * NX && e < 1016; e += 64) g_vdump[call][e] = s[L::XS + e];
-        if (t < NX) g_vdump[call][1016 + t] = s[L::PV + t];
-      }
-      __syncthreads();
-    }
-#endif
     SPROF(1)
     // k_f = -Ru^-1 (g_u + B'v) per stage, lin = sum Y'k_f  (stage-parallel)
     double lin[NQ];
@@ -1890,7 +1775,6 @@ struct Coop {
         const int k = 1 + j;
         wdma(j + L::DV);
         vmwait<(L::DV - 1) * PW>();
-        dbg_check(vslot((j + 1) % L::NSV), 2 + j < N ? 2 + j : N - 1, L::LO_FWD, L::W_FWD, 3);
         double an[NX], cn;
         fld(vslot((j + 1) % L::NSV), an, cn);
         __builtin_amdgcn_sched_barrier(0);
@@ -2084,7 +1968,6 @@ struct Coop {
       const int rb = L::DXV + (j & 1) * NX, wb = L::DXV + ((j + 1) & 1) * NX;
       cdma(j + L::DV);
       vmwait<(L::DV - 1) * PC>();
-      dbg_check(vslot((j + 1) % L::NSV), N - 2 - j >= 1 ? N - 2 - j : 1, 0, L::W_COS, 4);
       double lam[NX], an[NX], cn;
       UNR for (int q = 0; q < NX; ++q) lam[q] = s[rb + q];
       cterms(vslot((j + 1) % L::NSV), an, cn);
@@ -2145,11 +2028,7 @@ struct Coop {
     // VGPR lanes, VGPRs to AGPRs) under a partial exec mask, and that build returned wrong merit values on a
     // few problems per batch: longer line searches than the oracle's, 3 % SQP-iteration agreement
     // (profiles/r02p_ur5_merit_bisect.log).
-#ifdef VBOC_MERIT_PARTIAL_EXEC
-    constexpr bool UNI = false;   // reproducer build of the round-2 defect (tools/ur5_merit_repro.sh)
-#else
     constexpr bool UNI = NQ == 4;
-#endif
     for (int k0 = UNI ? 0 : t; k0 <= N; k0 += 64) {
       const bool live = !UNI || k0 + t <= N;
       const int k = UNI ? (live ? k0 + t : N) : k0;
@@ -2355,20 +2234,6 @@ void k_wave(Work w, Opts o, Inputs in, SlotState ss, WaveJobs jb) {
   const int t = (int)threadIdx.x;
   Coop<NQ, FM, HC> C(smem, gptr(jb.regions) + (long long)blockIdx.x * jb.region_doubles, w, o, t);
   if constexpr (HC) C.gh = gptr(jb.hc) + (long long)blockIdx.x * jb.hc_doubles;
-#if defined(VBOC_LDS_ZERO) || defined(VBOC_LDS_NAN)
-  {   // measurement builds: fill the workgroup's LDS before the first job (uninitialised-LDS reads then show)
-    using LL = WaveLayout<NQ>;
-    const long long nm = jb.region_doubles / LL::REC - 1 - LL::SLACK;
-    const int n = LL::XS + (int)(nm + 1) * LL::NX;
-#ifdef VBOC_LDS_NAN
-    const double fill = __builtin_nan("");
-#else
-    const double fill = 0.0;
-#endif
-    for (int e = t; e < n; e += 64) smem[e] = fill;
-    __syncthreads();
-  }
-#endif
   for (;;) {
     unsigned idx = 0;
     if (t == 0) idx = atomicAdd(jb.next, 1u);

@@ -65,9 +65,6 @@ struct DgJobs {
   int spec_events, spec_stride;   // events in the pool, doubles per event
   int spec_early;                 // once at most this many problems are left unclaimed, queued restart jobs go first
   int spec_first;                 // 1: once the new problems run out, queued restart jobs go before parked resumes
-#ifdef VBOC_SPEC_MIN_EXT
-  int spec_min_ext;               // (measurement builds) a failed chain publishes restart jobs only from this solve on
-#endif
   double* spec;                   // [spec_events][spec_stride]: snapshot header, then DG_SPEC_JOBS results
   int* spec_claim;                // [spec_events][DG_SPEC_JOBS + 1]: 0 free, 1 claimed
   int* spec_done;                 // [spec_events][DG_SPEC_JOBS + 1]: 1 = result written
@@ -707,11 +704,7 @@ struct Dg {
             take_result(ev, j, N);
             return 2;
           }
-#ifdef VBOC_SPEC_MIN_EXT
-        } else if (ev < 0 && s->ext >= J.spec_min_ext) {
-#else
         } else if (ev < 0) {
-#endif
           spawn(att, N);
         }
         crit_check(s->spec_ev);

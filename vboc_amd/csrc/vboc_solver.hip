@@ -1518,7 +1518,6 @@ struct vboc_solver {
   int dg_spec_first = 2;
   bool dg_spec_crit = false;        // critical-path rule for the eager restart queue (dg.h crit_check)
   int dg_spec_window = 0;           // eager window: a chain's next attempts that go before every problem (dg.h; off: measured slower)
-  int dg_spec_min_ext = 0;          // (-DVBOC_SPEC_MIN_EXT builds) restart jobs only from this extension solve on
   double* wave_hc = nullptr;        // path-constraint rows of the wave solver, one region per workgroup
   long long wave_hc_doubles = 0;
   bool hc_wave = true;              // constrained problems on the wave solver (k_wave<NQ, false, true>)
@@ -1908,9 +1907,6 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "dg_park") h->dg_park = v != 0.0;
   else if (s == "dg_park_window") h->dg_park_window = v > 0.0 ? (int)v : 0;
   else if (s == "dg_park_hi") h->dg_park_hi = v > 0.0 ? (int)v : 0;
-#ifdef VBOC_SPEC_MIN_EXT
-  else if (s == "dg_spec_min_ext") h->dg_spec_min_ext = v > 0.0 ? (int)v : 0;
-#endif
   else if (s == "hc_wave") h->hc_wave = v != 0.0;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
@@ -2116,22 +2112,6 @@ int vboc_debug_counters(unsigned long long* out16) {
   static const unsigned long long zero[16] = {0};
   HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_wave_prof), zero, sizeof(zero)));
   return VBOC_OK;
-}
-
-// measurement builds (-DVBOC_VEC_DUMP, coop.h): the dumped vector-pass outputs [8][1024], then [8][256] of the first
-// landed slot / its record window / pcur, and the call count (reset)
-int vboc_debug_dump(double* out8k, unsigned* calls) {
-  if (!out8k || !calls) return fail(VBOC_ERR_ARG, "vboc_debug_dump: NULL argument");
-#ifndef VBOC_VEC_DUMP
-  return fail(VBOC_ERR_UNSUPPORTED, "vboc_debug_dump: a measurement build (-DVBOC_VEC_DUMP) only");
-#else
-  HIPCHK(hipMemcpyFromSymbol(out8k, HIP_SYMBOL(g_vdump), 8 * 1024 * sizeof(double)));
-  HIPCHK(hipMemcpyFromSymbol(calls, HIP_SYMBOL(g_vdump_calls), sizeof(unsigned)));
-  HIPCHK(hipMemcpyFromSymbol(out8k + 8 * 1024, HIP_SYMBOL(g_vdump2), 8 * 256 * sizeof(double)));
-  const unsigned z = 0;
-  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_vdump_calls), &z, sizeof(z)));
-  return VBOC_OK;
-#endif
 }
 
 int vboc_last_kernel_ms(vboc_handle h, double* ms, int* launches) {
@@ -2549,9 +2529,6 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   J.spec_count = (unsigned long long*)(h->head + 10);
   // speculative restarts: one event per failed horizon-extension chain, at most min(B, 8192) per launch
   J.spec_events = 0; J.spec_stride = 0; J.spec = nullptr; J.spec_early = h->dg_spec_early; J.spec_first = (h->dg_spec_first == 1 || (h->dg_spec_first == 2 && (long long)b->B < 128 * groups)) ? 1 : 0;
-#ifdef VBOC_SPEC_MIN_EXT
-  J.spec_min_ext = h->dg_spec_min_ext;
-#endif
   J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = J.spec_eq = nullptr;
   J.spec_window = 0; J.spec_eq_tail = h->head + 20; J.spec_eq_head = h->head + 21;
   J.spec_crit = 0; J.t_launch = (unsigned long long*)(h->head + 22);   // [22..23]

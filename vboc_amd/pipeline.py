@@ -187,6 +187,9 @@ class StreamedRounds:
         self.host_flags = torch.zeros(max(self.sizes + [1]), dtype=torch.int32).pin_memory()
         torch.cuda.synchronize(dev)
         self.t_start = time.time()
+        # jobs in round order: a round's restart chains and parked resumes go before a later round's new problems
+        # (dg.h round gate), so the rounds complete in order while the launch keeps every wave busy
+        solver.set_option("dg_round", max(self.sizes))
         self.out = solver.data_generation_device(self.ids, N_start=N_start, seed=seed, rows_cap=B * rpp,
                                                  stream=self.producer, done_flag=self.flags, cancel=self.cancel_word,
                                                  wait=False)
