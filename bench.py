@@ -183,8 +183,6 @@ class GpuEngine:
         self.solver.set_option("dg_spec_crit", getattr(args, "spec_crit", 0))
         if getattr(args, "wave_groups", 0):   # resident problems (default: sized to the 256 MiB MALL)
             self.solver.set_option("wave_groups", args.wave_groups)
-        if getattr(args, "spec_min_ext", 0):   # measurement builds only (a VBOC_LIB variant; profiles/r03z_spec_early_ab.json)
-            self.solver.set_option("dg_spec_min_ext", args.spec_min_ext)
         self.stream = torch.cuda.current_stream(self.device)
         self.kernel = {("dg-loop", "wave"): f"k_dg<{nq}>", ("first-solve", "wave"): f"k_wave<{nq}>",
                        ("first-solve", "lane"): f"k_qp_factor<{nq}>"}[(args.workload, args.mode)]
@@ -284,8 +282,6 @@ def parse(argv=None):
                          "configs[2] round; DESIGN.md section 14)")
     ap.add_argument("--spec-crit", type=int, default=0,
                     help="dg-loop: 1 = the critical-path rule for speculative restarts (DESIGN.md section 14)")
-    ap.add_argument("--spec-min-ext", type=int, default=0,
-                    help="dg-loop: a failed horizon-extension chain publishes speculative restarts only from this solve on")
     ap.add_argument("--mode", choices=("wave", "lane"), default="wave",
                     help="first-solve: wave (one problem per wave, default) or lane (lane-per-problem kernels)")
     ap.add_argument("--wave-groups", type=int, default=0,

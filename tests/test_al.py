@@ -115,11 +115,7 @@ def test_gpu_testing_driver_reproduces_fixture():
     from vboc_amd.al import OCPtriplependulumINIT
     g = json.load(open(os.path.join(HERE, "golden", "al_testing_3.json")))
     ocp = OCPtriplependulumINIT()
-
-    def fn(X):
-        r = ocp.compute_problem_batch(X)
-        return r["label"], r["x"]
-    got = al_testing_batch(ocp.spec, np.array(g["X"]), fn)
+    got = al_testing_batch(ocp.spec, np.array(g["X"]), ocp.labels)
     for b, (a, ref) in enumerate(zip(got, g["results"])):
         if ref is None:
             assert a is None, b

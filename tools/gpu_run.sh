@@ -3,6 +3,8 @@
 # limit, and the call stops at the first failing step (no GPU step after a fault, an abort or a timeout):
 #   tests[=<pytest -k expr>]  the GPU suite (or a -k selection of it), parity records to <out>/parity
 #   tests_file=<path,...>     GPU test files
+#   tests_lib=<name>:<files>[:<-k expr>]  GPU test files (comma-separated) on vboc_amd/ab/libvboc_amd_<name>.so
+#                             (VBOC_LIB): the parity suite on a variant build, parity records to <out>/parity_<name>
 #   smoke                     __graft_entry__.smoke()
 #   bench                     the driver's command (bench.py --steps 20 --warmup 5) -> <out>/bench.json
 #   prof                      the same command under rocprofv3 --kernel-trace --stats -> <out>/prof
@@ -32,6 +34,11 @@ for step in "$@"; do
                --timeout-method thread -k "${step#tests=}" > $O/pytest_sel.log 2>&1;;
     tests_file=*) run tests_file 900 env VBOC_PARITY_OUT=$O/parity python -u -m pytest $(echo ${step#tests_file=} | tr , ' ') -m gpu \
                     -x -v --timeout 300 --timeout-method thread > $O/pytest_file.log 2>&1;;
+    tests_lib=*) spec=${step#tests_lib=}; n=${spec%%:*}; rest=${spec#*:}; files=${rest%%:*}; k=""
+                 [ "$rest" != "$files" ] && k=${rest#*:}
+                 run "tests_lib $n" 900 env VBOC_LIB=$R/vboc_amd/ab/libvboc_amd_$n.so VBOC_PARITY_OUT=$O/parity_$n \
+                   python -u -m pytest $(echo $files | tr , ' ') -m gpu -x -v --timeout 300 --timeout-method thread \
+                   ${k:+-k "$k"} > $O/pytest_lib_$n.log 2>&1;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1;;
     bench) run bench 420 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err; cat $O/bench.json;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 420 rocprofv3 --kernel-trace --stats --output-format csv \

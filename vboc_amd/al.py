@@ -95,6 +95,11 @@ class OCPtriplependulumINIT:
         torch.cuda.synchronize(dev)
         return {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
 
+    def labels(self, X):
+        """(labels [B], trajectories [B, N+1, 6]) of compute_problem for every state of X: testing_batch's label_fn."""
+        r = self.compute_problem_batch(X)
+        return r["label"], r["x"]
+
     def compute_problem(self, q0, v0):
         x0 = np.array([q0[0], q0[1], q0[2], v0[0], v0[1], v0[2]], dtype=np.float64)   # :152
         r = self.compute_problem_batch(x0[None])

@@ -89,6 +89,10 @@ struct DgJobs {
   int park_window;                // new problems go first while fewer than this many parked problems wait
   int park_hi_it;                 // first solves with >= this many SQP iterations resume first (queue 0)
   int* park_q;                    // [2][count]: queues 0 (high) and 1 of job + 1, 0 = not yet written
+  // round gate of a streamed launch (pipeline.StreamedRounds, option dg_round; 0 off): jobs are the rounds' problems
+  // in order, round_n per round; a parked resume or queued restart attempt of a round before the next new problem's
+  // round goes before that new problem, so the rounds complete in order
+  int round_n;
   unsigned* park_tail;            // [2] entries pushed
   unsigned* park_head;            // [2] entries taken
 };
@@ -550,7 +554,7 @@ struct Dg {
   // success.  Results are those of the sequential chain (same inputs, same deterministic solver); unused
   // speculative solves are counted apart (spec_count) and never in the solve statistics.
   enum : int { H_N = 0, H_JS, H_VS, H_QIS, H_QFS, H_RAN, H_QO = H_RAN + 2, H_IC, H_RNG = H_IC + 4, H_PID, H_NJOBS,
-               H_TS, H_P, H_LB = H_P + NP, H_UB = H_LB + NXR, H_END = H_UB + NXR };
+               H_TS, H_P, H_LB = H_P + NP, H_UB = H_LB + NXR, H_JOB = H_UB + NXR, H_END };
   static_assert(H_END <= DG_SPEC_HDR, "event header");
   __device__ __forceinline__ double* spec_hdr(int ev) const { return J.spec + (long long)ev * J.spec_stride; }
   __device__ __forceinline__ double* spec_res(int ev, int j) const {
@@ -583,6 +587,7 @@ struct Dg {
     UNR for (int c = 0; c < 4; ++c) st_coh(h + H_IC + c, s->store_ic[c]);
     st_coh(h + H_RNG, s->rng_pos); st_coh(h + H_PID, (double)pid); st_coh(h + H_NJOBS, nj);
     st_coh(h + H_TS, (double)__builtin_amdgcn_s_memrealtime());
+    st_coh(h + H_JOB, (double)job);
     UNR for (int c = 0; c < NP; ++c) st_coh(h + H_P + c, P[c]);
     UNR for (int c = 0; c < NXR; ++c) { st_coh(h + H_LB + c, lb0[c]); st_coh(h + H_UB + c, ub0[c]); }
     if (t == 0) {
@@ -1026,6 +1031,29 @@ __device__ __forceinline__ unsigned dg_parked_waiting(const DgJobs* J) {
   return w;
 }
 
+// lane 0, round gate (J->round_n > 0): a parked job of a round before round r waits at the head of a park queue
+__device__ __forceinline__ bool dg_parked_before(const DgJobs* J, unsigned r) {
+  for (int q = 0; q < 2; ++q) {
+    const unsigned h = __hip_atomic_load(&J->park_head[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (h >= __hip_atomic_load(&J->park_tail[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
+    const int e = ld_flag(&J->park_q[(long long)q * J->count + h]);
+    if (e > 0 && (unsigned)(e - 1) / (unsigned)J->round_n < r) return true;
+  }
+  return false;
+}
+// lane 0, round gate: the restart attempt at the head of the lazy queue belongs to a chain of a round before round r
+template <int NQ>
+__device__ __forceinline__ bool dg_restart_before(const DgJobs* J, unsigned r) {
+  const unsigned h = __hip_atomic_load(J->spec_q_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (h >= __hip_atomic_load(J->spec_q_tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+  const int e = ld_flag(&J->spec_q[h]);
+  if (e <= 0) return false;
+  after_flag();
+  const int ev = (e - 1) / (DG_SPEC_JOBS + 1);
+  const double job = ld_coh(J->spec + (long long)ev * J->spec_stride + Dg<NQ>::H_JOB);
+  return (unsigned)job / (unsigned)J->round_n < r;
+}
+
 // one workgroup = one wave: it owns one problem's whole data_generation at a time, or - once the problem
 // queue is drained - runs one speculative restart solve for another problem's owner (they shorten the
 // chains of failing solves that make the launch tail).  `in` is the Inputs batch of one problem per workgroup (the wave solver works on problem index wg
@@ -1095,12 +1123,23 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
       }
       pre = dg_bcast(pre);
     }
+    //    Round gate (streamed launches): a restart attempt of an earlier round's chain goes before a later round's new
+    //    problem
+    if (mode == 0 && spec && !pre && J->round_n > 0) {
+      if (t == 0) {
+        const unsigned nx = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pre = nx < (unsigned)count && dg_restart_before<NQ>(J, nx / (unsigned)J->round_n);
+      }
+      pre = dg_bcast(pre);
+    }
     // 1. the next problem: a new one, or a parked one once the new ones run out or park_window parked ones wait
     if (mode == 0 && !pre) {
       int got = -1, res = 0;
       if (t == 0) {
-        const bool more = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)count;
-        if (park && (!more || dg_parked_waiting(J) >= (unsigned)J->park_window)) {
+        const unsigned nx = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool more = nx < (unsigned)count;
+        if (park && (!more || dg_parked_waiting(J) >= (unsigned)J->park_window ||
+                     (J->round_n > 0 && dg_parked_before(J, nx / (unsigned)J->round_n)))) {
           got = dg_take_parked(J);
           res = got >= 0;
         }

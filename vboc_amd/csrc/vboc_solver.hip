@@ -1532,6 +1532,7 @@ struct vboc_solver {
   bool dg_park = true;
   int dg_park_window = 0;           // 0: parked problems wait until the new ones run out
   int dg_park_hi = 100;             // first solves with >= this many SQP iterations resume first
+  int dg_round = 0;                 // streamed launches: problems per round of the round gate (dg.h DgJobs::round_n)
   void* dg_park_buf = nullptr;
   size_t dg_park_bytes = 0;
   // a vboc_data_generation_async launch is running on this handle's buffers (dg_scratch, regions, head counters)
@@ -1907,6 +1908,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "dg_park") h->dg_park = v != 0.0;
   else if (s == "dg_park_window") h->dg_park_window = v > 0.0 ? (int)v : 0;
   else if (s == "dg_park_hi") h->dg_park_hi = v > 0.0 ? (int)v : 0;
+  else if (s == "dg_round") h->dg_round = v > 0.0 ? (int)v : 0;
   else if (s == "hc_wave") h->hc_wave = v != 0.0;
   else if (s == "profile_kernels") {
     h->profile = v != 0.0;
@@ -1949,6 +1951,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "dg_park") *v = h->dg_park ? 1.0 : 0.0;
   else if (s == "dg_park_window") *v = (double)h->dg_park_window;
   else if (s == "dg_park_hi") *v = (double)h->dg_park_hi;
+  else if (s == "dg_round") *v = (double)h->dg_round;
   else if (s == "hc_wave") *v = h->hc_wave ? 1.0 : 0.0;
   else if (s == "factor_mfma") *v = h->factor_mfma ? 1.0 : 0.0;
   else if (s == "wave_groups") *v = (double)h->n_regions;
@@ -2562,6 +2565,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   // parked first solves (data generation only): one result record per job, two queues, counters head[16..19]
   J.park_res = nullptr; J.park_q = nullptr; J.park_stride = 0;
   J.park_window = 0; J.park_hi_it = h->dg_park_hi;
+  J.round_n = done_flag ? h->dg_round : 0;   // the round gate belongs to streamed launches (done flags) only
   J.park_tail = h->head + 16; J.park_head = h->head + 18;
   if (h->dg_park && !testing) {
     const int stride = (8 + (b->N_start + 1) * NXR + b->N_start * NU + 1) & ~1;
