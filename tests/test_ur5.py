@@ -298,8 +298,13 @@ def test_ur5_driver_on_gpu_matches_reference():
 
 @pytest.mark.gpu
 def test_ur5_full_batch_properties():
-    """4096 first solves: converged solutions are dynamically feasible (re-simulated with the ORACLE's RK4 on
-    a sample, the GPU twin on all), inside the boxes, at rest at N, start along p, cost = p . qdot_0."""
+    """4096 first solves at nlp_solver_max_iter 100 (a truncated budget that keeps the test short): the statuses are
+    the CPU oracle's problem by problem (tests/golden/ur5_status_4096.json, tools/ur5_converged_share.py: 81.7 %
+    converged, 680 stopped at the 100-iteration cap - still iterating, not failed - and 69 QP failures) on >= 98 % of
+    the problems and the converged share within 0.5 % of the oracle's; converged solutions are dynamically feasible
+    (re-simulated with the ORACLE's RK4 on a sample, the GPU twin on all), inside the boxes, at rest at N, start
+    along p, cost = p . qdot_0."""
+    import json
     import oracle
     from vboc_amd import lib
     from vboc_amd.ics import ur5_ics
@@ -307,7 +312,10 @@ def test_ur5_full_batch_properties():
     b = ur5_ics(np.arange(10**6, 10**6 + 4096))
     g = _gpu_solve(b, nlp_solver_max_iter=100)
     ok = g["status"] == 0
-    assert ok.mean() > 0.5
+    ref = np.array(json.load(open(os.path.join(HERE, "golden", "ur5_status_4096.json")))["status"])
+    print(f"converged: GPU {ok.mean():.4f}, oracle {(ref == 0).mean():.4f}; same status {np.mean(g['status'] == ref):.4f}")
+    assert np.mean(g["status"] == ref) >= 0.98
+    assert abs(ok.mean() - (ref == 0).mean()) <= 0.005
     X, U = g["x"][ok, :, :8], g["u"][ok]
     N = 100
     x1 = lib.rk4_host(4, 1e-2, X[:, :N].reshape(-1, 8), U[:, :N].reshape(-1, 4)).reshape(-1, N, 8)

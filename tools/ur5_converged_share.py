@@ -1,7 +1,8 @@
 """The CPU oracle's converged share on test_ur5_full_batch_properties's 4096 UR5 first solves (ids 10^6 .. +4095,
 nlp_solver_max_iter 100), the bar that test holds the GPU solver to (verdict r05 item 7).  Also the status histogram
 and the SQP-iteration distribution of the unconverged ones (they are max_iter stops: the truncated budget, not
-failures).  usage: python tools/ur5_converged_share.py [out.json]"""
+failures).  Writes the per-problem statuses to tests/golden/ur5_status_4096.json (the GPU test compares problem by
+problem).  usage: python tools/ur5_converged_share.py [out.json]"""
 import json
 import os
 import sys
@@ -28,8 +29,11 @@ def main():
                sqp_iter_converged_p50_p99=[float(np.percentile(r["sqp_iter"][st == 0], q)) for q in (50, 99)],
                seconds=time.time() - t, threads=os.cpu_count(), status=st.tolist())
     print(json.dumps({k: v for k, v in out.items() if k != "status"}))
+    json.dump({"ids_first": 10**6, "n": 4096, "nlp_solver_max_iter": 100, "levenberg_marquardt": 1e-2,
+               "generator": "tools/ur5_converged_share.py (oracle/, CPU)", "status": out.pop("status")},
+              open(os.path.join(ROOT, "tests", "golden", "ur5_status_4096.json"), "w"))
     if len(sys.argv) > 1:
-        json.dump(out, open(sys.argv[1], "w"))
+        json.dump(out, open(sys.argv[1], "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -290,20 +290,22 @@ __device__ unsigned long long g_wave_prof[16];
 
 // Pass fusions of the IPM iteration (round 5; pendulum chains with the MFMA factorisation, no path constraint - the
 // instantiations of the data-generation loop and the first solves).  Each removes stage-record traffic (a pass or
-// part of a window) with the same arithmetic in the same order, so results are bit-identical; -DVBOC_FUSE=<mask>
-// selects them for measurements (0: the round-4 passes).
+// part of a window); -DVBOC_FUSE=<mask> selects them for measurements (0: the round-4 passes).  1, 4 and 8 keep the
+// arithmetic and its order (bit-identical); 2 re-associates at rounding level and is accepted under the tolerance
+// parity rule of round 6.
 //   1 FAC1   the factorisation's window is its inputs [A, K) - one LDS-DMA per stage instead of two ([K, C) was
 //            loaded only to be overwritten by the stage's outputs before the write-back);
 //   2 PFUSE  the predictor preparation (D = H, DA = predictor gradient) is computed by the iterate update of the
-//            previous IPM iteration from the values it has just written (prep_pred runs for the first only) - OFF:
-//            not bit-identical on the box (another digest of the 100k-problem launch, gpurun_out/r05a; the compiler
-//            contracts the inlined copy differently), +0.4 % bulk rate alone;
+//            previous IPM iteration from the values it has just written (prep_pred runs for the first only); the
+//            compiler contracts the inlined copy differently (rounding level; round 5 dropped it on the digest);
+//            with RINV below +2.1 % bulk rate, -3.2 % kernel time on 200k problems (same box, bracketed,
+//            profiles/r06_probe_pfuse_rinv_ab.jsonl), parity suite green (profiles/r06_pytest_gpu_parity_pfuse_rinv.log);
 //   4 CCORR  the corrector gradient pass also forms the corrector vector pass's constant c' (vec's stage-parallel
 //            pre-pass re-read the gradient with K, A_cl, P e);
 //   8 KFM    the forward sweep's constant pass stores k_f - M nu over k_f, and the step-length pass reads it instead
 //            of re-reading M and chol(Ru) to recompute it.
 #ifndef VBOC_FUSE
-#define VBOC_FUSE 13
+#define VBOC_FUSE 15
 #endif
 
 // HC: the Cartesian path-constraint rows (vboc_set_path_constraint; oracle/vboc_oracle.c hc_*, Lane::hc_*) on
@@ -1130,15 +1132,14 @@ struct Coop {
   // H_u rows NX .. NX+NU-1 live in accumulator registers HR0, HR0 + 1; the LDS image keeps those two
   // registers of every lane group: image row (row & 3) + 4 * ((row >> 2) - HR0)
   static constexpr int HR0 = NX >> 2;
-  // -DVBOC_RINV (measurement builds): factor_mfma stores Ru^-1 in closed form instead of chol(Ru) for the
-  // triple, vec's k_f reads it as such.  Off in the product: 2 % less kernel time on 16k first solves, but a
-  // rounding-level change that flips one tolerance decision of the reference fixture's 12 data-generation
-  // problems (profiles/r03z_rinv_ab.json)
-#ifdef VBOC_RINV
-  static constexpr bool RINV = FM && NU == 3;
-#else
-  static constexpr bool RINV = false;
+  // RINV: factor_mfma stores Ru^-1 in closed form instead of chol(Ru) for the triple, vec's k_f reads it as such
+  // (the factorisation -4.9 % cycles, profiles/r05_factor_loop_experiments.json).  A rounding-level change (round 3 /
+  // 5 kept it off because a digest or one tolerance decision moved, profiles/r03z_rinv_ab.json); on since round 6
+  // under the tolerance parity rule, with PFUSE above.  -DVBOC_RINV=0: the Cholesky form.
+#ifndef VBOC_RINV
+#define VBOC_RINV 1
 #endif
+  static constexpr bool RINV = VBOC_RINV && FM && NU == 3;
   static_assert(((NX + NU - 1) >> 2) <= HR0 + 1, "H_u spans two accumulator registers");
   __device__ __forceinline__ static constexpr int hrow(int row) { return (row & 3) + 4 * ((row >> 2) - HR0); }
   // The loop body is written for a low VALU count (the wave solver is VALU-issue bound): loop-invariant
