@@ -171,10 +171,6 @@ class GpuEngine:
         import torch
         from vboc_amd import lib
         self.torch, self.lib = torch, lib
-        # rank -> GPU: LOCAL_RANK.  VBOC_RANKS_SHARE_GPUS=1 (rehearsals on a box with fewer GPUs than ranks, never the
-        # driver's runs): LOCAL_RANK modulo the visible GPUs, so the N-rank RCCL path runs with ranks sharing a device
-        if os.environ.get("VBOC_RANKS_SHARE_GPUS") == "1":
-            local = local % max(1, torch.cuda.device_count())
         self.device = torch.device("cuda", local)
         torch.cuda.set_device(self.device)
         nmax = 100 + 20 if args.workload == "dg-loop" else 100

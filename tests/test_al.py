@@ -137,3 +137,24 @@ def test_gpu_dropin_compute_problem():
         assert res == r["label"][i]
         if res == 1:
             assert np.abs(np.array([ocp.ocp_solver.get(k, "x") for k in range(ocp.N + 1)]) - r["x"][i]).max() < 1e-7
+
+
+@pytest.mark.gpu
+def test_gpu_al_error_codes_and_empty_batch():
+    """The C ABI's argument checks: an nq != 3 handle is refused (VBOC_ERR_UNSUPPORTED), a horizon past nmax is an
+    argument error, an empty batch is a no-op."""
+    import ctypes
+    import torch
+    from vboc_amd import lib
+    spec = AlSpec()
+    s2 = lib.Solver(2, 100)
+    x0 = torch.zeros((4, 6), dtype=torch.float64, device="cuda:0")
+    with pytest.raises(lib.VbocError, match="nq = 3"):
+        s2.al_solve_device(spec, x0)
+    s3 = lib.Solver(3, 50)
+    with pytest.raises(lib.VbocError, match="nmax"):
+        s3.al_solve_device(spec, x0)
+    s = lib.Solver(3, 100)
+    out = s.al_solve_device(spec, torch.zeros((0, 6), dtype=torch.float64, device="cuda:0"))
+    torch.cuda.synchronize()
+    assert out["label"].numel() == 0

@@ -33,3 +33,5 @@ def test_error_reporting_without_device():
     assert rc == -1
     assert b"nq" in so.vboc_last_error()
     assert so.vboc_rk4_batch(3, -1, 0.01, None, None, None, None) == -1
+    assert so.vboc_al_solve_batch(None, None, None) == -1
+    assert b"vboc_al_solve_batch" in so.vboc_last_error()

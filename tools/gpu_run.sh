@@ -5,9 +5,6 @@
 #   tests_file=<path,...>     GPU test files
 #   tests_lib=<name>:<files>[:<-k expr>]  GPU test files (comma-separated) on vboc_amd/ab/libvboc_amd_<name>.so
 #                             (VBOC_LIB): the parity suite on a variant build, parity records to <out>/parity_<name>
-#   rccl2                     bench.py --gpus 2 with both ranks on the box's one GPU (VBOC_RANKS_SHARE_GPUS=1): the N > 1
-#                             path - spawned ranks, nccl (RCCL) process group, per-rank dg-loop, RCCL all-gather of the
-#                             samples, max-over-ranks timing - on hardware; its rate is no scaling measurement
 #   smoke                     __graft_entry__.smoke()
 #   bench                     the driver's command (bench.py --steps 20 --warmup 5) -> <out>/bench.json
 #   prof                      the same command under rocprofv3 --kernel-trace --stats -> <out>/prof
@@ -42,8 +39,6 @@ for step in "$@"; do
                  run "tests_lib $n" 900 env VBOC_LIB=$R/vboc_amd/ab/libvboc_amd_$n.so VBOC_PARITY_OUT=$O/parity_$n \
                    python -u -m pytest $(echo $files | tr , ' ') -m gpu -x -v --timeout 300 --timeout-method thread \
                    ${k:+-k "$k"} > $O/pytest_lib_$n.log 2>&1;;
-    rccl2) run rccl2 240 env VBOC_RANKS_SHARE_GPUS=1 NCCL_DEBUG=WARN python bench.py --gpus 2 --steps 2 --warmup 1 \
-             --batch 4000 --no-cpu > $O/bench_rccl2.json 2> $O/bench_rccl2.err; cat $O/bench_rccl2.json;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1;;
     bench) run bench 420 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err; cat $O/bench.json;;
     prof) (cd /tmp && export TMPDIR=/tmp && run prof 420 rocprofv3 --kernel-trace --stats --output-format csv \
