@@ -343,12 +343,14 @@ int vboc_mpc_soft_solve_batch(vboc_handle h, const vboc_mpc_batch_t* batch, cons
  * or 2 (any other status), as compute_problem returns.  LINEAR_LS cost 1/2 |[x; u]|^2_W on stages 0..N-1 (times
  * cost_scale) + 1/2 |x_N|^2_We, yref = 0; path boxes lbx/ubx, lbu/ubu; terminal lbx_e/ubx_e (lb == ub: fixed, the
  * class's zero final velocity).  Device pointers except W [3nq] / We [2nq] (host); asynchronous on `stream`.
- * The handle: nq = 3, nmax >= N.  x0[B][2nq]; outputs label[B], status[B], x_out[B][N+1][2nq] (get(i, "x")),
- * u_out[B][N][nq], qp_iter[B]. */
+ * The handle: nq = 3, nmax >= N.  x0[B][2nq], x_guess (optional, see the struct); outputs label[B], status[B],
+ * x_out[B][N+1][2nq] (get(i, "x")), u_out[B][N][nq], qp_iter[B]. */
 typedef struct {
   int B, N;
   double h, cost_scale;
   const double* x0;
+  const double* x_guess;  /* [B][N+1][2nq] or NULL: compute_problem's (q0, 0) at every stage; compute_problem_nnguess
+                             (:171-201) passes the guess network's trajectory (stage 0 = x0) */
   const double *lbx, *ubx, *lbu, *ubu, *lbx_e, *ubx_e;
   const double *W, *We;   /* host */
   int* label;

@@ -327,11 +327,14 @@ def mpc_row(x, params, mean, std, margin=-1.0):
     return out
 
 
-def al_solve_batch(spec, x0, opts=None, nthreads=None):
+def al_solve_batch(spec, x0, x_guess=None, opts=None, nthreads=None):
     """AL's compute_problem (vboc_oracle_ft.c vboc_oracle_al_solve_batch) for every row of x0 [B, 6]: spec a
-    vboc_amd.al.AlSpec.  Returns dict(label, status, qp_iter, x [B, N+1, 6], u [B, N, 3])."""
+    vboc_amd.al.AlSpec; x_guess [B, N+1, 6] (optional): compute_problem_nnguess's stage guesses.  Returns
+    dict(label, status, qp_iter, x [B, N+1, 6], u [B, N, 3])."""
     x0 = np.ascontiguousarray(x0, dtype=np.float64)
     B, N = x0.shape[0], spec.N
+    xg = None if x_guess is None else np.ascontiguousarray(x_guess, dtype=np.float64)
+    assert xg is None or xg.shape == (B, N + 1, 6)
     x_out, u_out = np.zeros((B, N + 1, 6)), np.zeros((B, N, 3))
     res = np.zeros(B, dtype=RESULT_DTYPE)
     label = np.zeros(B, np.int32)
@@ -339,7 +342,8 @@ def al_solve_batch(spec, x0, opts=None, nthreads=None):
         opts = default_opts(lm=spec.lm, tol_stat=1e-6, qp_tol_stat=1e-8, qp_max_iter=spec.qp_iter_max)
     vec = [np.ascontiguousarray(a, dtype=np.float64) for a in
            (spec.xmin, spec.xmax, spec.umin, spec.umax, spec.xmin_e, spec.xmax_e, spec.W, spec.W_e)]
-    rc = lib().vboc_oracle_al_solve_batch(3, B, N, ctypes.c_double(spec.time_step), _p(x0), *[_p(a) for a in vec],
+    rc = lib().vboc_oracle_al_solve_batch(3, B, N, ctypes.c_double(spec.time_step), _p(x0),
+                                          _p(xg) if xg is not None else None, *[_p(a) for a in vec],
                                           ctypes.c_double(spec.cost_scale), ctypes.byref(opts),
                                           int(nthreads or os.cpu_count()), _p(x_out), _p(u_out), _p(res), _p(label))
     if rc != 0:

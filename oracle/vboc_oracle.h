@@ -93,11 +93,12 @@ int vboc_oracle_mpc_soft_solve_batch(int nq, int B, int N, double h, const doubl
                                      int rti, const vboc_opts_t* opts, int nthreads, double* x_out, double* u_out,
                                      vboc_result_t* res, double* hrow);
 void vboc_oracle_mpc_row(int nq, int B, const double* x, const vboc_mpc_nn_t* nn, double margin, double* out);
-/* AL's compute_problem (vboc_oracle_ft.c): x0 [B][2 nq]; boxes [2 nq] / [nq]; W [3 nq], We [2 nq]; label [B] 1/0/2 */
-int vboc_oracle_al_solve_batch(int nq, int B, int N, double h, const double* x0, const double* xlb, const double* xub,
-                               const double* ulb, const double* uub, const double* xNlb, const double* xNub,
-                               const double* W, const double* We, double cs, const vboc_opts_t* opts, int nthreads,
-                               double* x_out, double* u_out, vboc_result_t* res, int* label);
+/* AL's compute_problem (vboc_oracle_ft.c): x0 [B][2 nq]; x_guess [B][N+1][2 nq] or NULL ((q0, 0)); boxes [2 nq] / [nq]; W [3 nq], We [2 nq]; label [B] 1/0/2 */
+int vboc_oracle_al_solve_batch(int nq, int B, int N, double h, const double* x0, const double* x_guess,
+                               const double* xlb, const double* xub, const double* ulb, const double* uub,
+                               const double* xNlb, const double* xNub, const double* W, const double* We, double cs,
+                               const vboc_opts_t* opts, int nthreads, double* x_out, double* u_out, vboc_result_t* res,
+                               int* label);
 /* HJR one-step OCP (vboc_oracle_hjr.c): x0 fixed, N = 1, terminal cost = logit 0 of NeuralNetCLS */
 void vboc_oracle_hjr_default_opts(int nq, vboc_opts_t* o);
 int vboc_oracle_hjr_solve_batch(int nq, int B, const double* x0, int h, const double* W0, const double* b0,

@@ -1299,12 +1299,14 @@ int vboc_oracle_mpc_solve_batch(int nq, int B, int N, double h, const double* x0
 /* Active learning's labelling OCP, OCPtriplependulumINIT.compute_problem(q0, v0) (AL/triplependulum_class_al.py:
    148-169; the OCP :82-144, terminal rest :204-222): the tracking OCP above with yref = 0, no row, ACADOS' default
    SQP_RTI (one QP at the reset point, its full step), x_0 = (q0, v0) fixed, every stage's guess (q0, 0) (:157-160),
-   u = 0 and zero multipliers (reset, :150); a QP stopped by qp_max_iter is a QP failure (qcf: the label is the QP's
+   u = 0 and zero multipliers (reset, :150) - or, x_guess [B][N+1][2 nq] given, compute_problem_nnguess's stage guesses
+   (:171-201); a QP stopped by qp_max_iter is a QP failure (qcf: the label is the QP's
    feasibility answer).  label[b] = 1 / 0 / 2 for status 0 / 4 / other (:164-169). */
-int vboc_oracle_al_solve_batch(int nq, int B, int N, double h, const double* x0, const double* xlb, const double* xub,
-                               const double* ulb, const double* uub, const double* xNlb, const double* xNub,
-                               const double* W, const double* We, double cs, const vboc_opts_t* opts, int nthreads,
-                               double* x_out, double* u_out, vboc_result_t* res, int* label) {
+int vboc_oracle_al_solve_batch(int nq, int B, int N, double h, const double* x0, const double* x_guess,
+                               const double* xlb, const double* xub, const double* ulb, const double* uub,
+                               const double* xNlb, const double* xNub, const double* W, const double* We, double cs,
+                               const vboc_opts_t* opts, int nthreads, double* x_out, double* u_out, vboc_result_t* res,
+                               int* label) {
   if (nq < 1 || nq > FQ || N < 1) return -1;
   const int n2 = 2 * nq;
   const double zero[3 * FQ] = {0};
@@ -1315,7 +1317,8 @@ int vboc_oracle_al_solve_batch(int nq, int B, int N, double h, const double* x0,
     if (!xg) { err |= 1; continue; }
     double* ug = xg + (size_t)(N + 1) * n2;
     for (int k = 0; k <= N; ++k)
-      for (int i = 0; i < n2; ++i) xg[k * n2 + i] = i < nq ? x0[(size_t)b * n2 + i] : 0.0;
+      for (int i = 0; i < n2; ++i)
+        xg[k * n2 + i] = x_guess ? x_guess[((size_t)b * (N + 1) + k) * n2 + i] : (i < nq ? x0[(size_t)b * n2 + i] : 0.0);
     for (int e = 0; e < N * nq; ++e) ug[e] = 0.0;
     const size_t xo = (size_t)b * (N + 1) * n2, uo = (size_t)b * N * nq;
     const int r = mpc_impl(nq, N, h, x0 + (size_t)b * n2, xg, ug, xlb, xub, ulb, uub, xNlb, xNub, W, We, zero, zero, cs,

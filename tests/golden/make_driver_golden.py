@@ -35,8 +35,9 @@ run the same way on the drop-in vboc_amd.cartesian.OCPdoublependulumINIT (keep-o
 The HJR labelling function data_generation(v) (HJR/triplependulum_hjr.py:21-40) is run the same way on a fake
 `ocp` whose compute_problem solves the HJR one-step OCP on the oracle (vboc_oracle_hjr.c).
 
-The active-learning driver testing(s0) (AL/triplependulum_al.py:24-42) is run the same way on a fake `ocp` whose
-compute_problem solves AL's labelling OCP on the oracle (vboc_oracle_al_solve_batch).
+The active-learning drivers testing(s0) and testing_guess(s0) (AL/triplependulum_al.py:24-62) are run the same way on a
+fake `ocp` whose compute_problem / compute_problem_nnguess solve AL's labelling OCP on the oracle
+(vboc_oracle_al_solve_batch), the latter with a seeded guess network.
 
 Usage: python tests/golden/make_driver_golden.py [dg|test|pend|ur5|cart|hjr|al]
   ->  tests/golden/driver_{2,3}.json, tests/golden/testing_{1,2,3}.json, tests/golden/driver_1.json,
@@ -370,6 +371,9 @@ def main_hjr():
     print("hjr_3.json", sum(o is not None and o[0] == 0 for _, o in out), "labelled viable of", len(out))
 
 
+GUESS_SEED = 0
+
+
 def main_al():
     """The active-learning labelling driver testing(s0) of AL/triplependulum_al.py:24-42 (fanned out at :133 / :284),
     AST-extracted and run over 96 states of the driver's unlabeled box (:115-123, seeded numpy draws; the widened
@@ -397,14 +401,37 @@ def main_al():
             self.ocp_solver.x = r["x"][0]
             return int(r["label"][0])
 
+    # testing_guess (:44-62) calls compute_problem_nnguess(q0, v0, model_guess, mean, std) (class :171-201): the guess
+    # network NeuralNetCLS(6, 500, 6 N) seeded with torch.manual_seed(GUESS_SEED) (untrained: the reference trains it on
+    # X_traj, :210-240), mean / std the scalar torch statistics of the candidate states as the driver's (:125-126)
+    import torch
+    from vboc_amd.al import nn_guess
+    from vboc_amd.learn import NeuralNetCLS
+    torch.manual_seed(GUESS_SEED)
+    model_guess = NeuralNetCLS(6, 500, 6 * spec.N)
+    Xt = torch.Tensor(X)
+    mean, std = torch.mean(Xt), torch.std(Xt)
+
+    class AlOcpGuess(AlOcp):
+        def compute_problem_nnguess(self, q0, v0, model, mean_, std_):
+            xg = nn_guess(spec.N, q0, v0, model, mean_, std_)
+            r = oracle.al_solve_batch(spec, np.r_[q0, v0][None], x_guess=xg[None], nthreads=1)
+            self.ocp_solver.x = r["x"][0]
+            return int(r["label"][0])
+
     code = extract(os.path.join(os.path.dirname(REF), "AL", "triplependulum_al.py"), "testing")
-    g = dict(np=np, ocp=AlOcp(), ocp_dim=6, q_max=spec.thetamax, q_min=spec.thetamin, v_max=spec.dthetamax,
-             v_min=-spec.dthetamax)
+    code_g = extract(os.path.join(os.path.dirname(REF), "AL", "triplependulum_al.py"), "testing_guess")
+    g = dict(np=np, ocp=AlOcpGuess(), ocp_dim=6, q_max=spec.thetamax, q_min=spec.thetamin, v_max=spec.dthetamax,
+             v_min=-spec.dthetamax, model_guess=model_guess, mean=mean, std=std)
     exec(code, g)
+    exec(code_g, g)
     out = [g["testing"](list(map(float, s))) for s in X]
-    json.dump({"nq": 3, "X": X.tolist(), "results": [None if o is None else [o[0], o[1]] for o in out]},
+    out_g = [g["testing_guess"](list(map(float, s))) for s in X]
+    enc = lambda res: [None if o is None else [o[0], o[1]] for o in res]
+    json.dump({"nq": 3, "X": X.tolist(), "results": enc(out), "guess_seed": GUESS_SEED, "results_guess": enc(out_g)},
               open(os.path.join(HERE, "al_testing_3.json"), "w"))
-    print("al_testing_3.json", sum(o is not None and o[0][-1] == 1 for o in out), "feasible of", len(out))
+    print("al_testing_3.json", sum(o is not None and o[0][-1] == 1 for o in out), "feasible of", len(out), "; with "
+          "the guess network", sum(o is not None and o[0][-1] == 1 for o in out_g))
 
 
 if __name__ == "__main__":

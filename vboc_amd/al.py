@@ -15,7 +15,8 @@ vboc_amd/csrc/ft.h through vboc_al_solve_batch) solves that QP with the Safe-MPC
 counts a QP the IPM has not finished after qp_solver_iter_max iterations as a failure (status 4); HPIPM's own
 status on such a QP is unpinned (ACADOS / HPIPM are not in this image).  The tests pin the label against an
 independent LP feasibility check of the same linearised QP (tests/test_al.py).  The driver `testing(s0)`
-(AL/triplependulum_al.py:24-42) is `testing_batch` below.
+(AL/triplependulum_al.py:24-42) is `testing_batch` below; with the guess network (compute_problem_nnguess, :171-201) the
+same function restates `testing_guess(s0)` (:44-62).
 """
 import math
 
@@ -105,6 +106,52 @@ class OCPtriplependulumINIT:
         r = self.compute_problem_batch(x0[None])
         self.ocp_solver.x, self.ocp_solver.u, self.ocp_solver.status = r["x"][0], r["u"][0], int(r["status"][0])
         return int(r["label"][0])
+
+    def compute_problem_nnguess_batch(self, x0, model, mean, std):
+        """compute_problem_nnguess (:171-201) for every row of x0 [B, 6]: the guess network's trajectory as every
+        stage's x guess (nn_guess), then the same RTI step.  Returns the dict of compute_problem_batch."""
+        import torch
+        x0 = np.ascontiguousarray(x0, dtype=np.float64)
+        xg = np.stack([nn_guess(self.N, s[:3], s[3:], model, mean, std) for s in x0]) if len(x0) else \
+            np.zeros((0, self.N + 1, 6))
+        dev = torch.device("cuda", self.device)
+        T = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)
+        out = self.solver.al_solve_device(self.spec, T(x0), x_guess=T(xg))
+        torch.cuda.synchronize(dev)
+        return {k: v.cpu().numpy() for k, v in out.items() if not k.startswith("_")}
+
+    def compute_problem_nnguess(self, q0, v0, model, mean, std):
+        x0 = np.array([q0[0], q0[1], q0[2], v0[0], v0[1], v0[2]], dtype=np.float64)   # :175
+        r = self.compute_problem_nnguess_batch(x0[None], model, mean, std)
+        self.ocp_solver.x, self.ocp_solver.u, self.ocp_solver.status = r["x"][0], r["u"][0], int(r["status"][0])
+        return int(r["label"][0])
+
+    def labels_nnguess(self, model, mean, std):
+        """testing_batch's label_fn for the driver's testing_guess (AL/triplependulum_al.py:44-62)."""
+        def fn(X):
+            r = self.compute_problem_nnguess_batch(X, model, mean, std)
+            return r["label"], r["x"]
+        return fn
+
+
+def nn_guess(N, q0, v0, model, mean, std):
+    """The stage guesses of compute_problem_nnguess (AL/triplependulum_class_al.py:180-192): the guess network
+    (NeuralNetCLS(6, 500, 6 N), FP32) evaluated on the normalised state exactly as the reference does it - one [1, 6]
+    float32 tensor, (x - mean) / std, model, * std + mean, reshaped to [N, 6] - and x0 at stage 0.  Evaluated on the
+    model's device (the reference's is the CPU, where the FP32 arithmetic is the reference's own)."""
+    import torch
+    dev = next(model.parameters()).device
+    with torch.no_grad():
+        inp = torch.Tensor([[q0[0], q0[1], q0[2], v0[0], v0[1], v0[2]]]).to(dev)
+        inp = (inp - mean) / std
+        out = model(inp)
+        out = out * std + mean
+        out = out.cpu().numpy()
+    out = np.reshape(out, (N, 6))
+    xg = np.empty((N + 1, 6))
+    xg[0] = [q0[0], q0[1], q0[2], v0[0], v0[1], v0[2]]
+    xg[1:] = out
+    return xg
 
 
 def out_of_bounds(spec, s0):

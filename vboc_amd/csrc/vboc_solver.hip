@@ -2328,7 +2328,7 @@ int vboc_al_solve_batch(vboc_handle h, const vboc_al_batch_t* b, void* stream) {
   static const double zero[3 * NQ] = {0.0};   // yref = yref_e = 0 (:114-115)
   vboc_mpc_batch_t m{};
   m.B = b->B; m.N = b->N; m.rti = 1; m.hidden = 0; m.h = b->h; m.cost_scale = b->cost_scale;
-  m.x0 = b->x0; m.x_guess = xg; m.u_guess = ug;
+  m.x0 = b->x0; m.x_guess = b->x_guess ? b->x_guess : xg; m.u_guess = ug;   // u = 0 (reset) in both variants
   m.lbx = b->lbx; m.ubx = b->ubx; m.lbu = b->lbu; m.ubu = b->ubu; m.lbx_e = b->lbx_e; m.ubx_e = b->ubx_e;
   m.W = b->W; m.We = b->We; m.yref = zero; m.yref_e = zero;
   m.status = b->status; m.x_out = b->x_out; m.u_out = b->u_out; m.cost = cost; m.sqp_iter = sqp;

@@ -91,8 +91,8 @@ class MpcSoft(ctypes.Structure):
 class AlBatch(ctypes.Structure):
     """vboc_al_batch_t (include/vboc.h): AL compute_problem batch (W, We are host arrays)."""
     _fields_ = [("B", ctypes.c_int), ("N", ctypes.c_int), ("h", ctypes.c_double), ("cost_scale", ctypes.c_double)] + \
-               [(n, ctypes.c_void_p) for n in ("x0", "lbx", "ubx", "lbu", "ubu", "lbx_e", "ubx_e", "W", "We", "label",
-                                               "status", "x_out", "u_out", "qp_iter")]
+               [(n, ctypes.c_void_p) for n in ("x0", "x_guess", "lbx", "ubx", "lbu", "ubu", "lbx_e", "ubx_e", "W", "We",
+                                               "label", "status", "x_out", "u_out", "qp_iter")]
 
 
 # per problem (vboc_dg_batch_t.stats); t0 / t1: the problem's start / end on its wave, 100 MHz ticks
@@ -438,13 +438,17 @@ class Solver:
         out["_keep"] = (bnd, host, W, arrs)
         return out
 
-    def al_solve_device(self, spec, x0, stream=None):
+    def al_solve_device(self, spec, x0, x_guess=None, stream=None):
         """AL's OCPtriplependulumINIT.compute_problem (vboc_al_solve_batch, ft.h) for every row of the float64 cuda
-        tensor x0 [B, 6]; spec a vboc_amd.al.AlSpec.  Returns a dict of device tensors: label (1 / 0 / 2), status,
+        tensor x0 [B, 6]; spec a vboc_amd.al.AlSpec; x_guess (float64 cuda [B, N+1, 6], optional):
+        compute_problem_nnguess's stage guesses.  Returns a dict of device tensors: label (1 / 0 / 2), status,
         x [B, N+1, 6], u [B, N, 3], qp_iter."""
         import torch
         assert x0.is_cuda and x0.dtype == torch.float64 and x0.is_contiguous() and x0.shape[1] == 6
         B, N, dev = x0.shape[0], spec.N, x0.device
+        if x_guess is not None:
+            assert (x_guess.is_cuda and x_guess.dtype == torch.float64 and x_guess.is_contiguous()
+                    and tuple(x_guess.shape) == (B, N + 1, 6))
         f64 = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)
         bnd = [f64(a) for a in (spec.xmin, spec.xmax, spec.umin, spec.umax, spec.xmin_e, spec.xmax_e)]
         host = [np.ascontiguousarray(a, dtype=np.float64) for a in (spec.W, spec.W_e)]
@@ -453,13 +457,14 @@ class Solver:
                    u=torch.empty((B, N, 3), dtype=torch.float64, device=dev),
                    qp_iter=torch.empty(B, dtype=torch.int32, device=dev))
         b = AlBatch(B=B, N=N, h=spec.time_step, cost_scale=spec.cost_scale, x0=x0.data_ptr(),
+                    x_guess=x_guess.data_ptr() if x_guess is not None else None,
                     **{n: t_.data_ptr() for n, t_ in zip(("lbx", "ubx", "lbu", "ubu", "lbx_e", "ubx_e"), bnd)},
                     W=host[0].ctypes.data, We=host[1].ctypes.data, label=out["label"].data_ptr(),
                     status=out["status"].data_ptr(), x_out=out["x"].data_ptr(), u_out=out["u"].data_ptr(),
                     qp_iter=out["qp_iter"].data_ptr())
         st = stream if stream is not None else torch.cuda.current_stream(dev)
         _check(self.lib.vboc_al_solve_batch(self.h, ctypes.byref(b), ctypes.c_void_p(st.cuda_stream)))
-        out["_keep"] = (bnd, host, x0)
+        out["_keep"] = (bnd, host, x0, x_guess)
         return out
 
     def kernel_stats(self):
