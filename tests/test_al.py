@@ -183,32 +183,47 @@ def test_gpu_testing_driver_reproduces_fixture():
 
 @pytest.mark.gpu
 def test_gpu_testing_guess_driver_reproduces_fixture():
-    """testing_guess on the GPU against the reference's function on the oracle: every state as the fixture, except a
-    state whose label parts because one side's QP stopped at the 50-iteration cap (with the untrained network's guesses
-    most feasible QPs end near the cap); those are counted and capped at 10 %."""
+    """testing_guess on the GPU against the reference's function on the oracle, both fed the same network guesses
+    (evaluated once, on this host): every state as the oracle's, except a state whose label parts because one side's
+    QP stopped at the 50-iteration cap (with the untrained network's guesses most feasible QPs end near the cap,
+    DESIGN.md section 20); those are counted and capped at 10 %.  The fixture itself was made with the guesses of the
+    container's CPU; the FP32 network rounds differently on another host's CPU, which moves near-cap QPs across the cap
+    (state 6 on the round-6 box) and moves every RTI point by the network's FP32 rounding, so against the fixture the
+    labels are held to 90 % agreement and the trajectories of agreeing label-1 states to 1e-5 (6.2e-7 seen on the
+    round-6 box; 0 where the host's guesses equal the container's)."""
     from vboc_amd.al import OCPtriplependulumINIT
     g = json.load(open(os.path.join(HERE, "golden", "al_testing_3.json")))
     ocp = OCPtriplependulumINIT()
     spec = ocp.spec
     model, mean, std = guess_network(g, spec)
     X = np.array(g["X"])
+    S = np.array([s for s in X if not out_of_bounds(spec, s)])
+    xg = np.stack([nn_guess(spec.N, s[:3], s[3:], model, mean, std) for s in S])
+    import torch
+    T = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device="cuda")
+    out = ocp.solver.al_solve_device(spec, T(S), x_guess=T(xg))
+    torch.cuda.synchronize()
+    lg, xgpu, ig = (out[k].cpu().numpy() for k in ("label", "x", "qp_iter"))
+    rr = oracle.al_solve_batch(spec, S, x_guess=xg)
+    cap = np.maximum(ig, rr["qp_iter"]) >= spec.qp_iter_max
+    diff = np.flatnonzero(lg != rr["label"])
+    assert all(cap[i] for i in diff), diff
+    print(f"network guesses: sum {xg.sum():.17g}")
+    print(f"testing_guess on the GPU: {len(diff)} of {len(S)} states part from the oracle at the QP cap: {diff}")
+    assert len(diff) <= 0.1 * len(S), diff
+    ok = (lg == 1) & (rr["label"] == 1)
+    assert np.abs(xgpu[ok] - rr["x"][ok]).max() < 1e-7
     got = al_testing_batch(spec, X, ocp.labels_nnguess(model, mean, std))
     ref = g["results_guess"]
-    S = np.array([s for s in X if not out_of_bounds(spec, s)])
-    gg = ocp.compute_problem_nnguess_batch(S, model, mean, std)
-    xg = np.stack([nn_guess(spec.N, s[:3], s[3:], model, mean, std) for s in S])
-    rr = oracle.al_solve_batch(spec, S, x_guess=xg)
-    capped = {tuple(s) for s, a, b in zip(S, gg["qp_iter"], rr["qp_iter"]) if max(a, b) >= spec.qp_iter_max}
-    parted = []
+    agree = 0
     for b, (a, r) in enumerate(zip(got, ref)):
         if (a is None) != (r is None) or (a is not None and a[0] != r[0]):
-            assert tuple(X[b]) in capped, b
-            parted.append(b)
             continue
+        agree += 1
         if r is not None and r[1] is not None:
-            assert np.abs(np.asarray(a[1]) - np.asarray(r[1])).max() < 1e-7, b
-    print(f"testing_guess on the GPU: {len(parted)} of {len(X)} states part at the QP cap: {parted}")
-    assert len(parted) <= 0.1 * len(S), parted
+            assert np.abs(np.asarray(a[1]) - np.asarray(r[1])).max() < 1e-5, b
+    print(f"testing_guess on the GPU against the fixture: {agree} of {len(X)} states agree")
+    assert agree >= 0.9 * len(X), agree
     S = np.array(g["X"])[:8]
     for s in S:
         if out_of_bounds(ocp.spec, s):

@@ -59,18 +59,25 @@ __host__ __device__ constexpr int rec_up(int v) { return (v + VBOC_REC_ALIGN - 1
 template <int NQ>
 struct WaveLayout {
   static constexpr int NX = 2 * NQ, NU = NQ, NZ = 3 * NQ, M0 = NQ + 1;
-  // global stage record: A, B, z (current iterate), dz, lambda_l, lambda_u, e (defect -> initial
-  // residual), K, k_f, chol(Ru), M, Y, P e, D (H / g_corr / corrector direction), DA (g_pred /
-  // affine direction / costate), V (v = P e + p), then the SQP state x, u, pi, lam_l, lam_u, w_pi
-  static constexpr int OA = 0, OB = OA + NX * NX, OZ = OB + NX * NU, ODZ = OZ + NZ, OQL = ODZ + NZ, OQU = OQL + NZ,
-                       OE = OQU + NZ, OD = OE + NX, ODA = OD + NZ, OK = ODA + NZ, OKF = OK + NU * NX,
+  // global stage record: A, B, e (defect -> initial residual), D (H / g_corr / corrector direction), DA (g_pred /
+  // affine direction / costate), z (current iterate), dz, lambda_l, lambda_u, K, k_f, chol(Ru) (Ru^-1), M, Y, P e, C,
+  // A_cl, then the SQP state x, u, pi, lam_l, lam_u, w_pi.  IN_FIRST (the pendulum chains, since round 6): the
+  // factorisation's inputs A, B, e, D lead the record, so its window [0, W_FIN) carries nothing it does not read (the
+  // triple: 70 doubles instead of the 114 before K); the arm (NQ = 4) keeps round 5's order A, B, z, dz, lambda, e, D, DA
+  // (its k_wave<4> code is left as it was)
+  static constexpr bool IN_FIRST = NQ <= 3;
+  static constexpr int OA = 0, OB = OA + NX * NX, P0 = OB + NX * NU, OE = IN_FIRST ? P0 : P0 + 4 * NZ, OD = OE + NX,
+                       ODA = OD + NZ, OZ = IN_FIRST ? ODA + NZ : P0, ODZ = OZ + NZ, OQL = ODZ + NZ, OQU = OQL + NZ,
+                       OK = P0 + 6 * NZ + NX, OKF = OK + NU * NX,
                        OLR = OKF + NU, OM = OLR + NU * NU, OY = OM + NU * NQ, OPE = OY + NU * NQ, OC = OPE + NX,
                        OACL = OC + NX, OX = OACL + NX * NX, OU = OX + NX, OPI = OU + NU, OLL = OPI + NX,
                        OLU = OLL + NZ, OWPI = OLU + NZ, REC = rec_up(OWPI + NX);
+  static_assert((IN_FIRST ? OQU : ODA) + NZ == OK, "the fields before K are A, B, e, D, DA, z, dz, lambda_l, lambda_u");
   // OC: per-pass constant of the vector / forward recursion; OACL: closed-loop A + B K (row-major)
-  // ring windows [lo, lo + W): factor [0, OC) (writes back [OK, OC)); vector pass [OPE, OX);
-  // forward sweep [OC, OX); costate [0, OE)
-  static constexpr int W_FAC = OC, LO_VEC = OPE, W_VEC = OX - OPE, LO_FWD = OC, W_FWD = OX - OC, W_COS = even_up(OE);
+  // ring windows [lo, lo + W): factor [0, OC) (writes back [OK, OC)), or with FAC1 its inputs [0, W_FIN); vector pass
+  // [OPE, OX); forward sweep [OC, OX); costate [0, W_COS): A (and B) to the end of lambda_u
+  static constexpr int W_FAC = OC, W_FIN = even_up(ODA), LO_VEC = OPE, W_VEC = OX - OPE, LO_FWD = OC, W_FWD = OX - OC,
+                       W_COS = even_up(OQU + NZ);
   // LDS-DMA rings (global_load_lds_dwordx4: one wave-instruction lands 64 lanes x 16 B = 128 doubles):
   // the factorisation streams its window two stages ahead through 4 slots of 2 KiB (two DMAs per
   // stage), the vector / forward / costate recursions six stages ahead through 8 slots of 1 KiB
@@ -293,8 +300,9 @@ __device__ unsigned long long g_wave_prof[16];
 // part of a window); -DVBOC_FUSE=<mask> selects them for measurements (0: the round-4 passes).  1, 4 and 8 keep the
 // arithmetic and its order (bit-identical); 2 re-associates at rounding level and is accepted under the tolerance
 // parity rule of round 6.
-//   1 FAC1   the factorisation's window is its inputs [A, K) - one LDS-DMA per stage instead of two ([K, C) was
-//            loaded only to be overwritten by the stage's outputs before the write-back);
+//   1 FAC1   the factorisation's window is its inputs [A, W_FIN) - one LDS-DMA per stage instead of two ([K, C) was
+//            loaded only to be overwritten by the stage's outputs before the write-back; since round 6 the record leads
+//            with A, B, e, D, so the window holds only what the factorisation reads, 70 of 114 doubles);
 //   2 PFUSE  the predictor preparation (D = H, DA = predictor gradient) is computed by the iterate update of the
 //            previous IPM iteration from the values it has just written (prep_pred runs for the first only); the
 //            compiler contracts the inlined copy differently (rounding level; round 5 dropped it on the digest);
@@ -1189,7 +1197,7 @@ struct Coop {
     // FAC1: the window is the stage's inputs [A, K) (A, B, z .. lambda_u, e, D, DA): the outputs [K, A_cl] are
     // written into the slot by this sweep before the write-back; k_f and C keep stale slot words, which the record
     // holds only until the vector passes rewrite them (neither is read before)
-    constexpr int WF = FAC1 ? OK : L::W_FAC, P = (WF + 127) / 128;
+    constexpr int WF = FAC1 ? L::W_FIN : L::W_FAC, P = (WF + 127) / 128;
     static_assert(!FAC1 || P == 1, "the factorisation's inputs fit one LDS-DMA");
     auto fdma = [&](int j) {
       const int kk = N - 1 - j >= 0 ? N - 1 - j : 0;
