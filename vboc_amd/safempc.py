@@ -17,7 +17,9 @@ The restatement: the free-time solver's model (dt a state, here pinned by x_0 an
 exact reformulation), its SQP / merit / Mehrotra IPM / Riccati recursion with the tracking cost's Gauss-Newton
 Hessian and gradient and the terminal row handled like the Cartesian rows (oracle/vboc_oracle_ft.c,
 vboc_amd/csrc/ft.h).  ACADOS' cost_scaling (stage costs times the time step in current releases, 1 in older
-ones) is unpinned: `cost_scale` states the choice (default: the time step).
+ones) is unpinned: `cost_scale` states the choice (default: the time step).  Under it the stage slack weights zl / Zl
+of stages 0..N-1 are scaled too (stage N stays at 1), as ACADOS scales them; the receding driver, whose path slack
+weights are large (10^(6(1 - ri/N)), 1e12), depends on that choice, so its closed-loop parity is unpinned as well.
 """
 import math
 
