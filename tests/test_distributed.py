@@ -232,8 +232,8 @@ def _main_blocks_worker(rank, world, port, out_dir):
     loop = vboc_run(2, OracleBackend(2), X_test, stop_time=1e9, num_prob=5, max_iterations=2, stream_rounds=2,
                     segment_factory=lambda f, k: _RankSegment(f, k, 2, 5),
                     trainer_kw=dict(hidden=8, minibatch=16, stop_val=1e9))
-    u = ur5_run(OracleBackend(4), num_test=5, num_train=7, device="cpu", minibatch=8, hidden=16)
-    c = cartesian_run(OracleBackend(2, path_constraint=cartesian_constraint()), num_test=3, num_train=5,
+    u = ur5_run(OracleBackend(4), num_test=2, num_train=3, device="cpu", minibatch=8, hidden=16)
+    c = cartesian_run(OracleBackend(2, path_constraint=cartesian_constraint()), num_test=2, num_train=3,
                       device="cpu", minibatch=8, hidden=16)
     res = dict(loop=loop["X_save"], loop_rmse=loop["rmse"], ur5_test=u["X_test"], ur5_train=u["X_train"],
                ur5_fit=u["fit"], cart_test=c["X_test"], cart_train=c["X_train"], cart_fit=c["fit"])
@@ -257,8 +257,8 @@ def test_main_blocks_at_world_two_equal_one_process(tmp_path):
     r0, r1 = [pickle.load(open(tmp_path / f"rank{r}.pkl", "rb")) for r in range(2)]
     loop_ref = np.concatenate([samples_array(2, _generate(2, OracleBackend(2), np.arange(i * 5, (i + 1) * 5), None,
                                                            20250124)[0]) for i in range(3)])
-    u = ur5_run(OracleBackend(4), num_test=5, num_train=7, device="cpu", minibatch=8, hidden=16)
-    c = cartesian_run(OracleBackend(2, path_constraint=cartesian_constraint()), num_test=3, num_train=5,
+    u = ur5_run(OracleBackend(4), num_test=2, num_train=3, device="cpu", minibatch=8, hidden=16)
+    c = cartesian_run(OracleBackend(2, path_constraint=cartesian_constraint()), num_test=2, num_train=3,
                       device="cpu", minibatch=8, hidden=16)
     for r in (r0, r1):
         np.testing.assert_array_equal(r["loop"], loop_ref)

@@ -46,6 +46,13 @@ def _states(B, seed=1):
     return sp, x0, xg, ug
 
 
+def _capped(sp):
+    """The oracle's options with the SQP stopped at 150 iterations instead of the class's 1000: the tests below compare
+    the converged problems only, whose iterates do not depend on the cap (the problems still iterating at 150 spend
+    most of the CPU suite's time otherwise)."""
+    return oracle.default_opts(lm=sp.lm, tol_stat=1e-6, qp_tol_stat=1e-8, max_iter=150)
+
+
 def test_spec_is_the_reference_ocp():
     from vboc_amd.safempc import MpcSpec
     sp = MpcSpec(4e-3, 0.148)
@@ -71,7 +78,7 @@ def test_oracle_optimum_is_the_slsqp_optimum(with_row):
     from nlp_reference import slsqp_mpc
     P = _net() if with_row else None
     sp, x0, xg, ug = _states(16)
-    x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD)
+    x, u, r, h = oracle.mpc_solve_batch(sp, x0, xg, ug, P, mean=MEAN, std=STD, opts=_capped(sp))
     ok = np.flatnonzero(r["status"] == 0)
     assert ok.size >= 6
     if with_row:
@@ -312,7 +319,7 @@ def test_soft_oracle_optimum_is_the_slsqp_optimum():
     P = _net()
     sp, x0, xg, ug = _states(16)
     Zl = _soft_weights(sp.N, "soft_traj")
-    x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, Zl, rti=False)
+    x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, Zl, rti=False, opts=_capped(sp))
     ok = np.flatnonzero(r["status"] == 0)
     assert ok.size >= 6
     for n, i in enumerate(ok[:2]):
@@ -332,8 +339,9 @@ def test_soft_rows_with_zero_weights_are_free():
     (OCPtriplependulumSTD) optimum, up to the solvers' tolerances."""
     P = _net()
     sp, x0, xg, ug = _states(16)
-    x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, np.zeros(sp.N + 1), rti=False)
-    xs, us, rs, hs = oracle.mpc_solve_batch(sp, x0, xg, ug, None, rti=False)
+    x, u, r, h = oracle.mpc_soft_solve_batch(sp, x0, xg, ug, P, MEAN, STD, MARGIN, np.zeros(sp.N + 1), rti=False,
+                                             opts=_capped(sp))
+    xs, us, rs, hs = oracle.mpc_solve_batch(sp, x0, xg, ug, None, rti=False, opts=_capped(sp))
     both = (r["status"] == 0) & (rs["status"] == 0)
     assert both.sum() >= 6
     assert np.abs(x[both] - xs[both]).max() < 1e-4 and np.abs(r["cost"][both] - rs["cost"][both]).max() < 1e-6

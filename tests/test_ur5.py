@@ -334,25 +334,26 @@ def test_ur5_full_batch_properties():
 
 def test_ur5_run_on_oracle(tmp_path):
     """The UR5 main block end to end on CPU (oracle solver, small sets, small minibatch): artefacts in the
-    reference's names and formats, loadable with weights_only=True."""
+    reference's names and formats, loadable with weights_only=True.  (Ids 0..10: id 11's data generation alone takes
+    the oracle ~30 s.)"""
     import torch
     from vboc_amd.pipeline import ur5_run
-    r = ur5_run(OracleBackend(4), num_test=8, num_train=24, out_dir=str(tmp_path), device="cpu", minibatch=8,
+    r = ur5_run(OracleBackend(4), num_test=3, num_train=6, out_dir=str(tmp_path), device="cpu", minibatch=8,
                 hidden=32)
-    assert r["X_train"].shape[1] == 8 and r["X_train"].shape[0] >= 12
+    assert r["X_train"].shape[1] == 8 and r["X_train"].shape[0] >= 4
     assert np.isfinite(r["rmse_train"]) and np.isfinite(r["rmse_test"])
     sd = torch.load(tmp_path / "model_4dof_vboc", weights_only=True)
     assert sd["linear_relu_stack.0.weight"].shape == (32, 8)
     assert np.load(tmp_path / "data_4dof_vboc_test.npy").shape == r["X_test"].shape
     # resume (X_old, VBOC/UR5/vboc_multiprocessing_ur5.py:501,530): the previous rows first, new ids after them
-    r2 = ur5_run(OracleBackend(4), num_test=8, num_train=16, out_dir=str(tmp_path), device="cpu", minibatch=8,
+    r2 = ur5_run(OracleBackend(4), num_test=3, num_train=2, out_dir=str(tmp_path), device="cpu", minibatch=8,
                  hidden=32, resume=True)
     n_old = r["X_train"].shape[0]
     np.testing.assert_array_equal(r2["X_train"][:n_old], r["X_train"])
     assert r2["X_train"].shape[0] > n_old
     assert not any((r2["X_train"][n_old:] == row).all(1).any() for row in r["X_train"])
     assert np.load(tmp_path / "data_4dof_vboc_train.npy").shape == r2["X_train"].shape
-    assert (tmp_path / "data_4dof_vboc_train.next_id").read_text() == str(8 + 24 + 16)
+    assert (tmp_path / "data_4dof_vboc_train.next_id").read_text() == str(3 + 6 + 2)
 
 
 def _same_tt(a_res, b_res, tol):

@@ -7,6 +7,9 @@
 //   seq_rl    the product's form: lane i owns row i, dx reaches every lane by readlane (coop.h fwd(), ungrouped)
 //   seq_dpp   the product's form with the readlanes replaced by DPP row_newbcast (lane q of each row of 16 to the
 //             row: no SGPR round trip)
+//   seq_mov64 the same with one 64-bit DPP move per component (v_mov_b64_dpp row_newbcast)
+//   seq_fdpp  the broadcast folded into the FMA: v_fmac_f64_dpp src0 row_newbcast:q (the product's arithmetic, in
+//             the same order: bit-identical dx)
 //   seq_red   every lane computes the whole dx = c + A dx from broadcast LDS reads (no cross-lane exchange)
 //   part<P>   P segments of L = ceil(N / P) stages on P lane groups of 16.  Pass A: lane (s, j < 6) carries column
 //             j of the segment's transition matrix Phi_s = A_{end-1} ... A_{start}, lane (s, 6) the segment's
@@ -41,6 +44,18 @@ __device__ __forceinline__ double rowbcast(double v) {
   return __longlong_as_double(((unsigned long long)hi << 32) | lo);
 }
 
+template <int Q>
+__device__ __forceinline__ double bc64(double v) { return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + Q, 0xF, 0xF, false); }
+// acc += (lane Q of the row's v) * a.  The first use after v is written waits the VALU -> DPP read hazard (2 states).
+template <int Q, bool FIRST>
+__device__ __forceinline__ void fmac_bc(double& acc, double a, double v) {
+  if constexpr (FIRST)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %2, %1 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc) : "v"(a), "v"(v), "i"(Q));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %2, %1 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(a), "v"(v), "i"(Q));
+}
+
 // LDS: windows [N][W], then the dx rows [N + 1][NX], then (part) Phi / y per segment and the segment starts
 __device__ __forceinline__ void load(double* s, const double* win, const double* dx0, int t) {
   const double* src = win + (size_t)blockIdx.x * N * W;
@@ -73,6 +88,61 @@ __global__ __launch_bounds__(64) void seq_rl(const double* win, const double* dx
     const double dn = p0 + p1;
     if (t < NX) s[N * W + (k + 1) * NX + t] = dn;
     _Pragma("unroll") for (int q = 0; q < NX; ++q) dx[q] = rdlane(dn, q);
+    _Pragma("unroll") for (int q = 0; q < NX; ++q) a[q] = an[q];
+    c = cn;
+  }
+  const long long c1 = clock64();
+  finish(s, out, cyc, c0, c1, t);
+}
+
+__global__ __launch_bounds__(64) void seq_mov64(const double* win, const double* dx0, double* out, long long* cyc) {
+  extern __shared__ double s[];
+  const int t = threadIdx.x, i = t < NX ? t : NX - 1;
+  load(s, win, dx0, t);
+  double dx[NX];
+  _Pragma("unroll") for (int q = 0; q < NX; ++q) dx[q] = s[N * W + q];
+  double a[NX], c = s[i];
+  _Pragma("unroll") for (int q = 0; q < NX; ++q) a[q] = s[NX + i * NX + q];
+  const long long c0 = clock64();
+  for (int k = 0; k < N; ++k) {
+    const int kn = k + 1 < N ? k + 1 : k;
+    double an[NX], cn = s[kn * W + i];
+    _Pragma("unroll") for (int q = 0; q < NX; ++q) an[q] = s[kn * W + NX + i * NX + q];
+    double p0 = c, p1 = 0.0;
+    _Pragma("unroll") for (int q = 0; q < NX; q += 2) p0 += a[q] * dx[q];
+    _Pragma("unroll") for (int q = 1; q < NX; q += 2) p1 += a[q] * dx[q];
+    const double dn = p0 + p1;
+    if (t < NX) s[N * W + (k + 1) * NX + t] = dn;
+    dx[0] = bc64<0>(dn); dx[1] = bc64<1>(dn); dx[2] = bc64<2>(dn);
+    dx[3] = bc64<3>(dn); dx[4] = bc64<4>(dn); dx[5] = bc64<5>(dn);
+    _Pragma("unroll") for (int q = 0; q < NX; ++q) a[q] = an[q];
+    c = cn;
+  }
+  const long long c1 = clock64();
+  finish(s, out, cyc, c0, c1, t);
+}
+
+__global__ __launch_bounds__(64) void seq_fdpp(const double* win, const double* dx0, double* out, long long* cyc) {
+  extern __shared__ double s[];
+  const int t = threadIdx.x, i = t < NX ? t : NX - 1;
+  load(s, win, dx0, t);
+  double dn = s[N * W + (t < NX ? t : 0)];   // lane q holds component q (lanes 0..5 of row 0)
+  double a[NX], c = s[i];
+  _Pragma("unroll") for (int q = 0; q < NX; ++q) a[q] = s[NX + i * NX + q];
+  const long long c0 = clock64();
+  for (int k = 0; k < N; ++k) {
+    const int kn = k + 1 < N ? k + 1 : k;
+    double an[NX], cn = s[kn * W + i];
+    _Pragma("unroll") for (int q = 0; q < NX; ++q) an[q] = s[kn * W + NX + i * NX + q];
+    double p0 = c, p1 = 0.0;
+    fmac_bc<0, true>(p0, a[0], dn);
+    fmac_bc<1, false>(p1, a[1], dn);
+    fmac_bc<2, false>(p0, a[2], dn);
+    fmac_bc<3, false>(p1, a[3], dn);
+    fmac_bc<4, false>(p0, a[4], dn);
+    fmac_bc<5, false>(p1, a[5], dn);
+    dn = p0 + p1;
+    if (t < NX) s[N * W + (k + 1) * NX + t] = dn;
     _Pragma("unroll") for (int q = 0; q < NX; ++q) a[q] = an[q];
     c = cn;
   }
@@ -225,6 +295,8 @@ int main() {
   struct K { const char* name; kern_t f; int chain; } ks[] = {
       {"seq_rl (product form)", seq_rl, N},
       {"seq_dpp", seq_dpp, N},
+      {"seq_mov64", seq_mov64, N},
+      {"seq_fdpp", seq_fdpp, N},
       {"seq_red", seq_red, N},
       {"part<2>", part<2>, 2 * ((N + 1) / 2) + 2},
       {"part<4>", part<4>, 2 * ((N + 3) / 4) + 4}};
