@@ -504,7 +504,7 @@ struct Coop {
       d[2 * c + 1] = v.y;
     }
   }
-  // z, dz, lambda_l, lambda_u of a stage: the contiguous range [OZ, OE)
+  // z, dz, lambda_l, lambda_u of a stage: the contiguous range [OZ, OZ + 4 NZ)
   static constexpr int NIP = (4 * NZ + 1) / 2;
   struct IP { double v[2 * NIP]; };
   __device__ __forceinline__ void ld_ip(int k, IP& r) const { ldr<OZ, NIP>(k, r.v); }
