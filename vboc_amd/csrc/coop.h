@@ -69,10 +69,15 @@ struct WaveLayout {
   static constexpr int OA = 0, OB = OA + NX * NX, P0 = OB + NX * NU, OE = IN_FIRST ? P0 : P0 + 4 * NZ, OD = OE + NX,
                        ODA = OD + NZ, OZ = IN_FIRST ? ODA + NZ : P0, ODZ = OZ + NZ, OQL = ODZ + NZ, OQU = OQL + NZ,
                        OK = P0 + 6 * NZ + NX, OKF = OK + NU * NX,
-                       OLR = OKF + NU, OM = OLR + NU * NU, OY = OM + NU * NQ, OPE = OY + NU * NQ, OC = OPE + NX,
+                       OLR = IN_FIRST ? OKF + NU + NU * NQ : OKF + NU, OM = IN_FIRST ? OKF + NU : OLR + NU * NU,
+                       OY = OKF + NU + NU * NU + NU * NQ, OPE = OY + NU * NQ, OC = OPE + NX,
                        OACL = OC + NX, OX = OACL + NX * NX, OU = OX + NX, OPI = OU + NU, OLL = OPI + NX,
                        OLU = OLL + NZ, OWPI = OLU + NZ, REC = rec_up(OWPI + NX);
   static_assert((IN_FIRST ? OQU : ODA) + NZ == OK, "the fields before K are A, B, e, D, DA, z, dz, lambda_l, lambda_u");
+  // IN_FIRST also puts M before chol(Ru): the forward sweep's constant pass reads [k_f, M] and the vector pass's k_f
+  // pass [chol(Ru), Y], each one contiguous range without the other's field
+  static_assert(IN_FIRST ? (OM == OKF + NU && OLR == OM + NU * NQ && OY == OLR + NU * NU)
+                         : (OLR == OKF + NU && OM == OLR + NU * NU && OY == OM + NU * NQ), "K, k_f, M / chol(Ru), Y");
   // OC: per-pass constant of the vector / forward recursion; OACL: closed-loop A + B K (row-major)
   // ring windows [lo, lo + W): factor [0, OC) (writes back [OK, OC)), or with FAC1 its inputs [0, W_FIN); vector pass
   // [OPE, OX); forward sweep [OC, OX); costate [0, W_COS): A (and B) to the end of lambda_u
@@ -508,6 +513,16 @@ struct Coop {
   static constexpr int NIP = (4 * NZ + 1) / 2;
   struct IP { double v[2 * NIP]; };
   __device__ __forceinline__ void ld_ip(int k, IP& r) const { ldr<OZ, NIP>(k, r.v); }
+  // a part [LO, LO + CNT) of the D / DA slots in registers: element i is v[OFF + i].  The pendulum chains (IN_FIRST)
+  // load its 16-B aligned cover only; the arm loads both slots [OD, OD + 2 NZ), as before round 6 (same k_wave<4> code)
+  template <int LO, int CNT, bool WIDE = !L::IN_FIRST>
+  struct Cov {
+    static_assert(LO >= OD && LO + CNT <= OD + 2 * NZ, "a part of the D / DA slots");
+    static constexpr int B = WIDE ? OD : (LO & ~1), OFF = LO - B, C = WIDE ? (2 * NZ + 1) / 2 : (OFF + CNT + 1) / 2;
+    double v[2 * C];
+  };
+  template <int LO, int CNT>
+  __device__ __forceinline__ void ldc(int k, Cov<LO, CNT>& c) const { ldr<Cov<LO, CNT>::B, Cov<LO, CNT>::C>(k, c.v); }
 
   struct CS { double tl, tu, itl, itu, ql, qu, dz; bool bx; };
   __device__ __forceinline__ CS comp_r(const IP& r, int k, int i) const {
@@ -1003,9 +1018,9 @@ struct Coop {
     fresh();
     for (int k = t; k <= N; k += 64) {
       IP r;
-      double da[2 * ((2 * NZ + 1) / 2)];
+      Cov<ODA, NZ> da;   // the affine direction (D is this pass's output)
       ld_ip(k, r);
-      ldr<OD, (2 * NZ + 1) / 2>(k, da);
+      ldc(k, da);
       __builtin_amdgcn_sched_barrier(0);
       gdouble* rec = &g[(long long)k * REC];
       double gv[NZ];
@@ -1014,7 +1029,7 @@ struct Coop {
         double gg = o.lm * c.dz + cgrad(k, i);
         if (c.bx) {
           double rl, ru;
-          corr_rhs(c, da[NZ + i], smu, rl, ru);
+          corr_rhs(c, da.v[da.OFF + i], smu, rl, ru);
           gg += -c.ql - rl * c.itl + c.qu + ru * c.itu;
         }
         rec[OD + i] = gg;
@@ -1454,27 +1469,28 @@ struct Coop {
     }
   }
   // PRE == false: the constants c' are already in OC (CCORR: prep_corr formed them)
-  template <bool PRE = true>
-  __device__ __forceinline__ bool vec(int OG, double (&w0)[M0], double (&nun)[NQ]) {
+  template <int OG, bool PRE = true>
+  __device__ __forceinline__ bool vec(double (&w0)[M0], double (&nun)[NQ]) {
     fresh();
     // p_k = c'_k + A_cl,k' p_{k+1},  c'_k = g_x + K'g_u + A_cl' PE_k  (lane i: row i of p);
     // v_k = PE_k + p_{k+1} is kept for k_f.  c' is formed stage-parallel first (-> OC).
     SPROF_DECL(2)
     if constexpr (PRE) {
-      constexpr int NZH = (2 * NZ + 1) / 2, NKK = (NU * NX) / 2;
+      constexpr int NKK = (NU * NX) / 2;
       for (int k = 1 + t; k < N; k += 64) {
-        double gg[2 * NZH], kk[2 * NKK], ac[NX * NX], pe[NX];
-        ldr<OD, NZH>(k, gg);
+        Cov<OG, NZ> gg;   // the gradient slot only
+        double kk[2 * NKK], ac[NX * NX], pe[NX];
+        ldc(k, gg);
         ldr<OK, NKK>(k, kk);
         ldr<OACL, NX * NX / 2>(k, ac);
         ldr<OPE, NX / 2>(k, pe);
         __builtin_amdgcn_sched_barrier(0);
-        const int go = OG - OD;
+        constexpr int go = Cov<OG, NZ>::OFF;
         gdbl2* dst = (gdbl2*)(g + (long long)k * REC + OC);
         double cv[NX];
         UNR for (int i = 0; i < NX; ++i) {
-          double c = gg[go + i];
-          UNR for (int q = 0; q < NU; ++q) c += kk[q * NX + i] * gg[go + NX + q];
+          double c = gg.v[go + i];
+          UNR for (int q = 0; q < NU; ++q) c += kk[q * NX + i] * gg.v[go + NX + q];
           UNR for (int q = 0; q < NX; ++q) c += ac[q * NX + i] * pe[q];
           cv[i] = c;
         }
@@ -1583,18 +1599,18 @@ struct Coop {
     // k_f = -Ru^-1 (g_u + B'v) per stage, lin = sum Y'k_f  (stage-parallel)
     double lin[NQ];
     UNR for (int j = 0; j < NQ; ++j) lin[j] = 0.0;
-    constexpr int NBB = (NX * NU + 1) / 2, NLY = (OPE - (OLR & ~1) + 1) / 2;   // B; chol(Ru), M, Y
+    constexpr int NBB = (NX * NU + 1) / 2, NLY = (OPE - (OLR & ~1) + 1) / 2;   // B; chol(Ru) (.. M, with the old order), Y
     for (int k = 1 + t; k < N; k += 64) {
-      double bb[2 * NBB], ly[2 * NLY], gg[2 * ((2 * NZ + 1) / 2)];
+      double bb[2 * NBB], ly[2 * NLY];
+      Cov<OG + NX, NU> gg;   // g_u of the gradient slot
       ldr<OB, NBB>(k, bb);
       ldr<(OLR & ~1), NLY>(k, ly);
-      ldr<OD, (2 * NZ + 1) / 2>(k, gg);
+      ldc(k, gg);
       __builtin_amdgcn_sched_barrier(0);
       constexpr int LR_ = OLR - (OLR & ~1), Y_ = OY - (OLR & ~1);
-      const int go = OG - OD;
       double r[NU], Lm[NU * NU];
       UNR for (int a = 0; a < NU; ++a) {
-        double x = (go == 0) ? gg[NX + a] : gg[NZ + NX + a];
+        double x = gg.v[gg.OFF + a];
         UNR for (int i = 0; i < NX; ++i) x += bb[i * NU + a] * s[L::XS + k * NX + i];
         r[a] = x;
       }
@@ -1683,7 +1699,7 @@ struct Coop {
     // dx_{k+1} = c_k + A_cl,k dx_k,  c_k = rs e_k + B_k (k_f - M_k nu)  (lane i: row i); c is formed
     // stage-parallel first (-> OC)
     {
-      constexpr int NBB = (NX * NU + 1) / 2, NFM = (OY - OKF + 1) / 2;   // B; k_f, chol(Ru), M
+      constexpr int NBB = (NX * NU + 1) / 2, NFM = (OM + NU * NQ - OKF + 1) / 2;   // B; k_f .. the end of M
       for (int k = 1 + t; k < N; k += 64) {
         double e[NX], bb[2 * NBB], fm[2 * NFM];
         ldr<OE, NX / 2>(k, e);
@@ -1804,15 +1820,16 @@ struct Coop {
     // controls of the middle stages, then the step-length tests (stage-parallel)
     typename Lane<NQ>::MinRatio mr{1.0, CORR ? o.tau : 1.0};
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
-    // K, k_f, chol(Ru), M: the range [OK, OY); KFM: K and k_f - M nu, the range [OK, OLR)
-    constexpr int NKM = KFM ? (OLR - OK + 1) / 2 : (OY - OK + 1) / 2;
+    // K, k_f, chol(Ru), M: the range [OK, OY); KFM: K and k_f - M nu, the range [OK, OKF + NU)
+    constexpr int NKM = KFM ? (OKF + NU - OK + 1) / 2 : (OY - OK + 1) / 2;
     for (int k = t; k <= N; k += 64) {
       IP r;
-      double km[2 * NKM], da[2 * ((2 * NZ + 1) / 2)];
+      double km[2 * NKM];
+      Cov<ODA, NZ> da;   // the affine direction
       const int kk = (k > 0 && k < N) ? k : 1 < N ? 1 : 0;
       ld_ip(k, r);
       ldr<OK, NKM>(kk, km);
-      if (CORR) ldr<OD, (2 * NZ + 1) / 2>(k, da);
+      if (CORR) ldc(k, da);
       __builtin_amdgcn_sched_barrier(0);
       W6(0)
       gdouble* rec = &g[(long long)k * REC];
@@ -1847,7 +1864,7 @@ struct Coop {
           a2 += d[i] * dll - d[i] * dlu;
         } else {
           double rl, ru;
-          corr_rhs(c, da[NZ + i], smu, rl, ru);
+          corr_rhs(c, da.v[da.OFF + i], smu, rl, ru);
           dll = (rl - c.ql * d[i]) * c.itl;
           dlu = (ru + c.qu * d[i]) * c.itu;
         }
@@ -2172,7 +2189,7 @@ struct Coop {
         if constexpr (!ACL_FUSED) VREP(3, acl_pass());
         CPROF(3)
         bool okv;
-        VREP(4, okv = vec(ODA, w0, nun));
+        VREP(4, okv = vec<ODA>(w0, nun));
         CPROF(4)
         if (!(okf && okv)) { qst = -1; break; }
         double aa, c0, c1, c2;
@@ -2185,7 +2202,7 @@ struct Coop {
         VREP(6, prep_corr(smu));
         CPROF(2)
         bool okc;
-        VREP(7, okc = vec<!CCORR>(OD, w0, nun));
+        VREP(7, (okc = vec<OD, !CCORR>(w0, nun)));
         if (!okc) { qst = -1; break; }
         CPROF(4)
         double amax;
