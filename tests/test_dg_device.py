@@ -193,12 +193,14 @@ def test_device_loop_restart_branches_match_host_driver(nq):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("opts", [{}, {"dg_spec_window": 2}, {"dg_spec_first": 1}, {"dg_spec_crit": 1},
-                                  {"dg_park": 0}], ids=["default", "window2", "spec_first", "spec_crit", "no_park"])
+                                  {"dg_park": 0}, {"dg_spec_pause": 20}],
+                         ids=["default", "window2", "spec_first", "spec_crit", "no_park", "early_events"])
 def test_speculative_restarts_change_nothing(opts):
     """Speculative restarts (dg_speculate) only run later attempts early: with and without them the
     device loop returns the same rows, counts and per-problem statistics (timing and speculation fields aside),
     here on a batch where the failure injection makes many chains fail - also with the eager window, with restart
-    jobs before parked resumes, and without parking."""
+    jobs before parked resumes, without parking, and with early events (a solve still iterating after 20 SQP
+    iterations publishes its chain's later attempts before it fails: 512 problems drain the queue at once)."""
     import torch
     from vboc_amd import lib
     ids = torch.arange(7000, 7000 + 512, dtype=torch.int64, device="cuda:0")

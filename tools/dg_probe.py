@@ -41,6 +41,8 @@ def main():
                     help="dg_spec_first option values to run (1: restart jobs before parked resumes)")
     ap.add_argument("--spec-crit", type=int, nargs="*", default=[0],
                     help="dg_spec_crit option values to run (1: the critical-path rule for restart jobs)")
+    ap.add_argument("--spec-pause", type=int, nargs="*", default=[0],
+                    help="dg_spec_pause option values to run (> 0: early events after that many SQP iterations)")
     ap.add_argument("--park-window", type=int, nargs="*", default=[0],
                     help="dg_park_window option values to run (0: the product default)")
     ap.add_argument("--save", default=None, help="write the per-problem stats (lib.DG_STATS) of each launch to "
@@ -48,8 +50,11 @@ def main():
     a = ap.parse_args()
     s = lib.Solver(a.nq, 120, device=0)
     ids = torch.arange(a.first, a.first + a.B, dtype=torch.int64, device="cuda:0")
-    for g, pk, wn, sf, sc, pw in [(g, pk, wn, sf, sc, pw) for pw in a.park_window for sc in a.spec_crit
-                                  for sf in a.spec_first for wn in a.window for pk in a.park for g in a.groups]:
+    for g, pk, wn, sf, sc, pw, sp in [(g, pk, wn, sf, sc, pw, sp) for sp in a.spec_pause for pw in a.park_window
+                                      for sc in a.spec_crit for sf in a.spec_first for wn in a.window for pk in a.park
+                                      for g in a.groups]:
+        if any(a.spec_pause):   # the option exists from round 6's library on
+            s.set_option("dg_spec_pause", sp)
         s.set_option("dg_park_window", pw)
         s.set_option("dg_spec_crit", sc)
         s.set_option("dg_spec_first", sf)
@@ -74,7 +79,7 @@ def main():
         h.update(out["row_cnt"].cpu().numpy().tobytes())
         h.update(st[:, [0, 1, 2, 3, 4, 7, 8]].tobytes())
         rec = {"lib": os.path.basename(os.environ.get("VBOC_LIB") or "libvboc_amd.so"), "nq": a.nq, "B": a.B,
-               "groups": int(s.get_option("last_groups")), "park": pk, "window": wn, "spec_first": sf, "spec_crit": sc, "park_window": pw, "kernel_ms": round(ms, 1), "wall_s": round(wall, 2),
+               "groups": int(s.get_option("last_groups")), "park": pk, "window": wn, "spec_first": sf, "spec_crit": sc, "park_window": pw, "spec_pause": sp, "kernel_ms": round(ms, 1), "wall_s": round(wall, 2),
                "solves": int(st[:, 0].sum()), "solves_per_s": round(float(st[:, 0].sum()) / (ms / 1e3), 1),
                "bulk_solves_per_s": round(bulk, 1) if bulk else None,
                "drained_ms": round(drained / lib.DG_CLOCK_HZ * 1e3, 1),

@@ -353,6 +353,7 @@ struct Coop {
 
   unsigned lds0;    // LDS byte address of s[0] (wave-uniform), for the LDS-DMA's M0
   gdouble* gh = nullptr;   // HC: this workgroup's path-constraint rows, FHC doubles per stage
+  int pause_at = -1;       // run<true>: return -2 at the top of SQP iteration pause_at (k_dg's early events)
 
   __device__ Coop(double* s_, gdouble* g_, const Work& w_, const Opts& o_, int t_)
       : s(s_), g(g_), w(w_), o(o_), t(t_), N(0),
@@ -2158,6 +2159,9 @@ struct Coop {
   }
 
   // the remaining SQP of the loaded problem, to termination; returns the ACADOS status
+  // PAUSE: stop with status -2 before SQP iteration pause_at; a second call resumes (every SQP iteration starts from
+  // the stage records and LDS alone, as the cooperative tail's resumption does)
+  template <bool PAUSE = false>
   __device__ __forceinline__ int run(int& it, int& qit) {
     for (int e = t; e < 16; e += 64) s[L::ZERO + e] = 0.0;
     __syncthreads();
@@ -2166,6 +2170,9 @@ struct Coop {
     const int it0 = it;
     int qtot = 0;
     for (;;) {
+      if constexpr (PAUSE) {
+        if (it == pause_at) { status = -2; break; }
+      }
       double rstat, req, rineq, rcomp;
       linearize(rstat, req, rineq, rcomp);
       CPROF(0)

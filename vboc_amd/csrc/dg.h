@@ -64,6 +64,8 @@ struct DgJobs {
   // speculative restarts (see "Speculative restarts" below); spec_events == 0 switches them off
   int spec_events, spec_stride;   // events in the pool, doubles per event
   int spec_early;                 // once at most this many problems are left unclaimed, queued restart jobs go first
+  int spec_pause;                 // > 0: early events - once the new problems have run out, a horizon-extension solve
+                                  // still iterating after this many SQP iterations publishes its chain's later attempts
   int spec_first;                 // 1: once the new problems run out, queued restart jobs go before parked resumes
   double* spec;                   // [spec_events][spec_stride]: snapshot header, then DG_SPEC_JOBS results
   int* spec_claim;                // [spec_events][DG_SPEC_JOBS + 1]: 0 free, 1 claimed
@@ -565,6 +567,17 @@ struct Dg {
     if (t == 0) r = atomicCAS(&J.spec_claim[ev * (DG_SPEC_JOBS + 1) + j], 0, 1) == 0 ? 1 : 0;
     return __builtin_amdgcn_readfirstlane(__shfl(r, 0)) != 0;
   }
+  // early event (spec_pause): the owner's horizon-extension attempt att = ext + 1 has run spec_pause SQP iterations
+  // without converging.  Its later attempts depend only on the problem's random stream, so they are published now, as
+  // its failure would publish them: spawn(att, N) with the running attempt's own restart state, job j = attempt att + j
+  // (spec_prepare perturbs j times from it, as the owner's perturb() at the failure does once).  A success cancels the
+  // event; a failure walks the chain from job 1.
+  __device__ __forceinline__ bool pause_ok() const { return s->phase == HEXT && s->spec_ev < 0 && s->ext + 1 < 10; }
+  __device__ __forceinline__ void early(int job_) {
+    job = job_;
+    pid = J.ids[job];
+    spawn(s->ext + 1, nreq());
+  }
   __device__ __forceinline__ void cancel_event() {
     const int ev = s->spec_ev;
     if (ev >= 0 && t == 0) __hip_atomic_store(&J.spec_cancel[ev], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -992,6 +1005,16 @@ __device__ __forceinline__ void dg_skip(const DgJobs* J, const Inputs* in, int w
   D.skip(job);
 }
 template <int NQ>
+__device__ __forceinline__ bool dg_pause_ok(const DgJobs* J, const Inputs* in, int wg, int t) {
+  Dg<NQ> D(*J, *in, wg, t);
+  return D.pause_ok();
+}
+template <int NQ>
+__device__ __forceinline__ void dg_early(const DgJobs* J, const Inputs* in, int wg, int t, int job) {
+  Dg<NQ> D(*J, *in, wg, t);
+  D.early(job);
+}
+template <int NQ>
 __device__ __forceinline__ void dg_spec_prepare(const DgJobs* J, const Inputs* in, int wg, int t, int ev, int j) {
   Dg<NQ> D(*J, *in, wg, t);
   D.spec_prepare(ev, j);
@@ -1227,7 +1250,23 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
           }
         } else {
           C.from_inputs(in, wg);
-          const int status = C.run(it, qit);
+          // early events (spec_pause): a horizon-extension solve pauses after spec_pause SQP iterations and then every
+          // 50; the event is published at the first pause after the new problems have run out (idle waves take its
+          // jobs only then, and the event pool is not spent on the bulk's long solves)
+          C.pause_at = (mode == 1 && spec && J->spec_pause > 0 && dg_pause_ok<NQ>(J, inp, wg, t)) ? J->spec_pause : -1;
+          int status;
+          for (;;) {
+            status = C.template run<true>(it, qit);
+            if (status != -2) break;
+            int drained = 0;
+            if (t == 0) drained = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)count;
+            if (dg_bcast(drained)) {
+              dg_early<NQ>(J, inp, wg, t, idx);
+              C.pause_at = -1;
+            } else {
+              C.pause_at = it + 50;
+            }
+          }
           C.store(in, wg, status, it, qit);
         }
         __syncthreads();

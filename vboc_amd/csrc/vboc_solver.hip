@@ -1512,6 +1512,7 @@ struct vboc_solver {
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
   int dg_spec_early = 0;            // restart jobs before new problems once this few problems are left (0: only after)
+  int dg_spec_pause = 300;          // early events after this many SQP iterations of a tail solve (0: at failures only)
   // restart jobs before parked resumes once the new problems run out (dg.h): 0 off, 1 on, 2 (default) on for a short
   // launch - fewer than 128 problems per resident wave - where the restart chains found late set the launch's end
   // (round 4, same box: the 100k warmup launch -5.2 %, the 400k launch +1.4 % with it on)
@@ -1902,6 +1903,7 @@ int vboc_set_option(vboc_handle h, const char* f, double v) {
   else if (s == "dg_fail_mod") h->dg_fail_mod = (int)v;
   else if (s == "dg_speculate") h->dg_speculate = v != 0.0;
   else if (s == "dg_spec_early") h->dg_spec_early = v > 0.0 ? (int)v : 0;
+  else if (s == "dg_spec_pause") h->dg_spec_pause = v > 0.0 ? (int)v : 0;
   else if (s == "dg_spec_first") h->dg_spec_first = v >= 2.0 ? 2 : (v != 0.0 ? 1 : 0);
   else if (s == "dg_spec_crit") h->dg_spec_crit = v != 0.0;
   else if (s == "dg_spec_window") h->dg_spec_window = v > 0.0 ? (v < 9.0 ? (int)v : 9) : 0;
@@ -1945,6 +1947,7 @@ int vboc_get_option(vboc_handle h, const char* f, double* v) {
   else if (s == "wave_all") *v = h->wave_all ? 1.0 : 0.0;
   else if (s == "dg_speculate") *v = h->dg_speculate ? 1.0 : 0.0;
   else if (s == "dg_spec_early") *v = (double)h->dg_spec_early;
+  else if (s == "dg_spec_pause") *v = (double)h->dg_spec_pause;
   else if (s == "dg_spec_first") *v = (double)h->dg_spec_first;
   else if (s == "dg_spec_crit") *v = h->dg_spec_crit ? 1.0 : 0.0;
   else if (s == "dg_spec_window") *v = (double)h->dg_spec_window;
@@ -2531,7 +2534,7 @@ static int dg_prepare(vboc_handle h, vboc_dg_batch_t* b, int* done_flag, const i
   J.spec_ev_next = h->head + 6; J.spec_q_tail = h->head + 7; J.spec_q_head = h->head + 8;
   J.spec_count = (unsigned long long*)(h->head + 10);
   // speculative restarts: one event per failed horizon-extension chain, at most min(B, 8192) per launch
-  J.spec_events = 0; J.spec_stride = 0; J.spec = nullptr; J.spec_early = h->dg_spec_early; J.spec_first = (h->dg_spec_first == 1 || (h->dg_spec_first == 2 && (long long)b->B < 128 * groups)) ? 1 : 0;
+  J.spec_events = 0; J.spec_stride = 0; J.spec = nullptr; J.spec_early = h->dg_spec_early; J.spec_pause = h->dg_spec_pause; J.spec_first = (h->dg_spec_first == 1 || (h->dg_spec_first == 2 && (long long)b->B < 128 * groups)) ? 1 : 0;
   J.spec_claim = J.spec_done = J.spec_cancel = J.spec_q = J.spec_eq = nullptr;
   J.spec_window = 0; J.spec_eq_tail = h->head + 20; J.spec_eq_head = h->head + 21;
   J.spec_crit = 0; J.t_launch = (unsigned long long*)(h->head + 22);   // [22..23]
