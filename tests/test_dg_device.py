@@ -199,14 +199,15 @@ def test_speculative_restarts_change_nothing(opts):
     """Speculative restarts (dg_speculate) only run later attempts early: with and without them the
     device loop returns the same rows, counts and per-problem statistics (timing and speculation fields aside),
     here on a batch where the failure injection makes many chains fail - also with the eager window, with restart
-    jobs before parked resumes, without parking, and with early events (a solve still iterating after 20 SQP
+    jobs before parked resumes, without parking, and with early events on the double (a solve still iterating after 20 SQP
     iterations publishes its chain's later attempts before it fails: 512 problems drain the queue at once)."""
     import torch
     from vboc_amd import lib
     ids = torch.arange(7000, 7000 + 512, dtype=torch.int64, device="cuda:0")
+    nq = 2 if "dg_spec_pause" in opts else 3   # early events are built into the double's (and single's) k_dg
     outs = []
     for spec in (1, 0):
-        s = lib.Solver(3, 120)
+        s = lib.Solver(nq, 120)
         s.set_option("dg_fail_mod", 3)
         s.set_option("dg_speculate", spec)
         if spec:

@@ -64,8 +64,6 @@ struct DgJobs {
   // speculative restarts (see "Speculative restarts" below); spec_events == 0 switches them off
   int spec_events, spec_stride;   // events in the pool, doubles per event
   int spec_early;                 // once at most this many problems are left unclaimed, queued restart jobs go first
-  int spec_pause;                 // > 0: early events - once the new problems have run out, a horizon-extension solve
-                                  // still iterating after this many SQP iterations publishes its chain's later attempts
   int spec_first;                 // 1: once the new problems run out, queued restart jobs go before parked resumes
   double* spec;                   // [spec_events][spec_stride]: snapshot header, then DG_SPEC_JOBS results
   int* spec_claim;                // [spec_events][DG_SPEC_JOBS + 1]: 0 free, 1 claimed
@@ -97,6 +95,10 @@ struct DgJobs {
   int round_n;
   unsigned* park_tail;            // [2] entries pushed
   unsigned* park_head;            // [2] entries taken
+  // early events (the single and double pendulum's k_dg): > 0 - once the new problems have run out, a horizon-extension
+  // solve still iterating after this many SQP iterations publishes its chain's later attempts (last, so that the other
+  // fields keep their offsets in the triple's kernel)
+  int spec_pause;
 };
 
 // a horizon extension gives up after 10 solves (VBOC/triplependulum_vboc.py:107): a failure at attempt a
@@ -1253,19 +1255,25 @@ void k_dg(Work w, Opts o, Inputs in, const Inputs* inp, const DgJobs* J, WaveJob
           // early events (spec_pause): a horizon-extension solve pauses after spec_pause SQP iterations and then every
           // 50; the event is published at the first pause after the new problems have run out (idle waves take its
           // jobs only then, and the event pool is not spent on the bulk's long solves)
-          C.pause_at = (mode == 1 && spec && J->spec_pause > 0 && dg_pause_ok<NQ>(J, inp, wg, t)) ? J->spec_pause : -1;
+          // (the single and double pendulum only: the triple's chains gained nothing from it, DESIGN.md section 14, and
+          // its kernel keeps the code of the validated round-6 build)
           int status;
-          for (;;) {
-            status = C.template run<true>(it, qit);
-            if (status != -2) break;
-            int drained = 0;
-            if (t == 0) drained = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)count;
-            if (dg_bcast(drained)) {
-              dg_early<NQ>(J, inp, wg, t, idx);
-              C.pause_at = -1;
-            } else {
-              C.pause_at = it + 50;
+          if constexpr (NQ <= 2) {
+            C.pause_at = (mode == 1 && spec && J->spec_pause > 0 && dg_pause_ok<NQ>(J, inp, wg, t)) ? J->spec_pause : -1;
+            for (;;) {
+              status = C.template run<true>(it, qit);
+              if (status != -2) break;
+              int drained = 0;
+              if (t == 0) drained = __hip_atomic_load(jb.next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)count;
+              if (dg_bcast(drained)) {
+                dg_early<NQ>(J, inp, wg, t, idx);
+                C.pause_at = -1;
+              } else {
+                C.pause_at = it + 50;
+              }
             }
+          } else {
+            status = C.run(it, qit);
           }
           C.store(in, wg, status, it, qit);
         }

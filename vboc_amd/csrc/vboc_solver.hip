@@ -1512,7 +1512,8 @@ struct vboc_solver {
   int dg_fail_mod = 0;              // test-only failure injection of the data-generation loop
   bool dg_speculate = true;         // speculative restarts of failed horizon-extension solves (dg.h)
   int dg_spec_early = 0;            // restart jobs before new problems once this few problems are left (0: only after)
-  int dg_spec_pause = 300;          // early events after this many SQP iterations of a tail solve (0: at failures only)
+  int dg_spec_pause = 300;          // early events after this many SQP iterations of a tail solve (0: at failures only;
+                                    // the single and double pendulum's k_dg)
   // restart jobs before parked resumes once the new problems run out (dg.h): 0 off, 1 on, 2 (default) on for a short
   // launch - fewer than 128 problems per resident wave - where the restart chains found late set the launch's end
   // (round 4, same box: the 100k warmup launch -5.2 %, the 400k launch +1.4 % with it on)
